@@ -1,0 +1,66 @@
+"""In-tree build of libccsc.so for gfx950 (hipcc, parallel object compiles).
+
+Usage:  python -m ccsc_code_iccv2017_amd.build [--force]
+The shared library lands next to this file so it travels with the repo
+snapshot to the GPU box (it is git-ignored, not gpurun-ignored).
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+CSRC = PKG / "csrc"
+OBJ = PKG.parent / "build" / "obj"
+LIB = PKG / "libccsc.so"
+ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
+HIPCC = str(ROCM / "bin" / "hipcc")
+ARCH = "gfx950"
+CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function"]
+
+
+def _sources():
+    return sorted(list(CSRC.glob("*.hip")) + list(CSRC.glob("*.cpp")))
+
+
+def _deps():
+    return sorted(list(CSRC.glob("*.hpp")) + [PKG.parent / "include" / "ccsc.h"])
+
+
+def _needs(target: Path, inputs) -> bool:
+    if not target.exists():
+        return True
+    t = target.stat().st_mtime
+    return any(p.stat().st_mtime > t for p in inputs)
+
+
+def _compile(src: Path, force: bool) -> Path:
+    obj = OBJ / (src.name + ".o")
+    if force or _needs(obj, [src] + _deps()):
+        cmd = [HIPCC] + CFLAGS + ["-c", str(src), "-o", str(obj)]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed for {src.name}:\n{r.stderr[-6000:]}")
+    return obj
+
+
+def build(force: bool = False, jobs: int | None = None) -> Path:
+    OBJ.mkdir(parents=True, exist_ok=True)
+    srcs = _sources()
+    jobs = jobs or min(len(srcs), max(1, min(8, os.cpu_count() or 1)))
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        objs = list(ex.map(lambda s: _compile(s, force), srcs))
+    if force or _needs(LIB, objs):
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-o", str(LIB)] + [str(o) for o in objs]
+        cmd += [f"-L{ROCM / 'lib'}", "-lrccl", f"-Wl,-rpath,{ROCM / 'lib'}"]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stderr[-6000:]}")
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv))

@@ -1,0 +1,60 @@
+// Common device/host helpers for libccsc (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstddef>
+
+namespace ccsc {
+
+template <typename T> struct cpx { T x, y; };
+template <typename T> struct vec2_t;
+template <> struct vec2_t<double> { using type = double2; };
+template <> struct vec2_t<float> { using type = float2; };
+
+template <typename T>
+__host__ __device__ __forceinline__ cpx<T> cmul(cpx<T> a, cpx<T> b) {
+  return {a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x};
+}
+// conj(a) * b
+template <typename T>
+__host__ __device__ __forceinline__ cpx<T> cmulc(cpx<T> a, cpx<T> b) {
+  return {a.x * b.x + a.y * b.y, a.x * b.y - a.y * b.x};
+}
+template <typename T>
+__host__ __device__ __forceinline__ cpx<T> cadd(cpx<T> a, cpx<T> b) { return {a.x + b.x, a.y + b.y}; }
+template <typename T>
+__host__ __device__ __forceinline__ cpx<T> csub(cpx<T> a, cpx<T> b) { return {a.x - b.x, a.y - b.y}; }
+template <typename T>
+__host__ __device__ __forceinline__ cpx<T> cscale(cpx<T> a, T s) { return {a.x * s, a.y * s}; }
+template <typename T>
+__host__ __device__ __forceinline__ T cabs2(cpx<T> a) { return a.x * a.x + a.y * a.y; }
+
+// Block size of every slice-resident kernel (8 waves of 64 lanes).
+constexpr int kNT = 512;
+
+// Wave-level sum (64 lanes) via shuffles.
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Block-level sum of one value per thread; result valid in every thread.
+// `scratch` must hold kNT/64 elements and not alias live data.
+template <typename T>
+__device__ __forceinline__ T block_sum(T v, T* scratch) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) scratch[w] = v;
+  __syncthreads();
+  T s = 0;
+#pragma unroll
+  for (int i = 0; i < kNT / 64; ++i) s += scratch[i];
+  __syncthreads();
+  return s;
+}
+
+}  // namespace ccsc

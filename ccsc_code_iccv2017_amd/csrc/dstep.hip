@@ -1,0 +1,254 @@
+// D-step per-frequency solves (gfx950).
+//
+// Reference: precompute_H_hat_D (dP:221-237) forms, for every frequency f of
+// a block, Sinv_f = 1/rho*I - 1/rho*A'*pinv(rho*I + A*A')*A  (A = ni x K code
+// spectra) == (A'A + rho I)^-1, and solve_conv_term_D (dP:252-276) applies
+// x_f = Sinv_f (A'b_f + rho c_f) once per d-iteration.
+//
+// Here the precompute builds G_f = A'A + rho I and h_f = A'b_f in fp64 and
+// stores the Cholesky factor L_f (packed lower, column-major, K(K+1)/2
+// complex); every d-iteration streams L_f once and does the two triangular
+// solves.  Only the half spectrum is solved: for real data S_{-f} = conj(S_f).
+#include "kernels.hpp"
+
+namespace ccsc {
+
+constexpr int kGramNT = 256;
+constexpr int kGramTS = 5;   // register tile (rows x cols) of G per thread
+constexpr int kGramPC = 16;  // patches staged in LDS per chunk
+
+__device__ __forceinline__ int pk_off(int j, int K) { return j * K - (j * (j - 1)) / 2; }
+
+// one workgroup per frequency (XCD-aware: consecutive f share an XCD's L2)
+template <typename T>
+__global__ __launch_bounds__(kGramNT) void k_gram_chol(const cpx<T>* __restrict__ Zh,
+                                                       const cpx<T>* __restrict__ Bh,
+                                                       cpx<T>* __restrict__ L,
+                                                       cpx<T>* __restrict__ h, int F, int K,
+                                                       int ni, T rho) {
+  const int per = gridDim.x >> 3;
+  const int f = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
+  if (f >= F) return;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  cpx<T>* sG = reinterpret_cast<cpx<T>*>(smem);           // packed G, Kp entries
+  const int Kp = K * (K + 1) / 2;
+  cpx<T>* sA = sG;                                          // chunk [PC][K] (aliases sG)
+  cpx<T>* sB = sA + kGramPC * K;                            // [PC]
+  const int tid = threadIdx.x;
+  const int Kt = (K + kGramTS - 1) / kGramTS;
+  const int ntiles = Kt * (Kt + 1) / 2;
+  const bool act = tid < ntiles;
+  int I = 0, J = 0;
+  if (act) {
+    I = (int)((sqrt(8.0 * tid + 1.0) - 1.0) * 0.5);
+    while ((I + 1) * (I + 2) / 2 <= tid) ++I;
+    while (I * (I + 1) / 2 > tid) --I;
+    J = tid - I * (I + 1) / 2;
+  }
+  cpx<T> acc[kGramTS][kGramTS];
+#pragma unroll
+  for (int a = 0; a < kGramTS; ++a)
+#pragma unroll
+    for (int b = 0; b < kGramTS; ++b) acc[a][b] = {(T)0, (T)0};
+  cpx<T> hacc = {(T)0, (T)0};
+
+  for (int p0 = 0; p0 < ni; p0 += kGramPC) {
+    const int pc = min(kGramPC, ni - p0);
+    __syncthreads();
+    for (int idx = tid; idx < pc * K; idx += kGramNT) {
+      const int pp = idx / K, k = idx - pp * K;
+      sA[idx] = Zh[((int64_t)(p0 + pp) * K + k) * F + f];
+    }
+    if (tid < pc) sB[tid] = Bh[(int64_t)(p0 + tid) * F + f];
+    __syncthreads();
+    if (act) {
+      for (int pp = 0; pp < pc; ++pp) {
+        const cpx<T>* a = sA + pp * K;
+        cpx<T> ai[kGramTS], aj[kGramTS];
+#pragma unroll
+        for (int t = 0; t < kGramTS; ++t) {
+          const int ri = I * kGramTS + t, cj = J * kGramTS + t;
+          ai[t] = (ri < K) ? a[ri] : cpx<T>{(T)0, (T)0};
+          aj[t] = (cj < K) ? a[cj] : cpx<T>{(T)0, (T)0};
+        }
+#pragma unroll
+        for (int u = 0; u < kGramTS; ++u)
+#pragma unroll
+          for (int v = 0; v < kGramTS; ++v) acc[u][v] = cadd(acc[u][v], cmulc(ai[u], aj[v]));
+      }
+    }
+    if (tid < K)
+      for (int pp = 0; pp < pc; ++pp) hacc = cadd(hacc, cmulc(sA[pp * K + tid], sB[pp]));
+  }
+  __syncthreads();  // chunk buffer (aliasing sG) no longer read
+  if (act) {
+#pragma unroll
+    for (int u = 0; u < kGramTS; ++u)
+#pragma unroll
+      for (int v = 0; v < kGramTS; ++v) {
+        const int row = I * kGramTS + u, col = J * kGramTS + v;
+        if (row < K && col <= row) {
+          cpx<T> g = acc[u][v];
+          if (row == col) {
+            g.x += rho;
+            g.y = (T)0;
+          }
+          sG[pk_off(col, K) + row - col] = g;
+        }
+      }
+  }
+  if (tid < K) h[(int64_t)f * K + tid] = hacc;
+  __syncthreads();
+
+  // right-looking Cholesky in LDS: G = L L^H
+  const int a0 = tid & 63, c0 = tid >> 6;  // 64 x 4 thread grid over the trailing block
+  for (int j = 0; j < K; ++j) {
+    const int oj = pk_off(j, K);
+    const T djj = sqrt(sG[oj].x);
+    const T inv = (T)1 / djj;
+    for (int i = j + 1 + tid; i < K; i += kGramNT) sG[oj + i - j] = cscale(sG[oj + i - j], inv);
+    __syncthreads();
+    if (tid == 0) sG[oj] = {djj, (T)0};
+    const int m = K - j - 1;
+    for (int c = c0; c < m; c += 4) {
+      const int l = j + 1 + c;
+      const cpx<T> glj = sG[oj + l - j];
+      const int ol = pk_off(l, K);
+      const int start = c + ((a0 - (c & 63)) & 63);
+      for (int a = start; a < m; a += 64) {
+        const int i = j + 1 + a;
+        const cpx<T> gij = sG[oj + i - j];
+        // G[i][l] -= G[i][j] * conj(G[l][j])
+        cpx<T> t = sG[ol + i - l];
+        t.x -= gij.x * glj.x + gij.y * glj.y;
+        t.y -= gij.y * glj.x - gij.x * glj.y;
+        sG[ol + i - l] = t;
+      }
+    }
+    __syncthreads();
+  }
+  cpx<T>* Lf = L + (int64_t)f * Kp;
+  for (int q = tid; q < Kp; q += kGramNT) Lf[q] = sG[q];
+}
+
+template <typename T>
+hipError_t launch_gram_chol(const cpx<T>* Zh, const cpx<T>* Bh, cpx<T>* L, cpx<T>* h, int F,
+                            int K, int ni, T rho, hipStream_t st) {
+  const int Kt = (K + kGramTS - 1) / kGramTS;
+  if (Kt * (Kt + 1) / 2 > kGramNT) return hipErrorInvalidValue;
+  const int Kp = K * (K + 1) / 2;
+  size_t sm = (size_t)Kp * sizeof(cpx<T>);
+  const size_t sm2 = (size_t)(kGramPC * K + kGramPC) * sizeof(cpx<T>);
+  if (sm2 > sm) sm = sm2;
+  const int grid = ((F + 7) / 8) * 8;
+  hipLaunchKernelGGL(k_gram_chol<T>, dim3(grid), dim3(kGramNT), sm, st, Zh, Bh, L, h, F, K, ni,
+                     rho);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// d-solve: one wave per (block, f); rows of the K-vector are spread over the
+// 64 lanes (RPL rows per lane).  Forward solve column-oriented (axpy with the
+// contiguous packed column), backward solve as wave-reduced dot products.
+// ---------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ cpx<T> shfl_c(cpx<T> v, int src) {
+  return {__shfl(v.x, src, 64), __shfl(v.y, src, 64)};
+}
+
+template <typename T, int RPL>
+__global__ __launch_bounds__(256) void k_dsolve(const cpx<T>* __restrict__ L,
+                                                const cpx<T>* __restrict__ h,
+                                                const cpx<T>* __restrict__ Ch,
+                                                cpx<T>* __restrict__ Dh, int F, int K, T rho,
+                                                int fgroups) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int blk = blockIdx.x / fgroups;
+  const int f = (blockIdx.x - blk * fgroups) * 4 + wave;
+  if (f >= F) return;
+  const int Kp = K * (K + 1) / 2;
+  const cpx<T>* Lf = L + ((int64_t)blk * F + f) * Kp;
+  const cpx<T>* hf = h + ((int64_t)blk * F + f) * K;
+  const cpx<T>* Cb = Ch + (int64_t)blk * K * F;
+  cpx<T> x[RPL];
+#pragma unroll
+  for (int t = 0; t < RPL; ++t) {
+    const int i = lane + 64 * t;
+    if (i < K) {
+      const cpx<T> c = Cb[(int64_t)i * F + f];
+      const cpx<T> hh = hf[i];
+      x[t] = {hh.x + rho * c.x, hh.y + rho * c.y};
+    } else {
+      x[t] = {(T)0, (T)0};
+    }
+  }
+  // forward: L y = rhs
+  int off = 0;
+#pragma unroll
+  for (int t = 0; t < RPL; ++t) {
+    for (int jl = 0; jl < 64; ++jl) {
+      const int j = t * 64 + jl;
+      if (j >= K) break;
+      const T inv = (T)1 / Lf[off].x;
+      cpx<T> xj = shfl_c(x[t], jl);
+      xj = cscale(xj, inv);
+      if (lane == jl) x[t] = xj;
+#pragma unroll
+      for (int u = 0; u < RPL; ++u) {
+        const int i = lane + 64 * u;
+        if (i > j && i < K) x[u] = csub(x[u], cmul(Lf[off + i - j], xj));
+      }
+      off += K - j;
+    }
+  }
+  // backward: L^H x = y
+#pragma unroll
+  for (int t = RPL - 1; t >= 0; --t) {
+    for (int jl = 63; jl >= 0; --jl) {
+      const int j = t * 64 + jl;
+      if (j >= K) continue;
+      const int oj = j * K - (j * (j - 1)) / 2;
+      cpx<T> part = {(T)0, (T)0};
+#pragma unroll
+      for (int u = 0; u < RPL; ++u) {
+        const int i = lane + 64 * u;
+        if (i > j && i < K) part = cadd(part, cmulc(Lf[oj + i - j], x[u]));
+      }
+      part.x = wave_sum(part.x);
+      part.y = wave_sum(part.y);
+      if (lane == jl) x[t] = cscale(csub(x[t], part), (T)1 / Lf[oj].x);
+    }
+  }
+  cpx<T>* Db = Dh + (int64_t)blk * K * F;
+#pragma unroll
+  for (int t = 0; t < RPL; ++t) {
+    const int i = lane + 64 * t;
+    if (i < K) Db[(int64_t)i * F + f] = x[t];
+  }
+}
+
+template <typename T>
+hipError_t launch_dsolve(const cpx<T>* L, const cpx<T>* h, const cpx<T>* Ch, cpx<T>* Dh,
+                         int nblocks, int F, int K, T rho, hipStream_t st) {
+  if (nblocks <= 0) return hipSuccess;
+  const int fgroups = (F + 3) / 4;
+  const dim3 grid((unsigned)(nblocks * fgroups));
+  if (K <= 64)
+    hipLaunchKernelGGL((k_dsolve<T, 1>), grid, dim3(256), 0, st, L, h, Ch, Dh, F, K, rho,
+                       fgroups);
+  else if (K <= 128)
+    hipLaunchKernelGGL((k_dsolve<T, 2>), grid, dim3(256), 0, st, L, h, Ch, Dh, F, K, rho,
+                       fgroups);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+template hipError_t launch_gram_chol<double>(const cpx<double>*, const cpx<double>*,
+                                             cpx<double>*, cpx<double>*, int, int, int, double,
+                                             hipStream_t);
+template hipError_t launch_dsolve<double>(const cpx<double>*, const cpx<double>*,
+                                          const cpx<double>*, cpx<double>*, int, int, int,
+                                          double, hipStream_t);
+
+}  // namespace ccsc

@@ -1,0 +1,945 @@
+// libccsc host engine: problem resolution, memory plan, the outer ADMM
+// schedule of the consensus learners, RCCL consensus, and the C-ABI.
+//
+// Schedule of one outer iteration (dP:89-190; dZ:90-194), per rank:
+//   precompute  for each local block: R2C of its z slices -> Zh;
+//               gram+cholesky -> L_f, h_f                       (dP:95-99)
+//   d-loop      dual+R2C -> C ; dsolve -> Dhat ; C2R -> D, support(D+y)
+//               -> local sum -> RCCL all-reduce -> projection u (dP:103-134)
+//   z-prep      dhat = Dhat of global block 1 (RCCL broadcast), sden  (dP:143)
+//   z-loop      fused z-iteration kernel over the local patches   (dP:147-168)
+#include "../../include/ccsc.h"
+#include "kernels.hpp"
+
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <limits>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+namespace ccsc {
+
+struct Err : std::runtime_error {
+  int code;
+  Err(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define HIPCHK(x)                                                                         \
+  do {                                                                                    \
+    hipError_t e_ = (x);                                                                  \
+    if (e_ != hipSuccess)                                                                 \
+      throw Err(CCSC_E_HIP, std::string(#x) + " failed: " + hipGetErrorString(e_));       \
+  } while (0)
+#define NCCLCHK(x)                                                                        \
+  do {                                                                                    \
+    ncclResult_t r_ = (x);                                                                \
+    if (r_ != ncclSuccess)                                                                \
+      throw Err(CCSC_E_RCCL, std::string(#x) + " failed: " + ncclGetErrorString(r_));     \
+  } while (0)
+
+static void set_err(char* err, size_t errlen, const std::string& m) {
+  if (err && errlen) {
+    std::snprintf(err, errlen, "%s", m.c_str());
+  }
+}
+
+template <typename F>
+static int32_t guarded(char* err, size_t errlen, F&& f) {
+  try {
+    f();
+    return CCSC_OK;
+  } catch (const Err& e) {
+    set_err(err, errlen, e.what());
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    set_err(err, errlen, "host allocation failed");
+    return CCSC_E_NOMEM;
+  } catch (const std::exception& e) {
+    set_err(err, errlen, e.what());
+    return CCSC_E_INVALID;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// FFT planning (host)
+// ---------------------------------------------------------------------------
+static const int kRadices[] = {11, 10, 8, 7, 5, 4, 3, 2};  // fft_pass_dispatch
+static constexpr int kMaxButterflies = kNT * 2;  // MAXB = 2 in the device passes
+
+static bool plan1d(int n, int nlines, Plan1D& out) {
+  Plan1D best{};
+  best.npass = 99;
+  std::vector<int> cur;
+  std::function<void(int, int)> dfs = [&](int rem, int start) {
+    if (rem == 1) {
+      if ((int)cur.size() < best.npass) {
+        best.n = n;
+        best.npass = (int)cur.size();
+        for (int i = 0; i < best.npass; ++i) best.rad[i] = cur[i];
+      }
+      return;
+    }
+    if ((int)cur.size() >= kMaxPass || (int)cur.size() + 1 >= best.npass) return;
+    for (int i = start; i < (int)(sizeof(kRadices) / sizeof(int)); ++i) {
+      const int R = kRadices[i];
+      if (rem % R) continue;
+      if ((int64_t)(n / R) * nlines > kMaxButterflies) continue;
+      cur.push_back(R);
+      dfs(rem / R, i);
+      cur.pop_back();
+    }
+  };
+  if (n == 1) {
+    out = Plan1D{1, 0, {0}};
+    return true;
+  }
+  dfs(n, 0);
+  if (best.npass == 99) return false;
+  out = best;
+  return true;
+}
+
+static bool make_grid2d(int X, int Y, Grid2D& G, std::string& why) {
+  G.X = X;
+  G.Y = Y;
+  G.Xh = X / 2 + 1;
+  G.RS = 2 * G.Xh;
+  G.Yp = Y + (Y & 1);
+  G.F = G.Xh * Y;
+  G.twx = 0;
+  G.twy = X;
+  if (!plan1d(X, G.Yp / 2, G.px)) {
+    why = "grid length " + std::to_string(X) +
+          " has no radix plan (prime factors must be in {2,3,5,7,11} and fit the butterfly budget)";
+    return false;
+  }
+  if (!plan1d(Y, G.Xh, G.py)) {
+    why = "grid length " + std::to_string(Y) +
+          " has no radix plan (prime factors must be in {2,3,5,7,11} and fit the butterfly budget)";
+    return false;
+  }
+  const size_t lds = slice_smem_bytes(G, sizeof(double));
+  if (lds > 160 * 1024) {
+    why = "padded slice " + std::to_string(X) + "x" + std::to_string(Y) +
+          " does not fit one CU's LDS in fp64";
+    return false;
+  }
+  if (pick_nb(G.F) < 0) {
+    why = "half spectrum too large for the register-resident z-solve";
+    return false;
+  }
+  return true;
+}
+
+static std::vector<cpx<double>> make_twiddles(const Grid2D& G) {
+  std::vector<cpx<double>> t(G.X + G.Y);
+  for (int m = 0; m < G.X; ++m) {
+    const long double a = -2.0L * 3.141592653589793238462643383279502884L * m / G.X;
+    t[m] = {(double)cosl(a), (double)sinl(a)};
+  }
+  for (int m = 0; m < G.Y; ++m) {
+    const long double a = -2.0L * 3.141592653589793238462643383279502884L * m / G.Y;
+    t[G.X + m] = {(double)cosl(a), (double)sinl(a)};
+  }
+  return t;
+}
+
+// ---------------------------------------------------------------------------
+// Problem resolution (Appendix A of SURVEY.md)
+// ---------------------------------------------------------------------------
+static void resolve_problem(ccsc_problem& p) {
+  if (p.variant < CCSC_DPAR || p.variant > CCSC_L4D) throw Err(CCSC_E_INVALID, "unknown variant");
+  const bool is3 = p.variant == CCSC_L3D;
+  const int want_ndim = is3 ? 3 : 2;
+  if (p.ndim == 0) p.ndim = want_ndim;
+  if (p.ndim != want_ndim) throw Err(CCSC_E_INVALID, "ndim does not match the variant");
+  for (int i = 0; i < p.ndim; ++i)
+    if (p.sb[i] <= 0) throw Err(CCSC_E_INVALID, "spatial size of b must be positive");
+  if (p.variant != CCSC_L4D) {
+    p.views[0] = p.views[1] = 1;
+  } else if (p.views[0] <= 0 || p.views[1] <= 0 || p.views[0] != p.views[1]) {
+    throw Err(CCSC_E_INVALID, "4D needs equal positive view counts U == V (L4:9-10, Q9)");
+  }
+  if (p.n <= 0) throw Err(CCSC_E_INVALID, "n must be positive");
+  if (p.K <= 0) throw Err(CCSC_E_INVALID, "K must be positive");
+  if (p.psf <= 0 || (p.psf & 1) == 0) throw Err(CCSC_E_INVALID, "psf size must be odd and positive");
+  if (p.max_it < 0) throw Err(CCSC_E_INVALID, "max_it must be >= 0");
+  // variant constants
+  int ni = 100, mid = 10, miz = 10;
+  double rd = 500, rz = 50, td = 50;
+  switch (p.variant) {
+    case CCSC_DPAR: break;                                     // dP:11,75-76,98,150,153
+    case CCSC_DZPAR: mid = 5; rd = 5000; rz = 1; td = 1; break;  // dZ:75,99,151,154
+    case CCSC_L3D:
+    case CCSC_L4D: {
+      const int64_t s = (int64_t)std::llround(std::sqrt((double)p.n));
+      if (s * s != p.n)
+        throw Err(CCSC_E_INVALID, "3D/4D learners need n to be a perfect square (ni = sqrt(n), L3:11)");
+      ni = (int)s;
+      if (p.variant == CCSC_L3D) { rd = 5000; rz = 1; td = 1; }  // L3:109,168,175
+      break;                                                      // L4:105,159,162
+    }
+  }
+  if (p.ni <= 0) p.ni = ni;
+  if (p.max_it_d <= 0) p.max_it_d = mid;
+  if (p.max_it_z <= 0) p.max_it_z = miz;
+  if (!(p.rho_d > 0)) p.rho_d = rd;
+  if (!(p.rho_z > 0)) p.rho_z = rz;
+  if (!(p.theta_div > 0)) p.theta_div = td;
+  if (p.n % p.ni != 0)
+    throw Err(CCSC_E_INVALID, "n (" + std::to_string(p.n) + ") must be a multiple of ni (" +
+                                  std::to_string(p.ni) + "); the reference floors n/ni silently (Q13)");
+  if (p.verbose < CCSC_VERBOSE_NONE || p.verbose > CCSC_VERBOSE_ALL)
+    throw Err(CCSC_E_INVALID, "bad verbose");
+  if (p.precision != CCSC_FP64 && p.precision != CCSC_FP32) throw Err(CCSC_E_INVALID, "bad precision");
+  const int r = p.psf / 2;
+  for (int i = 0; i < p.ndim; ++i)
+    if (p.sb[i] + 2 * r < p.psf) throw Err(CCSC_E_INVALID, "grid smaller than the filter");
+}
+
+// engine capability check (separate from validity: valid reference inputs we
+// do not run yet return CCSC_E_UNSUPPORTED)
+static void check_supported(const ccsc_problem& p, Grid2D* Gout) {
+  if (p.variant == CCSC_L3D || p.variant == CCSC_L4D)
+    throw Err(CCSC_E_UNSUPPORTED, "3D/4D learners are not on the GPU engine yet (SURVEY §8f)");
+  if (p.precision != CCSC_FP64) throw Err(CCSC_E_UNSUPPORTED, "only CCSC_FP64 is built");
+  if (p.K > 110) throw Err(CCSC_E_UNSUPPORTED, "K > 110 exceeds the gram kernel's tile budget");
+  const int r = p.psf / 2;
+  Grid2D G{};
+  std::string why;
+  if (!make_grid2d((int)(p.sb[0] + 2 * r), (int)(p.sb[1] + 2 * r), G, why))
+    throw Err(CCSC_E_UNSUPPORTED, why);
+  if (Gout) *Gout = G;
+}
+
+static void shard(const ccsc_problem& p, int rank, int nranks, int64_t& b0, int64_t& nb) {
+  if (nranks <= 0 || rank < 0 || rank >= nranks) throw Err(CCSC_E_INVALID, "bad rank/nranks");
+  const int64_t N = p.n / p.ni;
+  if (N < nranks) throw Err(CCSC_E_INVALID, "fewer blocks than ranks");
+  const int64_t base = N / nranks, rem = N % nranks;
+  nb = base + (rank < rem ? 1 : 0);
+  b0 = rank * base + std::min<int64_t>(rank, rem);
+}
+
+// ---------------------------------------------------------------------------
+// device memory helpers
+// ---------------------------------------------------------------------------
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() { release(); }
+  void alloc(size_t b) {
+    release();
+    if (b == 0) return;
+    HIPCHK(hipMalloc(&p, b));
+    bytes = b;
+  }
+  void release() {
+    if (p) hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  template <typename X> X* as() const { return reinterpret_cast<X*>(p); }
+};
+
+}  // namespace ccsc
+
+using namespace ccsc;
+
+struct ccsc_ctx {
+  int device = 0;
+  int rank = 0;
+  int nranks = 1;
+  hipStream_t stream = nullptr;
+  ncclComm_t comm = nullptr;
+};
+
+namespace ccsc {
+
+// memory plan shared by ccsc_plan_bytes and the session
+struct Plan2D {
+  int64_t np, nbl, b0;
+  size_t z, yz, cbuf, D, yD, Bhat, b, L, h, Ch, Dh, Zh, misc;
+  size_t total() const { return z + yz + cbuf + D + yD + Bhat + b + L + h + Ch + Dh + Zh + misc; }
+};
+
+static Plan2D plan2d(const ccsc_problem& p, const Grid2D& G, int rank, int nranks) {
+  Plan2D m{};
+  shard(p, rank, nranks, m.b0, m.nbl);
+  m.np = m.nbl * p.ni;
+  const size_t P = (size_t)G.X * G.Y, F = G.F, K = p.K;
+  const size_t Kp = K * (K + 1) / 2;
+  const size_t s = p.psf;
+  m.z = m.np * K * P * 8;
+  m.yz = m.z;
+  m.cbuf = (p.tol > 0) ? m.z : 0;
+  m.D = m.nbl * K * P * 8;
+  m.yD = m.D;
+  m.Bhat = m.np * F * 16;
+  m.b = m.np * (size_t)p.sb[0] * p.sb[1] * 8;
+  m.L = m.nbl * F * Kp * 16;
+  m.h = m.nbl * F * K * 16;
+  m.Ch = m.nbl * K * F * 16;
+  m.Dh = m.Ch;
+  m.Zh = (size_t)p.ni * K * F * 16;
+  m.misc = (2 * K * F) * 16 + F * 8 + (m.nbl + 2) * K * s * s * 8 * 2 + (4 * m.np + 4 * K + 64) * 8 +
+           (G.X + G.Y) * 16;
+  return m;
+}
+
+static const char* kKernelNames[5] = {"zstep", "gram_chol", "dsolve", "dual_r2c", "c2r_dout"};
+
+// ---------------------------------------------------------------------------
+// Session: 2D consensus learners (dP / dZ)
+// ---------------------------------------------------------------------------
+struct Session2D {
+  ccsc_ctx* ctx;
+  ccsc_problem p;
+  Grid2D G;
+  Plan2D m;
+  int r, s, K, ni, P, F, Kp;
+  int64_t N, nbl, b0, np;
+  bool owner0;
+  double theta;
+  hipStream_t st;
+
+  DevBuf tw, bdev, Bhat, z, yz, cbuf, D, yD, Usup, ssum, supp, Ch, Dh, L, h, Zh, dhat, dtmp, sden,
+      dnorm, znorm, part, pair;
+
+  // host-side log
+  int outer_done = 0;
+  bool finished = false;
+  double last_d = std::numeric_limits<double>::infinity();
+  double last_z = std::numeric_limits<double>::infinity();
+  double obj_filter = std::numeric_limits<double>::quiet_NaN();
+  double obj_z = std::numeric_limits<double>::quiet_NaN();
+  std::vector<double> v_obj_d, v_obj_z, v_tim, tr_od, tr_oz, tr_dd, tr_zd;
+  std::vector<int32_t> v_nd, v_nz;
+
+  // profiling
+  bool prof = false;
+  struct Rec { int id; hipEvent_t a, b; };
+  std::vector<Rec> recs;
+  std::vector<hipEvent_t> pool;
+  int64_t k_launch[5] = {0, 0, 0, 0, 0};
+  double k_ms[5] = {0, 0, 0, 0, 0};
+
+  hipEvent_t get_event() {
+    if (!pool.empty()) {
+      hipEvent_t e = pool.back();
+      pool.pop_back();
+      return e;
+    }
+    hipEvent_t e;
+    HIPCHK(hipEventCreate(&e));
+    return e;
+  }
+  template <typename Fn>
+  void timed(int id, Fn&& fn) {
+    if (!prof) {
+      fn();
+      return;
+    }
+    Rec rc{id, get_event(), get_event()};
+    HIPCHK(hipEventRecord(rc.a, st));
+    fn();
+    HIPCHK(hipEventRecord(rc.b, st));
+    recs.push_back(rc);
+  }
+  void drain_records() {
+    for (auto& rc : recs) {
+      float ms = 0;
+      HIPCHK(hipEventSynchronize(rc.b));
+      HIPCHK(hipEventElapsedTime(&ms, rc.a, rc.b));
+      k_launch[rc.id] += 1;
+      k_ms[rc.id] += ms;
+      pool.push_back(rc.a);
+      pool.push_back(rc.b);
+    }
+    recs.clear();
+  }
+
+  ~Session2D() {
+    if (st) hipStreamSynchronize(st);
+    for (auto& rc : recs) {
+      hipEventDestroy(rc.a);
+      hipEventDestroy(rc.b);
+    }
+    for (auto e : pool) hipEventDestroy(e);
+  }
+
+  bool verbose_refresh_d() const {
+    if (p.variant == CCSC_DPAR) return p.verbose == CCSC_VERBOSE_BRIEF;  // dP:126
+    return p.verbose != CCSC_VERBOSE_NONE;                               // dZ:127
+  }
+  bool verbose_refresh_z() const {
+    if (p.variant == CCSC_DPAR) return p.verbose == CCSC_VERBOSE_BRIEF;  // dP:161
+    return p.verbose != CCSC_VERBOSE_NONE;                               // dZ:165
+  }
+
+  Session2D(ccsc_ctx* c, const ccsc_problem& pin, const double* b, const double* d0,
+            const double* z0)
+      : ctx(c), p(pin), st(c->stream) {
+    resolve_problem(p);
+    check_supported(p, &G);
+    m = plan2d(p, G, ctx->rank, ctx->nranks);
+    r = p.psf / 2;
+    s = p.psf;
+    K = p.K;
+    ni = p.ni;
+    P = G.X * G.Y;
+    F = G.F;
+    Kp = K * (K + 1) / 2;
+    N = p.n / ni;
+    nbl = m.nbl;
+    b0 = m.b0;
+    np = m.np;
+    owner0 = (b0 == 0);
+    theta = p.lambda_prior / p.theta_div;
+    if (!b) throw Err(CCSC_E_INVALID, "b must not be NULL");
+
+    size_t freeb = 0, totalb = 0;
+    HIPCHK(hipMemGetInfo(&freeb, &totalb));
+    if (m.total() > freeb)
+      throw Err(CCSC_E_NOMEM, "device plan needs " + std::to_string(m.total() >> 20) +
+                                  " MiB, " + std::to_string(freeb >> 20) + " MiB free" +
+                                  (p.tol > 0 ? " (tol > 0 adds a z-sized buffer)" : ""));
+    auto tws = make_twiddles(G);
+    tw.alloc(tws.size() * sizeof(cpx<double>));
+    HIPCHK(hipMemcpy(tw.p, tws.data(), tw.bytes, hipMemcpyHostToDevice));
+    const size_t KP = (size_t)K * P;
+    bdev.alloc(m.b);
+    Bhat.alloc(m.Bhat);
+    z.alloc(m.z);
+    yz.alloc(m.yz);
+    if (m.cbuf) cbuf.alloc(m.cbuf);
+    D.alloc(m.D);
+    yD.alloc(m.yD);
+    Usup.alloc((size_t)K * s * s * 8);
+    ssum.alloc((size_t)K * s * s * 8);
+    supp.alloc((size_t)nbl * K * s * s * 8);
+    Ch.alloc(m.Ch);
+    Dh.alloc(m.Dh);
+    L.alloc(m.L);
+    h.alloc(m.h);
+    Zh.alloc(m.Zh);
+    dhat.alloc((size_t)K * F * 16);
+    dtmp.alloc((size_t)K * F * 16);
+    sden.alloc((size_t)F * 8);
+    dnorm.alloc((size_t)2 * K * 8);
+    znorm.alloc((size_t)2 * std::max<int64_t>(np, 1) * 8);
+    part.alloc((size_t)2 * std::max<int64_t>(np, 1) * 8);
+    pair.alloc(4 * 8);
+
+    // data: b (rank-local, [sbx, sby, np] column-major) and its padded spectrum
+    const int sbx = (int)p.sb[0], sby = (int)p.sb[1];
+    HIPCHK(hipMemcpy(bdev.p, b, m.b, hipMemcpyHostToDevice));
+    HIPCHK(launch_r2c_embed<double>(bdev.as<double>(), (int64_t)sbx * sby, sbx, sby, r, r,
+                                    Bhat.as<cpx<double>>(), F, np, tw.as<cpx<double>>(), G, st));
+    // filters: init.d or device RNG (dP:38-39)
+    DevBuf d0dev;
+    const size_t nd0 = (size_t)s * s * K;
+    d0dev.alloc(nd0 * 8);
+    if (d0) HIPCHK(hipMemcpy(d0dev.p, d0, nd0 * 8, hipMemcpyHostToDevice));
+    else HIPCHK(launch_randn<double>(d0dev.as<double>(), (int64_t)nd0, p.seed ^ 0xd0d0d0d0ULL, 0, st));
+    HIPCHK(launch_embed_filters<double>(d0dev.as<double>(), D.as<double>(), (int)nbl, K, s, G, st));
+    HIPCHK(hipMemsetAsync(yD.p, 0, m.yD, st));
+    HIPCHK(hipMemsetAsync(Usup.p, 0, Usup.bytes, st));  // u = Pi(0) = 0 (Q2)
+    HIPCHK(hipMemsetAsync(yz.p, 0, m.yz, st));
+    // codes: init.z or device RNG (dP:45; dZ:44-47 replicates one z0 per block)
+    if (p.variant == CCSC_DZPAR) {
+      const size_t nz0 = (size_t)ni * KP;
+      if (z0) HIPCHK(hipMemcpy(z.p, z0, nz0 * 8, hipMemcpyHostToDevice));
+      else HIPCHK(launch_randn<double>(z.as<double>(), (int64_t)nz0, p.seed, 0, st));
+      if (nbl > 1)
+        HIPCHK(launch_replicate<double>(z.as<double>(), z.as<double>() + nz0, (int64_t)nz0,
+                                        (int)nbl - 1, st));
+    } else {
+      if (z0) HIPCHK(hipMemcpy(z.p, z0, m.z, hipMemcpyHostToDevice));
+      else
+        HIPCHK(launch_randn<double>(z.as<double>(), (int64_t)(np * KP), p.seed,
+                                    (uint64_t)(b0 * ni) * KP, st));
+    }
+    // dhat = fft2(d) of the initial filters (all blocks share d0, dP:41-42)
+    HIPCHK(launch_r2c_embed<double>(D.as<double>(), P, G.X, G.Y, 0, 0, dhat.as<cpx<double>>(),
+                                    F, K, tw.as<cpx<double>>(), G, st));
+    HIPCHK(hipStreamSynchronize(st));
+
+    v_obj_d.push_back(std::numeric_limits<double>::quiet_NaN());
+    v_obj_z.push_back(std::numeric_limits<double>::quiet_NaN());
+    v_tim.push_back(0.0);
+    if (p.verbose != CCSC_VERBOSE_NONE || p.trace_objective) {
+      const double o = objective(dhat.as<cpx<double>>(), nullptr);  // dP:56
+      obj_filter = obj_z = o;
+      v_obj_d[0] = o;
+      v_obj_z[0] = o;
+    }
+  }
+
+  // ---- collectives ----------------------------------------------------------
+  void allreduce(double* buf, size_t count) {
+    if (ctx->nranks > 1)
+      NCCLCHK(ncclAllReduce(buf, buf, count, ncclDouble, ncclSum, ctx->comm, st));
+  }
+  void bcast0(double* buf, size_t count) {
+    if (ctx->nranks > 1) NCCLCHK(ncclBroadcast(buf, buf, count, ncclDouble, 0, ctx->comm, st));
+  }
+  void pair_to_host(double* out2) {
+    HIPCHK(hipMemcpyAsync(out2, pair.p, 2 * sizeof(double), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+  }
+
+  // objective with filter spectrum `dsp` (valid on every rank); DZ optional.
+  double objective(const cpx<double>* dsp, double* DZdev) {
+    HIPCHK(launch_objective<double>(z.as<double>(), dsp, bdev.as<double>(), (int)p.sb[0],
+                                    (int)p.sb[1], r, DZdev, part.as<double>(), np,
+                                    tw.as<cpx<double>>(), G, K, st));
+    HIPCHK(launch_sum_pairs<double>(part.as<double>(), (int)np, pair.as<double>(), st));
+    allreduce(pair.as<double>(), 2);
+    double h2[2];
+    pair_to_host(h2);
+    return p.lambda_residual * 0.5 * h2[0] + p.lambda_prior * h2[1];
+  }
+  // current filter spectrum of global block 1 into dtmp on every rank
+  const cpx<double>* current_dhat() {
+    if (owner0)
+      HIPCHK(hipMemcpyAsync(dtmp.p, Dh.p, (size_t)K * F * 16, hipMemcpyDeviceToDevice, st));
+    bcast0(dtmp.as<double>(), (size_t)2 * K * F);
+    return dtmp.as<cpx<double>>();
+  }
+
+  // ---- one outer iteration --------------------------------------------------
+  void outer_iteration() {
+    const int it = outer_done;
+    const auto* twc = tw.as<cpx<double>>();
+    hipEvent_t e0 = get_event(), e1 = get_event();
+    double obj_ms = 0;
+    auto objective_timed = [&](const cpx<double>* dsp) {
+      hipEvent_t a = get_event(), b = get_event();
+      HIPCHK(hipEventRecord(a, st));
+      const double o = objective(dsp, nullptr);
+      HIPCHK(hipEventRecord(b, st));
+      HIPCHK(hipEventSynchronize(b));
+      float ms = 0;
+      HIPCHK(hipEventElapsedTime(&ms, a, b));
+      obj_ms += ms;
+      pool.push_back(a);
+      pool.push_back(b);
+      return o;
+    };
+    HIPCHK(hipEventRecord(e0, st));
+
+    // ---- D precompute (dP:95-99) ----
+    for (int64_t jl = 0; jl < nbl; ++jl) {
+      HIPCHK(launch_r2c_embed<double>(z.as<double>() + (size_t)jl * ni * K * P, P, G.X, G.Y, 0, 0,
+                                      Zh.as<cpx<double>>(), F, (int64_t)ni * K, twc, G, st));
+      timed(1, [&] {
+        HIPCHK(launch_gram_chol<double>(Zh.as<cpx<double>>(),
+                                        Bhat.as<cpx<double>>() + (size_t)jl * ni * F,
+                                        L.as<cpx<double>>() + (size_t)jl * F * Kp,
+                                        h.as<cpx<double>>() + (size_t)jl * F * K, F, K, ni,
+                                        p.rho_d, st));
+      });
+    }
+    // ---- D iterations (dP:103-134) ----
+    const bool tol_on = p.tol > 0;
+    const bool want_od = verbose_refresh_d() || p.trace_objective;
+    int nd = 0;
+    for (int id = 0; id < p.max_it_d; ++id) {
+      timed(3, [&] {
+        HIPCHK(launch_dual_r2c<double>(D.as<double>(), yD.as<double>(), Usup.as<double>(),
+                                       Ch.as<cpx<double>>(), nbl * K, twc, G, K, r, st));
+      });
+      timed(2, [&] {
+        HIPCHK(launch_dsolve<double>(L.as<cpx<double>>(), h.as<cpx<double>>(),
+                                     Ch.as<cpx<double>>(), Dh.as<cpx<double>>(), (int)nbl, F, K,
+                                     p.rho_d, st));
+      });
+      timed(4, [&] {
+        HIPCHK(launch_c2r_dout<double>(Dh.as<cpx<double>>(), D.as<double>(), yD.as<double>(),
+                                       supp.as<double>(), dnorm.as<double>(),
+                                       owner0 ? K : 0, nbl * K, twc, G, r, st));
+      });
+      HIPCHK(launch_supp_reduce<double>(supp.as<double>(), ssum.as<double>(), (int)nbl,
+                                        K * s * s, st));
+      allreduce(ssum.as<double>(), (size_t)K * s * s);
+      HIPCHK(launch_project<double>(ssum.as<double>(), Usup.as<double>(), K, s * s,
+                                    1.0 / (double)N, st));
+      ++nd;
+      double dd = std::numeric_limits<double>::quiet_NaN();
+      if (tol_on) {
+        if (owner0) HIPCHK(launch_sum_pairs<double>(dnorm.as<double>(), K, pair.as<double>(), st));
+        else HIPCHK(hipMemsetAsync(pair.p, 0, 2 * sizeof(double), st));
+        allreduce(pair.as<double>(), 2);
+        double h2[2];
+        pair_to_host(h2);
+        dd = std::sqrt(h2[0]) / std::sqrt(h2[1]);
+        last_d = dd;
+        tr_dd[(size_t)it * p.max_it_d + id] = dd;
+      }
+      if (want_od) {
+        const double o = objective_timed(current_dhat());
+        if (verbose_refresh_d()) obj_filter = o;
+        if (p.trace_objective) tr_od[(size_t)it * p.max_it_d + id] = o;
+      }
+      if (tol_on && dd < p.tol) break;  // dP:130-132
+    }
+    // ---- Z precompute (dP:143-144): d = Dhat of block 1 ----
+    if (owner0) HIPCHK(hipMemcpyAsync(dhat.p, Dh.p, (size_t)K * F * 16, hipMemcpyDeviceToDevice, st));
+    bcast0(dhat.as<double>(), (size_t)2 * K * F);
+    HIPCHK(launch_sden<double>(dhat.as<cpx<double>>(), sden.as<double>(), F, K, p.rho_z,
+                               1.0 / (double)P, st));
+    // ---- Z iterations (dP:147-168) ----
+    const bool want_oz = verbose_refresh_z() || p.trace_objective;
+    int nz = 0;
+    for (int iz = 0; iz < p.max_it_z; ++iz) {
+      timed(0, [&] {
+        HIPCHK(launch_zstep<double>(z.as<double>(), yz.as<double>(), cbuf.as<double>(),
+                                    Bhat.as<cpx<double>>(), dhat.as<cpx<double>>(),
+                                    sden.as<double>(), np, twc, G, K, theta, znorm.as<double>(),
+                                    tol_on, st));
+      });
+      ++nz;
+      double zd = std::numeric_limits<double>::quiet_NaN();
+      if (tol_on) {
+        HIPCHK(launch_sum_pairs<double>(znorm.as<double>(), (int)np, pair.as<double>(), st));
+        allreduce(pair.as<double>(), 2);
+        double h2[2];
+        pair_to_host(h2);
+        zd = std::sqrt(h2[0]) / std::sqrt(h2[1]);
+        last_z = zd;
+        tr_zd[(size_t)it * p.max_it_z + iz] = zd;
+      }
+      if (want_oz) {
+        const double o = objective_timed(dhat.as<cpx<double>>());
+        if (verbose_refresh_z()) obj_z = o;
+        if (p.trace_objective) tr_oz[(size_t)it * p.max_it_z + iz] = o;
+      }
+      if (tol_on && zd < p.tol) break;  // dP:165-167
+    }
+    HIPCHK(hipEventRecord(e1, st));
+    HIPCHK(hipEventSynchronize(e1));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+    pool.push_back(e0);
+    pool.push_back(e1);
+    drain_records();
+    const double secs = (ms - obj_ms) * 1e-3;
+    v_obj_d.push_back(obj_filter);  // dP:174-176
+    v_obj_z.push_back(obj_z);
+    v_tim.push_back(v_tim.back() + secs);
+    v_nd.push_back(nd);
+    v_nz.push_back(nz);
+    ++outer_done;
+    if (tol_on && last_z < p.tol && last_d < p.tol) finished = true;  // dP:186-188
+  }
+
+  void ensure_trace_capacity(int total_outer) {
+    const size_t nd = (size_t)total_outer * p.max_it_d, nz = (size_t)total_outer * p.max_it_z;
+    const double nan = std::numeric_limits<double>::quiet_NaN();
+    if (tr_od.size() < nd) tr_od.resize(nd, nan);
+    if (tr_dd.size() < nd) tr_dd.resize(nd, nan);
+    if (tr_oz.size() < nz) tr_oz.resize(nz, nan);
+    if (tr_zd.size() < nz) tr_zd.resize(nz, nan);
+  }
+
+  void step(int n_outer, int32_t* done) {
+    ensure_trace_capacity(outer_done + n_outer);
+    for (int i = 0; i < n_outer && !finished; ++i) outer_iteration();
+    if (done) *done = finished ? 1 : 0;
+  }
+
+  void results(ccsc_outputs* out) {
+    if (!out) return;
+    if (out->d_res) {
+      // D1 lives on rank 0 (block 1); broadcast so every rank returns it.
+      std::vector<double> D1((size_t)K * P);
+      DevBuf tmp;
+      tmp.alloc((size_t)K * P * 8);
+      if (owner0) HIPCHK(hipMemcpyAsync(tmp.p, D.p, tmp.bytes, hipMemcpyDeviceToDevice, st));
+      bcast0(tmp.as<double>(), (size_t)K * P);
+      HIPCHK(hipMemcpyAsync(D1.data(), tmp.p, tmp.bytes, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      // d_res = circshift(D1, +r)(1:psf, 1:psf, :)   (dP:195-196)
+      for (int k = 0; k < K; ++k)
+        for (int j = 0; j < s; ++j)
+          for (int i = 0; i < s; ++i) {
+            const int x = (i - r + G.X) % G.X, y = (j - r + G.Y) % G.Y;
+            out->d_res[i + (size_t)s * (j + (size_t)s * k)] = D1[(size_t)k * P + (size_t)y * G.X + x];
+          }
+    }
+    if (out->z_res) {
+      HIPCHK(hipMemcpy(out->z_res, z.p, m.z, hipMemcpyDeviceToHost));
+    }
+    if (out->DZ) {
+      // DZ = real(ifft2(sum_k zhat .* dup{1}))  (dP:193), uncropped [X,Y,1,n]
+      DevBuf dz;
+      dz.alloc((size_t)np * P * 8);
+      objective(dhat.as<cpx<double>>(), dz.as<double>());
+      HIPCHK(hipMemcpy(out->DZ, dz.p, dz.bytes, hipMemcpyDeviceToHost));
+    }
+    if (out->obj_val) *out->obj_val = objective(dhat.as<cpx<double>>(), nullptr);
+  }
+
+  void iterlog(ccsc_iterlog* lg) {
+    if (!lg) return;
+    const int cnt = std::min<int>(lg->capacity, (int)v_tim.size());
+    lg->count = cnt;
+    for (int i = 0; i < cnt; ++i) {
+      if (lg->obj_vals_d) lg->obj_vals_d[i] = v_obj_d[i];
+      if (lg->obj_vals_z) lg->obj_vals_z[i] = v_obj_z[i];
+      if (lg->tim_vals) lg->tim_vals[i] = v_tim[i];
+    }
+    const int no = std::min<int>(lg->capacity, outer_done);
+    for (int i = 0; i < no; ++i) {
+      if (lg->n_d) lg->n_d[i] = v_nd[i];
+      if (lg->n_z) lg->n_z[i] = v_nz[i];
+      for (int t = 0; t < p.max_it_d; ++t) {
+        const size_t q = (size_t)i * p.max_it_d + t;
+        if (lg->trace_obj_d) lg->trace_obj_d[q] = q < tr_od.size() ? tr_od[q] : NAN;
+        if (lg->trace_d_diff) lg->trace_d_diff[q] = q < tr_dd.size() ? tr_dd[q] : NAN;
+      }
+      for (int t = 0; t < p.max_it_z; ++t) {
+        const size_t q = (size_t)i * p.max_it_z + t;
+        if (lg->trace_obj_z) lg->trace_obj_z[q] = q < tr_oz.size() ? tr_oz[q] : NAN;
+        if (lg->trace_z_diff) lg->trace_z_diff[q] = q < tr_zd.size() ? tr_zd[q] : NAN;
+      }
+    }
+  }
+
+  double alg_bytes(int id) const {
+    const double Pd = P, Fd = F, Kd = K;
+    switch (id) {
+      case 0:  // z-iteration compulsory state traffic: read z,y + write z,y (fp64), B per patch
+        return (double)np * Kd * 4.0 * 8.0 * Pd + (double)np * 16.0 * Fd + Kd * Fd * 16.0;
+      case 1:  // gram+chol per block: read A (ni x K x F) + b, write L, h
+        return (double)ni * Kd * Fd * 16.0 + ni * Fd * 16.0 + Fd * Kp * 16.0 + Fd * Kd * 16.0;
+      case 2:  // dsolve over local blocks: read L, h, C; write Dhat
+        return (double)nbl * Fd * (Kp + 3.0 * Kd) * 16.0;
+      case 3:  // dual+R2C: read D, y; write y, C
+        return (double)nbl * Kd * (3.0 * 8.0 * Pd + 16.0 * Fd);
+      case 4:  // C2R + support: read Dhat, write D
+        return (double)nbl * Kd * (16.0 * Fd + 8.0 * Pd);
+    }
+    return 0;
+  }
+};
+
+}  // namespace ccsc
+
+struct ccsc_session {
+  std::unique_ptr<ccsc::Session2D> s2;
+};
+
+// ===========================================================================
+// C-ABI
+// ===========================================================================
+extern "C" {
+
+int32_t ccsc_abi_version(void) { return CCSC_ABI_VERSION; }
+
+int32_t ccsc_resolve(ccsc_problem* p, char* err, size_t errlen) {
+  return guarded(err, errlen, [&] {
+    if (!p) throw Err(CCSC_E_INVALID, "problem is NULL");
+    resolve_problem(*p);
+    check_supported(*p, nullptr);
+  });
+}
+
+int32_t ccsc_shard(const ccsc_problem* p, int32_t rank, int32_t nranks, int64_t* block_begin,
+                   int64_t* block_count, char* err, size_t errlen) {
+  return guarded(err, errlen, [&] {
+    if (!p || !block_begin || !block_count) throw Err(CCSC_E_INVALID, "NULL argument");
+    ccsc_problem q = *p;
+    resolve_problem(q);
+    shard(q, rank, nranks, *block_begin, *block_count);
+  });
+}
+
+int32_t ccsc_plan_bytes(const ccsc_problem* p, int32_t rank, int32_t nranks, uint64_t* bytes,
+                        char* err, size_t errlen) {
+  return guarded(err, errlen, [&] {
+    if (!p || !bytes) throw Err(CCSC_E_INVALID, "NULL argument");
+    ccsc_problem q = *p;
+    resolve_problem(q);
+    Grid2D G{};
+    check_supported(q, &G);
+    *bytes = plan2d(q, G, rank, nranks).total();
+  });
+}
+
+int32_t ccsc_device_count(int32_t* count, char* err, size_t errlen) {
+  return guarded(err, errlen, [&] {
+    int c = 0;
+    HIPCHK(hipGetDeviceCount(&c));
+    *count = c;
+  });
+}
+
+int32_t ccsc_get_unique_id(uint8_t* uid128, char* err, size_t errlen) {
+  return guarded(err, errlen, [&] {
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+    ncclUniqueId id;
+    NCCLCHK(ncclGetUniqueId(&id));
+    std::memcpy(uid128, &id, 128);
+  });
+}
+
+ccsc_ctx* ccsc_create(int32_t device, int32_t rank, int32_t nranks, const uint8_t* uid128,
+                      char* err, size_t errlen) {
+  ccsc_ctx* ctx = nullptr;
+  const int rc = guarded(err, errlen, [&] {
+    if (nranks < 1 || rank < 0 || rank >= nranks) throw Err(CCSC_E_INVALID, "bad rank/nranks");
+    std::unique_ptr<ccsc_ctx> c(new ccsc_ctx());
+    c->device = device;
+    c->rank = rank;
+    c->nranks = nranks;
+    HIPCHK(hipSetDevice(device));
+    HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    if (nranks > 1) {
+      if (!uid128) throw Err(CCSC_E_INVALID, "multi-rank context needs the RCCL unique id");
+      ncclUniqueId id;
+      std::memcpy(&id, uid128, 128);
+      NCCLCHK(ncclCommInitRank(&c->comm, nranks, id, rank));
+    }
+    ctx = c.release();
+  });
+  return rc == CCSC_OK ? ctx : nullptr;
+}
+
+void ccsc_destroy(ccsc_ctx* ctx) {
+  if (!ctx) return;
+  hipSetDevice(ctx->device);
+  if (ctx->stream) hipStreamSynchronize(ctx->stream);
+  if (ctx->comm) ncclCommDestroy(ctx->comm);
+  if (ctx->stream) hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+ccsc_session* ccsc_session_create(ccsc_ctx* ctx, const ccsc_problem* p, const double* b,
+                                  const double* d0, const double* z0, char* err, size_t errlen) {
+  ccsc_session* out = nullptr;
+  guarded(err, errlen, [&] {
+    if (!ctx || !p) throw Err(CCSC_E_INVALID, "NULL ctx/problem");
+    HIPCHK(hipSetDevice(ctx->device));
+    std::unique_ptr<ccsc_session> s(new ccsc_session());
+    s->s2.reset(new Session2D(ctx, *p, b, d0, z0));
+    out = s.release();
+  });
+  return out;
+}
+
+int32_t ccsc_session_step(ccsc_session* s, int32_t n_outer, int32_t* done, char* err,
+                          size_t errlen) {
+  return guarded(err, errlen, [&] {
+    if (!s || !s->s2) throw Err(CCSC_E_STATE, "no session");
+    HIPCHK(hipSetDevice(s->s2->ctx->device));
+    s->s2->step(n_outer, done);
+  });
+}
+
+int32_t ccsc_session_objective(ccsc_session* s, double* obj, char* err, size_t errlen) {
+  return guarded(err, errlen, [&] {
+    if (!s || !s->s2 || !obj) throw Err(CCSC_E_STATE, "no session");
+    HIPCHK(hipSetDevice(s->s2->ctx->device));
+    *obj = s->s2->objective(s->s2->dhat.as<cpx<double>>(), nullptr);
+  });
+}
+
+int32_t ccsc_session_results(ccsc_session* s, ccsc_outputs* out, char* err, size_t errlen) {
+  return guarded(err, errlen, [&] {
+    if (!s || !s->s2) throw Err(CCSC_E_STATE, "no session");
+    HIPCHK(hipSetDevice(s->s2->ctx->device));
+    s->s2->results(out);
+  });
+}
+
+int32_t ccsc_session_iterlog(ccsc_session* s, ccsc_iterlog* log, char* err, size_t errlen) {
+  return guarded(err, errlen, [&] {
+    if (!s || !s->s2) throw Err(CCSC_E_STATE, "no session");
+    s->s2->iterlog(log);
+  });
+}
+
+int32_t ccsc_session_set_profiling(ccsc_session* s, int32_t on) {
+  if (!s || !s->s2) return CCSC_E_STATE;
+  s->s2->prof = on != 0;
+  return CCSC_OK;
+}
+
+int32_t ccsc_session_kernel_stats(ccsc_session* s, int32_t id, int64_t* launches,
+                                  double* total_ms, double* alg_bytes_per_launch, char* err,
+                                  size_t errlen) {
+  return guarded(err, errlen, [&] {
+    if (!s || !s->s2) throw Err(CCSC_E_STATE, "no session");
+    if (id < 0 || id > 4) throw Err(CCSC_E_INVALID, "kernel id out of range");
+    if (launches) *launches = s->s2->k_launch[id];
+    if (total_ms) *total_ms = s->s2->k_ms[id];
+    if (alg_bytes_per_launch) *alg_bytes_per_launch = s->s2->alg_bytes(id);
+    (void)kKernelNames;
+  });
+}
+
+void ccsc_session_destroy(ccsc_session* s) {
+  if (!s) return;
+  if (s->s2) hipSetDevice(s->s2->ctx->device);
+  delete s;
+}
+
+int32_t ccsc_learn(ccsc_ctx* ctx, const ccsc_problem* p, const double* b, const double* d0,
+                   const double* z0, ccsc_outputs* out, ccsc_iterlog* log, ccsc_cb cb,
+                   void* user, char* err, size_t errlen) {
+  return guarded(err, errlen, [&] {
+    if (!ctx || !p) throw Err(CCSC_E_INVALID, "NULL ctx/problem");
+    HIPCHK(hipSetDevice(ctx->device));
+    Session2D S(ctx, *p, b, d0, z0);
+    S.ensure_trace_capacity(S.p.max_it);
+    for (int i = 0; i < S.p.max_it && !S.finished; ++i) {
+      S.outer_iteration();
+      if (cb) cb(user, S.outer_done, S.v_obj_d.back(), S.v_obj_z.back(), S.v_tim.back());
+    }
+    S.results(out);
+    S.iterlog(log);
+  });
+}
+
+int32_t ccsc_test_fft2d(ccsc_ctx* ctx, int32_t X, int32_t Y, int32_t count, const double* in,
+                        double* out_halfspec, double* roundtrip, char* err, size_t errlen) {
+  return guarded(err, errlen, [&] {
+    if (!ctx || !in || count <= 0) throw Err(CCSC_E_INVALID, "bad arguments");
+    HIPCHK(hipSetDevice(ctx->device));
+    Grid2D G{};
+    std::string why;
+    if (!make_grid2d(X, Y, G, why)) throw Err(CCSC_E_UNSUPPORTED, why);
+    auto tws = make_twiddles(G);
+    DevBuf tw, a, hs, rt;
+    tw.alloc(tws.size() * 16);
+    HIPCHK(hipMemcpy(tw.p, tws.data(), tw.bytes, hipMemcpyHostToDevice));
+    const size_t P = (size_t)X * Y;
+    a.alloc(P * count * 8);
+    hs.alloc((size_t)G.F * count * 16);
+    rt.alloc(P * count * 8);
+    HIPCHK(hipMemcpy(a.p, in, a.bytes, hipMemcpyHostToDevice));
+    hipStream_t st = ctx->stream;
+    HIPCHK(launch_r2c_embed<double>(a.as<double>(), P, X, Y, 0, 0, hs.as<cpx<double>>(), G.F,
+                                    count, tw.as<cpx<double>>(), G, st));
+    HIPCHK(launch_c2r_plain<double>(hs.as<cpx<double>>(), G.F, rt.as<double>(), P, count,
+                                    tw.as<cpx<double>>(), G, 1.0 / (double)P, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (out_halfspec) HIPCHK(hipMemcpy(out_halfspec, hs.p, hs.bytes, hipMemcpyDeviceToHost));
+    if (roundtrip) HIPCHK(hipMemcpy(roundtrip, rt.p, rt.bytes, hipMemcpyDeviceToHost));
+  });
+}
+
+}  // extern "C"

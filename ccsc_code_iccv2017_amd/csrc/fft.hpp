@@ -1,0 +1,373 @@
+// LDS-resident mixed-radix Stockham FFT building blocks for gfx950.
+//
+// Replaces the fft2/ifft2/fftn builtins the reference calls on every
+// (filter, patch) slice (dP:24,41,46,110,112,143,152,154).
+// One workgroup (kNT threads) transforms one slice held in LDS:
+//
+//   R2C  (forward, MATLAB fft2):  x-pass on column pairs (two real rows packed
+//        as one complex line, "split" format: re in row 2j, im in row 2j+1),
+//        then y-passes over the Xh = X/2+1 half-spectrum columns.  The
+//        two-for-one separation is folded into the first y-pass's loads.
+//   C2R  (inverse, MATLAB real(ifft2), unnormalised): y-passes, then x-passes
+//        whose first load rebuilds the Hermitian pair Z = A_2j + i*A_2j+1.
+//
+// Lengths are the reference's own padded grids (110 = 10*11 for 2D, 74, 42,
+// 60 ...), not powers of two: padding further would change the optimisation
+// problem the reference solves (SURVEY.md §7 "Hard parts").
+//
+// Every pass is in place: each thread keeps all of its butterflies of the pass
+// in registers between a "read all" and a "write all" barrier, so one slice
+// needs only its own footprint of LDS (98.6 KB at 110x110 in fp64).
+#pragma once
+
+#include "common.hpp"
+
+#include <utility>
+
+namespace ccsc {
+
+// ---------------------------------------------------------------------------
+// compile-time trig for the in-register DFT constants
+// ---------------------------------------------------------------------------
+constexpr double kPi = 3.14159265358979323846264338327950288;
+
+constexpr double series_sin(double x) {  // |x| <= pi/4
+  double t = x, s = x;
+  for (int i = 1; i < 14; ++i) {
+    t *= -x * x / ((2 * i) * (2 * i + 1));
+    s += t;
+  }
+  return s;
+}
+constexpr double series_cos(double x) {  // |x| <= pi/4
+  double t = 1.0, s = 1.0;
+  for (int i = 1; i < 14; ++i) {
+    t *= -x * x / ((2 * i - 1) * (2 * i));
+    s += t;
+  }
+  return s;
+}
+// cos / sin of 2*pi*m/R with octant reduction done in exact integer arithmetic.
+constexpr void turn_cos_sin(int m, int R, double& c, double& s) {
+  m %= R;
+  if (m < 0) m += R;
+  // t = m / R in [0,1)
+  double sc = 1.0, ss = 1.0;
+  int num = m, den = R;  // t = num/den
+  if (2 * num > den) {   // t > 1/2: sin(t) = -sin(1-t), cos(t) = cos(1-t)
+    num = den - num;
+    ss = -ss;
+  }
+  bool swap = false;
+  if (4 * num > den) {   // t in (1/4,1/2]: cos(t) = -cos(1/2-t), sin(t) = sin(1/2-t)
+    num = den - 2 * num;
+    den *= 2;
+    sc = -sc;
+  }
+  if (8 * num > den) {   // t in (1/8,1/4]: swap to 1/4 - t
+    num = den - 4 * num;
+    den *= 4;
+    swap = true;
+  }
+  const double x = 2.0 * kPi * (double)num / (double)den;
+  const double cx = series_cos(x), sx = series_sin(x);
+  c = sc * (swap ? sx : cx);
+  s = ss * (swap ? cx : sx);
+}
+
+constexpr double turn_cos(int m, int R) {
+  double c = 0, s = 0;
+  turn_cos_sin(m, R, c, s);
+  return c;
+}
+constexpr double turn_sin(int m, int R) {
+  double c = 0, s = 0;
+  turn_cos_sin(m, R, c, s);
+  return s;
+}
+// cos/sin(2*pi*M/R) as compile-time immediates
+template <int R, int M> struct TC {
+  static constexpr double c = turn_cos(M, R);
+  static constexpr double s = turn_sin(M, R);
+};
+
+// compile-time loop: f(std::integral_constant<int, 0..N-1>)
+template <typename Fn, int... I>
+__device__ __forceinline__ void sfor_impl(Fn&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename Fn>
+__device__ __forceinline__ void sfor(Fn&& f) {
+  sfor_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// ---------------------------------------------------------------------------
+// In-register DFT of size R:  out[q] = sum_r v[r] * exp(SIGN*2*pi*i*r*q/R).
+// Odd/even pairing (r, R-r) halves the multiplies of the direct form.
+// ---------------------------------------------------------------------------
+template <typename T, int R, int SIGN>
+__device__ __forceinline__ void dft(cpx<T> (&v)[R]) {
+  if constexpr (R == 1) {
+    return;
+  } else if constexpr (R == 2) {
+    const cpx<T> a = v[0], b = v[1];
+    v[0] = cadd(a, b);
+    v[1] = csub(a, b);
+  } else if constexpr (R == 4) {
+    const cpx<T> a0 = cadd(v[0], v[2]), a1 = csub(v[0], v[2]);
+    const cpx<T> b0 = cadd(v[1], v[3]), b1 = csub(v[1], v[3]);
+    // b1 * (SIGN*i)
+    const cpx<T> b1i = {-(T)SIGN * b1.y, (T)SIGN * b1.x};
+    v[0] = cadd(a0, b0);
+    v[2] = csub(a0, b0);
+    v[1] = cadd(a1, b1i);
+    v[3] = csub(a1, b1i);
+  } else {
+    constexpr int H = (R - 1) / 2;
+    constexpr bool EVEN = (R % 2) == 0;
+    cpx<T> a[H + 1], b[H + 1];
+    sfor<H>([&](auto ri) {
+      constexpr int r = decltype(ri)::value + 1;
+      a[r] = cadd(v[r], v[R - r]);
+      b[r] = csub(v[r], v[R - r]);
+    });
+    cpx<T> out[R];
+    {
+      cpx<T> s0 = v[0];
+      sfor<H>([&](auto ri) { s0 = cadd(s0, a[decltype(ri)::value + 1]); });
+      if constexpr (EVEN) s0 = cadd(s0, v[R / 2]);
+      out[0] = s0;
+    }
+    sfor<H>([&](auto qi) {
+      constexpr int q = decltype(qi)::value + 1;
+      cpx<T> re = v[0];
+      cpx<T> im = {(T)0, (T)0};
+      sfor<H>([&](auto ri) {
+        constexpr int r = decltype(ri)::value + 1;
+        constexpr int m = (r * q) % R;
+        constexpr T c = (T)TC<R, m>::c;
+        constexpr T s = (T)TC<R, m>::s;
+        re.x += a[r].x * c;
+        re.y += a[r].y * c;
+        im.x += b[r].x * s;
+        im.y += b[r].y * s;
+      });
+      if constexpr (EVEN) {
+        if constexpr (q & 1) re = csub(re, v[R / 2]);
+        else re = cadd(re, v[R / 2]);
+      }
+      // SIGN * i * im = (-SIGN*im.y, SIGN*im.x)
+      const cpx<T> ii = {-(T)SIGN * im.y, (T)SIGN * im.x};
+      out[q] = cadd(re, ii);
+      out[R - q] = csub(re, ii);
+    });
+    if constexpr (EVEN) {
+      cpx<T> s0 = v[0];
+      sfor<H>([&](auto ri) {
+        constexpr int r = decltype(ri)::value + 1;
+        if constexpr (r & 1) s0 = csub(s0, a[r]);
+        else s0 = cadd(s0, a[r]);
+      });
+      if constexpr ((R / 2) & 1) s0 = csub(s0, v[R / 2]);
+      else s0 = cadd(s0, v[R / 2]);
+      out[R / 2] = s0;
+    }
+    sfor<R>([&](auto qi) { v[decltype(qi)::value] = out[decltype(qi)::value]; });
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Geometry of a batch of lines inside the LDS slice (units of T).
+// ---------------------------------------------------------------------------
+struct LineGeom {
+  int nlines;   // number of independent 1D transforms
+  int lstride;  // distance between consecutive lines
+  int estride;  // distance between consecutive elements of a line
+  int imoff;    // offset of the imaginary part from the real part
+};
+
+constexpr int kMaxPass = 3;
+struct Plan1D {
+  int n;
+  int npass;
+  int rad[kMaxPass];
+};
+
+// Per-slice description of the 2D grid (all in units of T unless noted).
+struct Grid2D {
+  int X, Y;     // padded grid (MATLAB dim 1 = x fastest, dim 2 = y)
+  int Xh;       // X/2 + 1 half-spectrum columns
+  int RS;       // LDS row stride in T = 2*Xh
+  int Yp;       // rows rounded up to even (column pairs = Yp/2)
+  int F;        // Xh * Y half-spectrum bins, layout [y][x'] (x' fastest)
+  Plan1D px, py;
+  int twx, twy; // offsets (complex units) of exp(-2 pi i m/X), exp(-2 pi i m/Y)
+                // inside the twiddle table
+};
+
+// Load-decoding modes of the first pass of a direction.
+constexpr int kModePlain = 0;
+constexpr int kModeSplitToHalf = 1;   // y-forward: two-for-one separation
+constexpr int kModeHermPair = 2;      // x-inverse: Z = A_2j + i*A_2j+1 (Hermitian ext.)
+
+template <typename T>
+__device__ __forceinline__ cpx<T> load_elem(const T* lds, const LineGeom& g, const Grid2D& G,
+                                            int mode, int line, int e) {
+  if (mode == kModePlain) {
+    const T* p = lds + line * g.lstride + e * g.estride;
+    return {p[0], p[g.imoff]};
+  } else if (mode == kModeSplitToHalf) {
+    // line = x' (half-spectrum column), e = y.  Pair j = y/2 holds rows 2j, 2j+1
+    // transformed together along x in split format.
+    const int j = e >> 1;
+    const int x1 = line;
+    const int x2 = (line == 0) ? 0 : G.X - line;
+    const T* r0 = lds + (2 * j) * G.RS;
+    const T* r1 = r0 + G.RS;
+    const cpx<T> z1 = {r0[x1], r1[x1]};
+    const cpx<T> z2 = {r0[x2], r1[x2]};
+    if ((e & 1) == 0) return {(T)0.5 * (z1.x + z2.x), (T)0.5 * (z1.y - z2.y)};
+    // -i/2 * (z1 - conj z2)
+    return {(T)0.5 * (z1.y + z2.y), (T)-0.5 * (z1.x - z2.x)};
+  } else {
+    // line = pair j, e = x.  Rows 2j, 2j+1 hold interleaved half spectra.
+    const int j = line;
+    const bool hi = e >= G.Xh;
+    const int c = hi ? G.X - e : e;
+    const T* r0 = lds + (2 * j) * G.RS + 2 * c;
+    cpx<T> a = {r0[0], r0[1]};
+    cpx<T> b = {(T)0, (T)0};
+    if (2 * j + 1 < G.Y) b = {r0[G.RS], r0[G.RS + 1]};
+    if (hi) {
+      a.y = -a.y;
+      b.y = -b.y;
+    }
+    return {a.x - b.y, a.y + b.x};
+  }
+}
+
+// One Stockham radix-R pass over all lines, in place.
+template <typename T, int R, int MAXB, int SIGN>
+__device__ __forceinline__ void fft_pass(T* lds, int mode, const LineGeom& gin,
+                                         const LineGeom& gout, const Grid2D& G, int n, int Ns,
+                                         const cpx<T>* __restrict__ tw) {
+  const int nb = n / R;
+  const int total = gin.nlines * nb;
+  const int step = n / (Ns * R);
+  cpx<T> v[MAXB][R];
+  int outbase[MAXB];
+  // read phase: load, twiddle (so no twiddle stays live across the barrier)
+#pragma unroll
+  for (int b = 0; b < MAXB; ++b) {
+    const int bf = (int)threadIdx.x + b * kNT;
+    outbase[b] = -1;
+    if (bf < total) {
+      const int line = bf / nb;
+      const int j = bf - line * nb;
+      const int k = j % Ns;
+      outbase[b] = line * gout.lstride + ((j - k) * R + k) * gout.estride;
+      v[b][0] = load_elem<T>(lds, gin, G, mode, line, j);
+#pragma unroll
+      for (int r = 1; r < R; ++r) {
+        const cpx<T> x = load_elem<T>(lds, gin, G, mode, line, j + r * nb);
+        if (Ns > 1) {
+          cpx<T> w = tw[r * k * step];
+          if (SIGN > 0) w.y = -w.y;
+          v[b][r] = cmul(x, w);
+        } else {
+          v[b][r] = x;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  const int ostride = Ns * gout.estride;
+#pragma unroll
+  for (int b = 0; b < MAXB; ++b) {
+    if (outbase[b] >= 0) {
+      dft<T, R, SIGN>(v[b]);
+      T* base = lds + outbase[b];
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        T* p = base + r * ostride;
+        p[0] = v[b][r].x;
+        p[gout.imoff] = v[b][r].y;
+      }
+    }
+  }
+  __syncthreads();
+}
+
+template <typename T, int MAXB, int SIGN>
+__device__ __forceinline__ void fft_pass_dispatch(int R, T* lds, int mode, const LineGeom& gin,
+                                                  const LineGeom& gout, const Grid2D& G, int n,
+                                                  int Ns, const cpx<T>* tw) {
+  switch (R) {
+    case 2: fft_pass<T, 2, MAXB, SIGN>(lds, mode, gin, gout, G, n, Ns, tw); break;
+    case 3: fft_pass<T, 3, MAXB, SIGN>(lds, mode, gin, gout, G, n, Ns, tw); break;
+    case 4: fft_pass<T, 4, MAXB, SIGN>(lds, mode, gin, gout, G, n, Ns, tw); break;
+    case 5: fft_pass<T, 5, MAXB, SIGN>(lds, mode, gin, gout, G, n, Ns, tw); break;
+    case 7: fft_pass<T, 7, MAXB, SIGN>(lds, mode, gin, gout, G, n, Ns, tw); break;
+    case 8: fft_pass<T, 8, MAXB, SIGN>(lds, mode, gin, gout, G, n, Ns, tw); break;
+    case 10: fft_pass<T, 10, MAXB, SIGN>(lds, mode, gin, gout, G, n, Ns, tw); break;
+    case 11: fft_pass<T, 11, MAXB, SIGN>(lds, mode, gin, gout, G, n, Ns, tw); break;
+    default: break;  // host planner only emits the radices above (kRadices in engine.cpp)
+  }
+}
+
+// All passes of one direction; the first pass decodes its loads with `mode0`.
+// The passes are unrolled into kMaxPass guarded slots: a runtime pass loop
+// around the radix switch makes the AMDGPU structurizer keep every case's
+// registers live (256 VGPRs + scratch); unrolled slots compile to ~134 VGPRs.
+// `n` is laundered through an empty asm: inside a caller's loop (the K loop of
+// the fused kernels) LICM would otherwise hoist every pass's loop-invariant
+// index math out of the loop and keep it live in registers (256 VGPRs + 5 KB
+// of scratch per lane).
+template <typename T, int MAXB, int SIGN>
+__device__ __forceinline__ void fft_dir(T* lds, int mode0, const LineGeom& gfirst,
+                                        const LineGeom& g, const Grid2D& G, const Plan1D& p,
+                                        const cpx<T>* tw) {
+  int Ns = 1;
+  int n = p.n;
+  asm volatile("" : "+s"(n));
+  sfor<kMaxPass>([&](auto si) {
+    constexpr int s = decltype(si)::value;
+    if (s < p.npass) {
+      const int R = p.rad[s];
+      if constexpr (s == 0) fft_pass_dispatch<T, MAXB, SIGN>(R, lds, mode0, gfirst, g, G, n, Ns, tw);
+      else fft_pass_dispatch<T, MAXB, SIGN>(R, lds, kModePlain, g, g, G, n, Ns, tw);
+      Ns *= R;
+    }
+  });
+}
+
+__device__ __forceinline__ LineGeom geom_xsplit(const Grid2D& G) {
+  return {G.Yp / 2, 2 * G.RS, 1, G.RS};
+}
+__device__ __forceinline__ LineGeom geom_ycols(const Grid2D& G) {
+  return {G.Xh, 2, G.RS, 1};
+}
+
+// Forward 2D R2C of the real slice in LDS rows [y*RS, y*RS+X) (rows Y..Yp-1 zero).
+// Result: interleaved half spectrum, bin (x', y) at lds[y*RS + 2x'].
+template <typename T, int MAXB>
+__device__ __forceinline__ void slice_r2c(T* lds, const Grid2D& G, const cpx<T>* tw) {
+  const LineGeom gx = geom_xsplit(G);
+  const LineGeom gy = geom_ycols(G);
+  __syncthreads();
+  fft_dir<T, MAXB, -1>(lds, kModePlain, gx, gx, G, G.px, tw + G.twx);
+  fft_dir<T, MAXB, -1>(lds, kModeSplitToHalf, gy, gy, G, G.py, tw + G.twy);
+}
+
+// Inverse 2D C2R (unnormalised) of the interleaved half spectrum in LDS.
+// Result: real rows [y*RS, y*RS+X).
+template <typename T, int MAXB>
+__device__ __forceinline__ void slice_c2r(T* lds, const Grid2D& G, const cpx<T>* tw) {
+  const LineGeom gx = geom_xsplit(G);
+  const LineGeom gy = geom_ycols(G);
+  __syncthreads();
+  fft_dir<T, MAXB, +1>(lds, kModePlain, gy, gy, G, G.py, tw + G.twy);
+  fft_dir<T, MAXB, +1>(lds, kModeHermPair, gx, gx, G, G.px, tw + G.twx);
+}
+
+}  // namespace ccsc

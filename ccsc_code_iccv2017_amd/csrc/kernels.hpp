@@ -1,0 +1,68 @@
+// Host-visible launchers of the libccsc device kernels.
+#pragma once
+
+#include "fft.hpp"
+
+namespace ccsc {
+
+size_t slice_smem_bytes(const Grid2D& G, size_t tsize);
+int pick_nb(int F);
+
+// ---- kernels2d.hip -------------------------------------------------------
+template <typename T>
+hipError_t launch_r2c_embed(const T* src, int64_t src_slice, int sx, int sy, int ox, int oy,
+                            cpx<T>* dst, int64_t dst_slice, int64_t count, const cpx<T>* tw,
+                            const Grid2D& G, hipStream_t st);
+template <typename T>
+hipError_t launch_c2r_plain(const cpx<T>* src, int64_t src_slice, T* dst, int64_t dst_slice,
+                            int64_t count, const cpx<T>* tw, const Grid2D& G, T scale,
+                            hipStream_t st);
+template <typename T>
+hipError_t launch_dual_r2c(const T* D, T* yD, const T* Usup, cpx<T>* Ch, int64_t nslices,
+                           const cpx<T>* tw, const Grid2D& G, int K, int r, hipStream_t st);
+template <typename T>
+hipError_t launch_c2r_dout(const cpx<T>* Dh, T* D, const T* yD, T* supp, T* dnorm, int nfirst,
+                           int64_t nslices, const cpx<T>* tw, const Grid2D& G, int r,
+                           hipStream_t st);
+template <typename T>
+hipError_t launch_supp_reduce(const T* supp, T* ssum, int nbl, int per_block, hipStream_t st);
+template <typename T>
+hipError_t launch_project(const T* ssum, T* Usup, int ngroups, int glen, T invN,
+                          hipStream_t st);
+template <typename T>
+hipError_t launch_sden(const cpx<T>* dhat, T* sden, int F, int K, T rho, T invP,
+                       hipStream_t st);
+template <typename T>
+hipError_t launch_zstep(T* z, T* yz, T* cbuf, const cpx<T>* Bhat, const cpx<T>* dhat,
+                        const T* sden, int64_t npatch, const cpx<T>* tw, const Grid2D& G, int K,
+                        T theta, T* znorm, bool tol, hipStream_t st);
+template <typename T>
+hipError_t launch_objective(const T* z, const cpx<T>* dhat, const T* b, int sbx, int sby, int r,
+                            T* DZ, T* part, int64_t npatch, const cpx<T>* tw, const Grid2D& G,
+                            int K, hipStream_t st);
+template <typename T>
+hipError_t launch_sum_pairs(const T* part, int count, T* out, hipStream_t st);
+
+// ---- dstep.hip ------------------------------------------------------------
+// Per frequency f of one block: G = A^H A + rho I (A = ni x K code spectra),
+// h = A^H b, Cholesky G = L L^H; L packed lower column-major per f.
+template <typename T>
+hipError_t launch_gram_chol(const cpx<T>* Zh, const cpx<T>* Bh, cpx<T>* L, cpx<T>* h, int F,
+                            int K, int ni, T rho, hipStream_t st);
+// x_f = (L L^H)^{-1} (h_f + rho * C_f) for every (block, f); writes Dh [blk][K][F].
+template <typename T>
+hipError_t launch_dsolve(const cpx<T>* L, const cpx<T>* h, const cpx<T>* Ch, cpx<T>* Dh,
+                         int nblocks, int F, int K, T rho, hipStream_t st);
+
+// ---- util.hip ---------------------------------------------------------------
+template <typename T>
+hipError_t launch_randn(T* out, int64_t count, uint64_t seed, uint64_t offset, hipStream_t st);
+// Embed [psf,psf,K] filters (column-major) into nrep copies of the [K][Y][X] grid
+// at circshift(-r) positions (dP:38-39).
+template <typename T>
+hipError_t launch_embed_filters(const T* d0, T* D, int nrep, int K, int psf, const Grid2D& G,
+                                hipStream_t st);
+template <typename T>
+hipError_t launch_replicate(const T* src, T* dst, int64_t n, int nrep, hipStream_t st);
+
+}  // namespace ccsc

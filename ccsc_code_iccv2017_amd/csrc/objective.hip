@@ -1,0 +1,108 @@
+// Objective / DZ kernel (reporting only; excluded from tim_vals like the
+// reference, dP:122 vs dP:127).
+#include "slice.hpp"
+
+namespace ccsc {
+
+int pick_nb(int F) {
+  const int need = (F + kNT - 1) / kNT;
+  const int opts[] = {2, 6, 13};
+  for (int o : opts)
+    if (o >= need) return o;
+  return -1;
+}
+
+// ---------------------------------------------------------------------------
+// Objective / DZ, one workgroup per patch (dP:305-324, dP:193):
+//   Dz = real(ifft2(sum_k fft2(z_k) .* dhat_k));
+//   part[p] = { ||crop(Dz) - b_p||^2, sum |z_p| }
+// b: [np][sby][sbx]; DZ (nullable): [np][Y][X] uncropped.
+// ---------------------------------------------------------------------------
+template <typename T, int NB>
+__global__ __launch_bounds__(kNT) void k_objective(const T* __restrict__ z,
+                                                   const cpx<T>* __restrict__ dhat,
+                                                   const T* __restrict__ b, int sbx, int sby,
+                                                   int r, T* __restrict__ DZ,
+                                                   T* __restrict__ part,
+                                                   const cpx<T>* __restrict__ twg, Grid2D G,
+                                                   int K) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  Smem<T> S = carve<T>(smem, G);
+  load_twiddles(S.tw, twg, G.X + G.Y);
+  const int p = blockIdx.x;
+  const int P = G.X * G.Y;
+  const int F = G.F;
+  cpx<T> acc[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) acc[i] = {(T)0, (T)0};
+  T l1 = 0;
+  for (int k = 0; k < K; ++k) {
+    const int64_t off = ((int64_t)p * K + k) * P;
+    __syncthreads();
+    for (int e = threadIdx.x; e < P; e += kNT) {
+      const int y = e / G.X, x = e - y * G.X;
+      const T v = z[off + e];
+      l1 += fabs(v);
+      S.slice[y * G.RS + x] = v;
+    }
+    zero_pad_row(S.slice, G);
+    slice_r2c<T, 2>(S.slice, G, S.tw);
+    const cpx<T>* dk = dhat + (int64_t)k * F;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int f = threadIdx.x + i * kNT;
+      if (f < F) acc[i] = cadd(acc[i], cmul(dk[f], cpx<T>{S.slice[2 * f], S.slice[2 * f + 1]}));
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int f = threadIdx.x + i * kNT;
+    if (f < F) {
+      S.slice[2 * f] = acc[i].x;
+      S.slice[2 * f + 1] = acc[i].y;
+    }
+  }
+  slice_c2r<T, 2>(S.slice, G, S.tw);
+  const T invP = (T)1 / (T)P;
+  if (DZ) {
+    T* o = DZ + (int64_t)p * P;
+    for (int e = threadIdx.x; e < P; e += kNT) {
+      const int y = e / G.X, x = e - y * G.X;
+      o[e] = S.slice[y * G.RS + x] * invP;
+    }
+  }
+  T sq = 0;
+  const T* bp = b + (int64_t)p * sbx * sby;
+  for (int e = threadIdx.x; e < sbx * sby; e += kNT) {
+    const int y = e / sbx, x = e - y * sbx;
+    const T d = S.slice[(y + r) * G.RS + x + r] * invP - bp[e];
+    sq += d * d;
+  }
+  sq = block_sum(sq, S.red);
+  l1 = block_sum(l1, S.red);
+  if (threadIdx.x == 0) {
+    part[2 * p] = sq;
+    part[2 * p + 1] = l1;
+  }
+}
+
+template <typename T>
+hipError_t launch_objective(const T* z, const cpx<T>* dhat, const T* b, int sbx, int sby, int r,
+                            T* DZ, T* part, int64_t npatch, const cpx<T>* tw, const Grid2D& G,
+                            int K, hipStream_t st) {
+  if (npatch <= 0) return hipSuccess;
+  const size_t sm = slice_smem_bytes(G, sizeof(T));
+  const int nbv = pick_nb(G.F);
+  CCSC_NB_SWITCH(nbv, hipLaunchKernelGGL((k_objective<T, NB>), dim3((unsigned)npatch),
+                                         dim3(kNT), sm, st, z, dhat, b, sbx, sby, r, DZ, part,
+                                         tw, G, K));
+  return hipGetLastError();
+}
+
+template hipError_t launch_objective<double>(const double*, const cpx<double>*, const double*,
+                                             int, int, int, double*, double*, int64_t,
+                                             const cpx<double>*, const Grid2D&, int,
+                                             hipStream_t);
+
+}  // namespace ccsc

@@ -1,0 +1,291 @@
+"""Python mirror of the reference learners' interface over the libccsc C-ABI.
+
+Same names, argument order, argument meaning and return tuples as the MATLAB
+functions they replace (what a MEX wrapper would expose):
+
+  d_res, z_res, DZ, iterations = admm_learn_conv2D_large_dParallel(
+      b, kernel_size, lambda_residual, lambda_prior, max_it, tol, verbose, init)
+                                   # 2D/admm_learn_conv2D_large_dParallel.m:1-4
+  d_res, z_res, DZ, iterations = admm_learn_conv2D_large_dzParallel(...)
+                                   # 2D/admm_learn_conv2D_large_dzParallel.m:1-4
+
+Arrays carry the MATLAB shapes (b: [x, y, n]; kernel_size = [psf, psf, K];
+d_res: [psf, psf, K]; z_res: [X, Y, K, n]; DZ: [X, Y, 1, n]) and are exchanged
+column-major, so a Fortran-ordered NumPy array is bit-for-bit an mxArray.
+
+``init`` (ignored by the reference, Q11) is honoured: ``{'d': [psf,psf,K],
+'z': size_z}`` (dZ: ``size_z_crop`` = [X, Y, K, ni], replicated per block).
+With ``init=None`` the engine draws d0/z0 on the device from ``seed``.
+
+Errors are raised as ``CCSCError`` (the MATLAB reference raises on bad shapes
+too; ``n % ni != 0`` is an error here rather than a silent floor, Q13).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+
+import numpy as np
+
+from . import _lib as L
+
+
+class Context:
+    """One GPU (one rank).  ``uid`` (128 bytes from ``unique_id()`` on rank 0)
+    is needed when ``nranks > 1``; the consensus then runs over RCCL."""
+
+    def __init__(self, device: int = 0, rank: int = 0, nranks: int = 1, uid: bytes | None = None):
+        self._lib = L.lib()
+        eb = L.errbuf()
+        self.ptr = self._lib.ccsc_create(device, rank, nranks, uid, eb, len(eb))
+        if not self.ptr:
+            raise L.CCSCError(L.CCSC_E_HIP, eb.value.decode(errors="replace"))
+        self.device, self.rank, self.nranks = device, rank, nranks
+
+    def close(self):
+        if self.ptr:
+            self._lib.ccsc_destroy(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+
+def unique_id() -> bytes:
+    eb = L.errbuf()
+    buf = C.create_string_buffer(128)
+    L.check(L.lib().ccsc_get_unique_id(buf, eb, len(eb)), eb)
+    return buf.raw
+
+
+_VARIANT_FOR = {
+    "dParallel": L.CCSC_DPAR,
+    "dzParallel": L.CCSC_DZPAR,
+}
+
+
+def make_problem(variant, b_shape, kernel_size, lambda_residual, lambda_prior, max_it, tol,
+                 verbose, *, ni=None, max_it_d=None, max_it_z=None, rho_d=None, rho_z=None,
+                 theta_div=None, trace_objective=False, seed=0, precision="fp64"):
+    p = L.Problem()
+    p.variant = variant
+    p.ndim = 2
+    p.sb[0], p.sb[1] = int(b_shape[0]), int(b_shape[1])
+    p.views[0] = p.views[1] = 1
+    p.n = int(b_shape[-1])
+    p.K = int(kernel_size[-1])
+    p.psf = int(kernel_size[0])
+    p.lambda_residual = float(lambda_residual)
+    p.lambda_prior = float(lambda_prior)
+    p.max_it = int(max_it)
+    p.tol = float(tol)
+    if verbose not in L.VERBOSE:
+        raise ValueError(f"verbose must be one of {sorted(L.VERBOSE)}")
+    p.verbose = L.VERBOSE[verbose]
+    p.ni = int(ni or 0)
+    p.max_it_d = int(max_it_d or 0)
+    p.max_it_z = int(max_it_z or 0)
+    p.rho_d = float(rho_d or 0)
+    p.rho_z = float(rho_z or 0)
+    p.theta_div = float(theta_div or 0)
+    p.precision = L.CCSC_FP64 if precision == "fp64" else L.CCSC_FP32
+    p.trace_objective = 1 if trace_objective else 0
+    p.seed = int(seed)
+    return p
+
+
+def resolve(p: L.Problem) -> L.Problem:
+    """Fill the variant defaults and validate; host only."""
+    q = L.Problem.from_buffer_copy(p)
+    eb = L.errbuf()
+    L.check(L.lib().ccsc_resolve(C.byref(q), eb, len(eb)), eb)
+    return q
+
+
+def shard(p: L.Problem, rank: int, nranks: int):
+    eb = L.errbuf()
+    b0, nb = C.c_int64(), C.c_int64()
+    L.check(L.lib().ccsc_shard(C.byref(p), rank, nranks, C.byref(b0), C.byref(nb), eb, len(eb)), eb)
+    return b0.value, nb.value
+
+
+def plan_bytes(p: L.Problem, rank: int = 0, nranks: int = 1) -> int:
+    eb = L.errbuf()
+    out = C.c_uint64()
+    L.check(L.lib().ccsc_plan_bytes(C.byref(p), rank, nranks, C.byref(out), eb, len(eb)), eb)
+    return out.value
+
+
+def _f64(a):
+    return None if a is None else np.asfortranarray(np.asarray(a, dtype=np.float64))
+
+
+class Session:
+    """Stateful learner (warm restart, bench): create -> step(k) -> results."""
+
+    def __init__(self, ctx: Context, p: L.Problem, b, d0=None, z0=None):
+        self.ctx = ctx
+        self.p = resolve(p)
+        self._b = _f64(b)
+        self._d0 = _f64(d0)
+        self._z0 = _f64(z0)
+        eb = L.errbuf()
+        self.ptr = L.lib().ccsc_session_create(ctx.ptr, C.byref(self.p), L.dptr(self._b),
+                                               L.dptr(self._d0), L.dptr(self._z0), eb, len(eb))
+        if not self.ptr:
+            raise L.CCSCError(L.CCSC_E_INVALID, eb.value.decode(errors="replace"))
+        b0, nb = shard(self.p, ctx.rank, ctx.nranks)
+        self.block_begin, self.nblocks = b0, nb
+        self.n_local = nb * self.p.ni
+        self.outer = 0
+
+    def step(self, n_outer: int = 1) -> bool:
+        eb = L.errbuf()
+        done = C.c_int32(0)
+        L.check(L.lib().ccsc_session_step(self.ptr, n_outer, C.byref(done), eb, len(eb)), eb)
+        self.outer += n_outer
+        return bool(done.value)
+
+    def objective(self) -> float:
+        eb = L.errbuf()
+        v = C.c_double()
+        L.check(L.lib().ccsc_session_objective(self.ptr, C.byref(v), eb, len(eb)), eb)
+        return v.value
+
+    def set_profiling(self, on: bool):
+        L.check(L.lib().ccsc_session_set_profiling(self.ptr, 1 if on else 0), L.errbuf())
+
+    def kernel_stats(self, kernel_id: int):
+        eb = L.errbuf()
+        n = C.c_int64()
+        ms = C.c_double()
+        by = C.c_double()
+        L.check(L.lib().ccsc_session_kernel_stats(self.ptr, kernel_id, C.byref(n), C.byref(ms),
+                                                  C.byref(by), eb, len(eb)), eb)
+        return n.value, ms.value, by.value
+
+    def grid(self):
+        r = self.p.psf // 2
+        return self.p.sb[0] + 2 * r, self.p.sb[1] + 2 * r
+
+    def results(self, want_z=True, want_DZ=True, want_obj=False):
+        X, Y = self.grid()
+        p = self.p
+        d_res = np.zeros((p.psf, p.psf, p.K), order="F")
+        z_res = np.zeros((X, Y, p.K, self.n_local), order="F") if want_z else None
+        DZ = np.zeros((X, Y, 1, self.n_local), order="F") if want_DZ else None
+        obj = np.zeros(1) if want_obj else None
+        out = L.Outputs(L.dptr(d_res), L.dptr(z_res), L.dptr(DZ), L.dptr(obj))
+        eb = L.errbuf()
+        L.check(L.lib().ccsc_session_results(self.ptr, C.byref(out), eb, len(eb)), eb)
+        return d_res, z_res, DZ, (float(obj[0]) if want_obj else None)
+
+    def iterlog(self, capacity=None):
+        p = self.p
+        cap = capacity or (self.outer + 1)
+        a = {k: np.full(cap, np.nan) for k in ("obj_vals_d", "obj_vals_z", "tim_vals")}
+        tr = {
+            "obj_d": np.full(cap * p.max_it_d, np.nan),
+            "obj_z": np.full(cap * p.max_it_z, np.nan),
+            "d_diff": np.full(cap * p.max_it_d, np.nan),
+            "z_diff": np.full(cap * p.max_it_z, np.nan),
+        }
+        nd = np.zeros(cap, dtype=np.int32)
+        nz = np.zeros(cap, dtype=np.int32)
+        lg = L.IterLog(cap, 0, L.dptr(a["obj_vals_d"]), L.dptr(a["obj_vals_z"]),
+                       L.dptr(a["tim_vals"]), L.dptr(tr["obj_d"]), L.dptr(tr["obj_z"]),
+                       L.dptr(tr["d_diff"]), L.dptr(tr["z_diff"]), L.iptr(nd), L.iptr(nz))
+        eb = L.errbuf()
+        L.check(L.lib().ccsc_session_iterlog(self.ptr, C.byref(lg), eb, len(eb)), eb)
+        cnt = lg.count
+        it = {k: v[:cnt].copy() for k, v in a.items()}
+        nout = max(cnt - 1, 0)
+        it["trace"] = {
+            "obj_d": tr["obj_d"][: nout * p.max_it_d].reshape(nout, p.max_it_d),
+            "obj_z": tr["obj_z"][: nout * p.max_it_z].reshape(nout, p.max_it_z),
+            "d_diff": tr["d_diff"][: nout * p.max_it_d].reshape(nout, p.max_it_d),
+            "z_diff": tr["z_diff"][: nout * p.max_it_z].reshape(nout, p.max_it_z),
+            "n_d": nd[:nout].copy(),
+            "n_z": nz[:nout].copy(),
+        }
+        return it
+
+    def close(self):
+        if self.ptr:
+            L.lib().ccsc_session_destroy(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _learn_2d(variant, b, kernel_size, lambda_residual, lambda_prior, max_it, tol, verbose, init,
+              ctx=None, device=0, want_z=True, want_DZ=True, **kw):
+    b = np.asarray(b, dtype=np.float64)
+    if b.ndim == 2:
+        b = b[:, :, None]
+    if b.ndim != 3:
+        raise ValueError("b must be [x, y, n]")
+    own = ctx is None
+    if own:
+        ctx = Context(device)
+    try:
+        p = make_problem(variant, b.shape, kernel_size, lambda_residual, lambda_prior, max_it, tol,
+                         verbose, **kw)
+        d0 = z0 = None
+        if init is not None and len(init) > 0:
+            d0 = init.get("d")
+            z0 = init.get("z")
+        s = Session(ctx, p, b, d0, z0)
+        try:
+            done = False
+            while s.outer < s.p.max_it and not done:
+                done = s.step(1)
+            d_res, z_res, DZ, _ = s.results(want_z=want_z, want_DZ=want_DZ)
+            iterations = s.iterlog()
+        finally:
+            s.close()
+    finally:
+        if own:
+            ctx.close()
+    return d_res, z_res, DZ, iterations
+
+
+def admm_learn_conv2D_large_dParallel(b, kernel_size, lambda_residual, lambda_prior, max_it, tol,
+                                      verbose, init=None, **kw):
+    """Drop-in for 2D/admm_learn_conv2D_large_dParallel.m:1-199."""
+    return _learn_2d(L.CCSC_DPAR, b, kernel_size, lambda_residual, lambda_prior, max_it, tol,
+                     verbose, init, **kw)
+
+
+def admm_learn_conv2D_large_dzParallel(b, kernel_size, lambda_residual, lambda_prior, max_it, tol,
+                                       verbose, init=None, **kw):
+    """Drop-in for 2D/admm_learn_conv2D_large_dzParallel.m:1-206."""
+    return _learn_2d(L.CCSC_DZPAR, b, kernel_size, lambda_residual, lambda_prior, max_it, tol,
+                     verbose, init, **kw)
+
+
+def fft2d_test(ctx: Context, slices):
+    """Kernel-level check: R2C half spectra + C2R round trip of [X, Y, count] slices."""
+    a = np.asfortranarray(np.asarray(slices, dtype=np.float64))
+    X, Y, cnt = a.shape
+    Xh = X // 2 + 1
+    hs = np.zeros(2 * Xh * Y * cnt)
+    rt = np.zeros_like(a, order="F")
+    eb = L.errbuf()
+    L.check(L.lib().ccsc_test_fft2d(ctx.ptr, X, Y, cnt, L.dptr(a), L.dptr(hs), L.dptr(rt), eb,
+                                    len(eb)), eb)
+    h = hs.view(np.complex128).reshape(cnt, Y, Xh)          # [slice][y][x']
+    return np.transpose(h, (2, 1, 0)), rt                     # [x', y, slice]

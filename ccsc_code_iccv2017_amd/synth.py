@@ -1,0 +1,111 @@
+"""Synthetic learner inputs -- the reference's drivers read
+image/video/light-field datasets that are not available here, so the bench and
+tests use seeded synthetic data of the same shapes:
+
+  * ground-truth filters: K random psf^d arrays, zero mean, unit norm
+  * codes: Bernoulli(density) * N(0, 1) per pixel per filter
+  * b_raw = sum_k d*_k (*) z*_k + noise * N(0, 1)      ('valid' convolution)
+  * local contrast normalisation + zero mean, restating the 'local_cn' branch
+    of image_helpers/CreateImages.m:299-369 (13x13 Gaussian, sigma 3*1.591,
+    reflection padding of image_helpers/rconv2.m:22-58, std floored at its
+    median) and the ZERO_MEAN branch CreateImages.m:652-657.  Like the
+    reference, the normalised image is stored as single then widened to double
+    (CreateImages.m:367, :711).
+
+PyTorch is used only as an array library here (CPU for tests, the GPU for the
+10^4-patch bench config); it is data preparation, not the learner.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+import torch.nn.functional as Fnn
+
+
+def fspecial_gaussian(size: int = 13, sigma: float = 3 * 1.591) -> np.ndarray:
+    """MATLAB fspecial('gaussian', [size size], sigma)."""
+    h = (size - 1) / 2.0
+    x = np.arange(-h, h + 1)
+    g = np.exp(-(x[:, None] ** 2 + x[None, :] ** 2) / (2.0 * sigma * sigma))
+    g[g < np.finfo(float).eps * g.max()] = 0
+    return g / g.sum()
+
+
+def rconv2(large: torch.Tensor, small: np.ndarray) -> torch.Tensor:
+    """image_helpers/rconv2.m:22-58 on a batch [n, H, W]: reflect about the edge
+    pixels (edge not repeated), then conv2(..., 'valid')."""
+    sy, sx = small.shape
+    py, px = (sy - 1) // 2, (sx - 1) // 2
+    t = large[:, None]
+    t = Fnn.pad(t, (px, sx - 1 - px, py, sy - 1 - py), mode="reflect")
+    k = torch.as_tensor(np.ascontiguousarray(small[::-1, ::-1]), dtype=t.dtype, device=t.device)
+    return Fnn.conv2d(t, k[None, None])[:, 0]
+
+
+def local_cn(imgs: torch.Tensor) -> torch.Tensor:
+    """CreateImages.m:299-369 ('local_cn') then :652-657 (ZERO_MEAN) per image.
+
+    imgs: [n, H, W] float64 (rows = MATLAB dim 1).  Returns float64 values that
+    went through the reference's single-precision storage.
+    """
+    k = fspecial_gaussian(13, 3 * 1.591)
+    lmn = rconv2(imgs, k)
+    lmnsq = rconv2(imgs * imgs, k)
+    lvar = torch.clamp(lmnsq - lmn * lmn, min=0)
+    lstd = torch.sqrt(lvar)
+    n = imgs.shape[0]
+    flat = lstd.reshape(n, -1)
+    q = torch.sort(flat, dim=1).values
+    lq = int(math.floor(flat.shape[1] / 2 + 0.5))            # MATLAB round(length/2), 1-based
+    th = q[:, lq - 1].clone()
+    zero = th == 0
+    if bool(zero.any()):                                       # CI:337-345: median of nonzeros
+        for i in torch.nonzero(zero).flatten().tolist():
+            nz = q[i][q[i] != 0]
+            th[i] = nz[int(math.floor(nz.numel() / 2 + 0.5)) - 1] if nz.numel() else 0
+    lstd = torch.maximum(lstd, th[:, None, None])
+    lstd = torch.where(lstd == 0, torch.full_like(lstd, np.finfo(float).eps), lstd)
+    out = ((imgs - lmn) / lstd).to(torch.float32)              # I{image} = single(temp)
+    out = out - out.mean(dim=(1, 2), keepdim=True)             # ZERO_MEAN, in single
+    return out.to(torch.float64)
+
+
+def make_filters(K: int, psf: int, ndim: int, rng: np.random.Generator) -> np.ndarray:
+    d = rng.standard_normal((K,) + (psf,) * ndim)
+    d -= d.reshape(K, -1).mean(1).reshape((K,) + (1,) * ndim)
+    d /= np.linalg.norm(d.reshape(K, -1), axis=1).reshape((K,) + (1,) * ndim)
+    return d
+
+
+def images_2d(n: int, size=(100, 100), K: int = 100, psf: int = 11, seed: int = 2017,
+              density: float = 0.002, noise: float = 0.01, device: str = "cpu",
+              chunk: int = 256, local_cn_on: bool = True) -> np.ndarray:
+    """Synthetic contrast-normalised images, MATLAB layout [x, y, n] float64."""
+    rng = np.random.default_rng(seed)
+    d = make_filters(K, psf, 2, rng)                         # [K, psf, psf]  (x, y)
+    dw = torch.as_tensor(np.ascontiguousarray(d[:, ::-1, ::-1]), dtype=torch.float32,
+                         device=device)[None]                # conv2d weight [1, K, psf, psf]
+    H, W = size
+    out = np.empty((H, W, n), order="F")
+    for c0 in range(0, n, chunk):
+        m = min(chunk, n - c0)
+        crng = np.random.default_rng([seed, 1 + c0])         # per-chunk substream
+        shape = (m, K, H + psf - 1, W + psf - 1)
+        g = torch.Generator(device="cpu").manual_seed(int(crng.integers(2**62)))
+        mask = torch.rand(shape, generator=g) < density
+        codes = torch.where(mask, torch.randn(shape, generator=g), torch.zeros(()))
+        raw = Fnn.conv2d(codes.to(device=device, dtype=torch.float32), dw)[:, 0].double()
+        raw = raw + noise * torch.randn(raw.shape, generator=g).to(device=device, dtype=torch.float64)
+        img = local_cn(raw) if local_cn_on else raw
+        out[:, :, c0:c0 + m] = img.permute(1, 2, 0).cpu().numpy()
+    return out
+
+
+def init_2d(kernel_size, size_z, seed: int = 7):
+    """d0 = randn(kernel_size); z0 = randn(size_z) (dP:38,45 draw order)."""
+    rng = np.random.default_rng(seed)
+    d0 = rng.standard_normal(tuple(kernel_size))
+    z0 = rng.standard_normal(tuple(size_z))
+    return {"d": d0, "z": z0}

@@ -1,0 +1,180 @@
+/*
+ * ccsc.h -- C-ABI of libccsc, the MI355X (gfx950) consensus-ADMM convolutional
+ * sparse coding engine.  Drop-in boundary for the four learners of the CCSC
+ * reference (paths relative to the reference repository):
+ *
+ *   admm_learn_conv2D_large_dParallel   2D/admm_learn_conv2D_large_dParallel.m:1-4
+ *   admm_learn_conv2D_large_dzParallel  2D/admm_learn_conv2D_large_dzParallel.m:1-4
+ *   admm_learn_conv3D_large             3D/admm_learn_conv3D_large.m:1-4
+ *   admm_learn_conv4D_lightfield        4D/admm_learn_conv4D_lightfield.m:1-4
+ *
+ * Each MATLAB function above becomes a thin .m wrapper over a MEX gateway that
+ * calls ccsc_learn(); the Python mirror in
+ * ccsc_code_iccv2017_amd/learners.py binds the same entry points via ctypes.
+ *
+ * Conventions
+ *  - Plain pointers and sizes only.  Every host array is MATLAB column-major
+ *    (first index fastest), float64, caller-owned; the library never retains a
+ *    host pointer past return.  Output pointers are nullable: a NULL output is
+ *    not computed/copied (z_res at the 10^4-patch config is ~97 GB).
+ *  - Every function returns 0 on success or a negative CCSC_E* code; when
+ *    `err` is non-NULL a NUL-terminated message (<= errlen bytes) says why.
+ *    No C++ exception crosses the ABI.
+ *  - Calls on one context come from one thread (MATLAB's / Python's).  The
+ *    progress callback runs on that calling thread only.
+ *  - Multi-GPU: one process per GPU.  Rank 0 calls ccsc_get_unique_id(); the
+ *    caller ships the 128 bytes to every rank (torch.distributed / MPI / file)
+ *    and each rank calls ccsc_create(device, rank, nranks, uid).  Blocks of
+ *    `ni` patches are sharded contiguously over ranks (ccsc_shard); the
+ *    consensus mean of the reference (dP:114-121) becomes one RCCL all-reduce
+ *    per d-iteration, the z-step's use of block 1's filters (dP:143) one RCCL
+ *    broadcast per outer iteration.
+ */
+#ifndef CCSC_H_
+#define CCSC_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CCSC_ABI_VERSION 1
+
+/* status codes */
+#define CCSC_OK 0
+#define CCSC_E_INVALID (-1)    /* bad argument / shape (e.g. n % ni != 0, Q13) */
+#define CCSC_E_HIP (-2)        /* HIP runtime error                            */
+#define CCSC_E_RCCL (-3)       /* RCCL error                                   */
+#define CCSC_E_NOMEM (-4)      /* device memory plan exceeds the GPU           */
+#define CCSC_E_UNSUPPORTED (-5)/* valid reference input not supported yet      */
+#define CCSC_E_STATE (-6)      /* call out of order                            */
+
+/* learner variants */
+#define CCSC_DPAR 0  /* 2D dParallel   dP:1-199  */
+#define CCSC_DZPAR 1 /* 2D dzParallel  dZ:1-206  */
+#define CCSC_L3D 2   /* 3D             L3:1-230  */
+#define CCSC_L4D 3   /* 4D light field L4:1-212  */
+
+/* verbose: which objectives the reference evaluates (dP:50-60,126,161) */
+#define CCSC_VERBOSE_NONE 0
+#define CCSC_VERBOSE_BRIEF 1
+#define CCSC_VERBOSE_ALL 2
+
+#define CCSC_FP64 0
+#define CCSC_FP32 1
+
+typedef struct ccsc_problem {
+  int32_t variant;          /* CCSC_DPAR .. CCSC_L4D                                */
+  int32_t ndim;             /* spatial dims of b: 2 (2D, 4D) or 3 (3D)              */
+  int64_t sb[3];            /* spatial size of b: x, y (, t for 3D)                 */
+  int32_t views[2];         /* 4D: U, V (angular views; kernel_size(3:4)); else 1,1 */
+  int64_t n;                /* number of patches (size(b, end))                     */
+  int32_t K;                /* number of filters (kernel_size(end))                 */
+  int32_t psf;              /* psf_s = kernel_size(1), odd                          */
+  double lambda_residual;   /* objective weight only (dP:21, Q-note)                */
+  double lambda_prior;      /* lambda: soft threshold = lambda / theta_div          */
+  int32_t max_it;           /* outer iterations                                     */
+  double tol;               /* relative-change tolerance; <= 0 disables the tests   */
+  int32_t verbose;          /* CCSC_VERBOSE_*                                       */
+  /* internal constants of the learners; 0 / <= 0 selects the variant default   */
+  int32_t ni;               /* patches per block (dP:11 = 100, L3:11 = sqrt(n))     */
+  int32_t max_it_d;         /* dP:75                                                */
+  int32_t max_it_z;         /* dP:76                                                */
+  double rho_d;             /* dP:98,111                                            */
+  double rho_z;             /* dP:153                                               */
+  double theta_div;         /* soft threshold = lambda_prior / theta_div (dP:150)   */
+  int32_t precision;        /* CCSC_FP64 (reference precision) or CCSC_FP32         */
+  int32_t trace_objective;  /* 1: evaluate the objective after every inner iter     */
+  uint64_t seed;            /* device RNG seed for d0/z0 when not supplied          */
+} ccsc_problem;
+
+typedef struct ccsc_outputs {
+  double* d_res; /* [psf,psf,(psf | U,V),K] cropped filters of block 1 (dP:195-196) */
+  double* z_res; /* this rank's codes: [X,Y,(T),K,n_local]; 4D: interleaved complex
+                    [X,Y,1,1,K,n_local] (L4:164, Q8 keeps it complex)                  */
+  double* DZ;    /* this rank's reconstruction (dP:193 uncropped; L4:205-206 cropped) */
+  double* obj_val; /* scalar final objective (L3:229, L4:211)                           */
+} ccsc_outputs;
+
+typedef struct ccsc_iterlog {
+  int32_t capacity;      /* entries available per array below (>= max_it + 1)         */
+  int32_t count;         /* entries written (outer iterations run + 1)                */
+  double* obj_vals_d;    /* iterations.obj_vals_d (dP:63,174), nullable                 */
+  double* obj_vals_z;    /* iterations.obj_vals_z (dP:64,175), nullable                 */
+  double* tim_vals;      /* iterations.tim_vals, seconds, objective excluded (dP:176)   */
+  /* extended trace (nullable; sized capacity * max_it_d / max_it_z)                   */
+  double* trace_obj_d;   /* objective after each d-iteration (trace_objective=1)        */
+  double* trace_obj_z;   /* objective after each z-iteration                            */
+  double* trace_d_diff;  /* ||D1 - D1_old|| / ||D1|| per d-iteration (tol > 0)          */
+  double* trace_z_diff;  /* ||z - z_old|| / ||z|| per z-iteration (tol > 0)             */
+  int32_t* n_d;          /* d-iterations run per outer iteration                        */
+  int32_t* n_z;          /* z-iterations run per outer iteration                        */
+} ccsc_iterlog;
+
+/* Progress callback, on the calling thread after each outer iteration. */
+typedef void (*ccsc_cb)(void* user, int32_t outer_it, double obj_d, double obj_z,
+                        double seconds);
+
+typedef struct ccsc_ctx ccsc_ctx;
+typedef struct ccsc_session ccsc_session;
+
+/* ---- host-only helpers (no GPU needed) ---------------------------------- */
+int32_t ccsc_abi_version(void);
+/* Fill variant defaults (Appendix A) in place and validate shapes. */
+int32_t ccsc_resolve(ccsc_problem* p, char* err, size_t errlen);
+/* Blocks [*block_begin, *block_begin + *block_count) of ni patches go to `rank`. */
+int32_t ccsc_shard(const ccsc_problem* p, int32_t rank, int32_t nranks,
+                   int64_t* block_begin, int64_t* block_count, char* err, size_t errlen);
+/* Device bytes one rank needs for this problem. */
+int32_t ccsc_plan_bytes(const ccsc_problem* p, int32_t rank, int32_t nranks,
+                        uint64_t* bytes, char* err, size_t errlen);
+
+/* ---- device / communicator ---------------------------------------------- */
+int32_t ccsc_device_count(int32_t* count, char* err, size_t errlen);
+/* RCCL unique id (128 bytes) for a multi-rank context; call on rank 0. */
+int32_t ccsc_get_unique_id(uint8_t* uid128, char* err, size_t errlen);
+/* nranks == 1: uid may be NULL and no communicator is created. */
+ccsc_ctx* ccsc_create(int32_t device, int32_t rank, int32_t nranks, const uint8_t* uid128,
+                      char* err, size_t errlen);
+void ccsc_destroy(ccsc_ctx* ctx);
+
+/* ---- one-shot learner: the literal drop-in for the .m functions --------- */
+/* b: this rank's patches, [sb..., (U,V), n_local] column-major float64.
+ * d0: [psf,psf,(psf|U,V),K] (init.d) or NULL (device RNG from p->seed).
+ * z0: init.z -- dP/L3/L4: size_z of this rank's patches; dZ: size_z_crop
+ *     ([X,Y,K,ni], replicated into every block, dZ:44-47); NULL = device RNG. */
+int32_t ccsc_learn(ccsc_ctx* ctx, const ccsc_problem* p, const double* b, const double* d0,
+                   const double* z0, ccsc_outputs* out, ccsc_iterlog* log, ccsc_cb cb,
+                   void* user, char* err, size_t errlen);
+
+/* ---- stateful session (bench / warm restart) ---------------------------- */
+ccsc_session* ccsc_session_create(ccsc_ctx* ctx, const ccsc_problem* p, const double* b,
+                                  const double* d0, const double* z0, char* err, size_t errlen);
+/* Run `n_outer` outer iterations (tol tests honoured); returns when the device is
+ * idle.  *done = 1 when the tol test ended the learning early. */
+int32_t ccsc_session_step(ccsc_session* s, int32_t n_outer, int32_t* done, char* err,
+                          size_t errlen);
+/* Objective of the current iterate: lambda_res/2||crop(Dz) - b||^2 + lambda|z|_1. */
+int32_t ccsc_session_objective(ccsc_session* s, double* obj, char* err, size_t errlen);
+int32_t ccsc_session_results(ccsc_session* s, ccsc_outputs* out, char* err, size_t errlen);
+int32_t ccsc_session_iterlog(ccsc_session* s, ccsc_iterlog* log, char* err, size_t errlen);
+/* Per-kernel timing with HIP events on the engine stream.  kernel ids: 0 = fused
+ * z-step, 1 = gram+cholesky, 2 = d-solve, 3 = dual+R2C, 4 = C2R+support.  Returns
+ * launches, total milliseconds and the algorithmic bytes of ONE launch. */
+int32_t ccsc_session_set_profiling(ccsc_session* s, int32_t on);
+int32_t ccsc_session_kernel_stats(ccsc_session* s, int32_t kernel_id, int64_t* launches,
+                                  double* total_ms, double* alg_bytes_per_launch, char* err,
+                                  size_t errlen);
+void ccsc_session_destroy(ccsc_session* s);
+
+/* ---- kernel-level entry points (parity tests of single stages) ---------- */
+/* 2D R2C of `count` real slices [X,Y] -> half spectra [Y][X/2+1] (re,im). */
+int32_t ccsc_test_fft2d(ccsc_ctx* ctx, int32_t X, int32_t Y, int32_t count, const double* in,
+                        double* out_halfspec, double* roundtrip, char* err, size_t errlen);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CCSC_H_ */
