@@ -81,25 +81,32 @@ def make_filters(K: int, psf: int, ndim: int, rng: np.random.Generator) -> np.nd
 
 def images_2d(n: int, size=(100, 100), K: int = 100, psf: int = 11, seed: int = 2017,
               density: float = 0.002, noise: float = 0.01, device: str = "cpu",
-              chunk: int = 256, local_cn_on: bool = True) -> np.ndarray:
-    """Synthetic contrast-normalised images, MATLAB layout [x, y, n] float64."""
+              chunk: int = 100, local_cn_on: bool = True, first: int = 0) -> np.ndarray:
+    """Synthetic contrast-normalised images, MATLAB layout [x, y, n] float64.
+
+    Patches first .. first+n-1 of the global sequence; chunk c (global patches
+    c*chunk ..) draws from its own seeded stream on `device`, so a rank that
+    generates only its shard gets exactly the single-GPU data.
+    """
     rng = np.random.default_rng(seed)
     d = make_filters(K, psf, 2, rng)                         # [K, psf, psf]  (x, y)
     dw = torch.as_tensor(np.ascontiguousarray(d[:, ::-1, ::-1]), dtype=torch.float32,
                          device=device)[None]                # conv2d weight [1, K, psf, psf]
     H, W = size
     out = np.empty((H, W, n), order="F")
-    for c0 in range(0, n, chunk):
-        m = min(chunk, n - c0)
-        crng = np.random.default_rng([seed, 1 + c0])         # per-chunk substream
+    if first % chunk:
+        raise ValueError("first must be chunk-aligned")
+    for c0 in range(first, first + n, chunk):
+        m = min(chunk, first + n - c0)
+        g = torch.Generator(device=device).manual_seed(seed * 1000003 + c0 // chunk)
         shape = (m, K, H + psf - 1, W + psf - 1)
-        g = torch.Generator(device="cpu").manual_seed(int(crng.integers(2**62)))
-        mask = torch.rand(shape, generator=g) < density
-        codes = torch.where(mask, torch.randn(shape, generator=g), torch.zeros(()))
-        raw = Fnn.conv2d(codes.to(device=device, dtype=torch.float32), dw)[:, 0].double()
-        raw = raw + noise * torch.randn(raw.shape, generator=g).to(device=device, dtype=torch.float64)
+        mask = torch.rand(shape, generator=g, device=device) < density
+        codes = torch.randn(shape, generator=g, device=device) * mask
+        raw = Fnn.conv2d(codes.to(torch.float32), dw)[:, 0].double()
+        del codes, mask
+        raw = raw + noise * torch.randn(raw.shape, generator=g, device=device, dtype=torch.float64)
         img = local_cn(raw) if local_cn_on else raw
-        out[:, :, c0:c0 + m] = img.permute(1, 2, 0).cpu().numpy()
+        out[:, :, c0 - first:c0 - first + m] = img.permute(1, 2, 0).cpu().numpy()
     return out
 
 
