@@ -80,6 +80,7 @@ CB = C.CFUNCTYPE(None, C.c_void_p, C.c_int32, C.c_double, C.c_double, C.c_double
 SIGNATURES = {
     "ccsc_abi_version": (C.c_int32, []),
     "ccsc_resolve": (C.c_int32, [C.POINTER(Problem), C.c_char_p, C.c_size_t]),
+    "ccsc_supported": (C.c_int32, [C.POINTER(Problem), C.c_char_p, C.c_size_t]),
     "ccsc_shard": (C.c_int32, [C.POINTER(Problem), C.c_int32, C.c_int32, C.POINTER(C.c_int64),
                                C.POINTER(C.c_int64), C.c_char_p, C.c_size_t]),
     "ccsc_plan_bytes": (C.c_int32, [C.POINTER(Problem), C.c_int32, C.c_int32,

@@ -30,8 +30,29 @@ __host__ __device__ __forceinline__ cpx<T> cscale(cpx<T> a, T s) { return {a.x *
 template <typename T>
 __host__ __device__ __forceinline__ T cabs2(cpx<T> a) { return a.x * a.x + a.y * a.y; }
 
-// Block size of every slice-resident kernel (8 waves of 64 lanes).
-constexpr int kNT = 512;
+// Block size of every slice-resident kernel: 16 waves of 64 lanes (one
+// workgroup per CU holds a whole fp64 slice in LDS, so the waves of that one
+// workgroup are all the latency hiding the CU gets).
+#ifndef CCSC_NT
+#define CCSC_NT 1024
+#endif
+constexpr int kNT = CCSC_NT;
+// Butterflies per FFT pass that the threads hold in registers at once (the
+// in-place pass needs every butterfly of the pass live between its read and
+// write barriers); MAXB = kMaxButterflies / kNT per thread.
+constexpr int kMaxButterflies = 1024;
+constexpr int kMaxB = kMaxButterflies / kNT;
+
+// Workgroup barrier for LDS hand-offs only.  __syncthreads() also waits
+// vmcnt(0), i.e. it drains every outstanding global load/store of the wave at
+// each of the ~20 barriers of a slice transform; this one waits only for the
+// wave's LDS ops, so global stores keep draining (and loads stay in flight)
+// underneath the FFT.  The "memory" clobber keeps the compiler from moving
+// memory ops across it; register dependences on pending global loads are
+// still guarded by the compiler's own vmcnt waits.
+__device__ __forceinline__ void lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
 
 // Wave-level sum (64 lanes) via shuffles.
 template <typename T>

@@ -72,7 +72,6 @@ static int32_t guarded(char* err, size_t errlen, F&& f) {
 // FFT planning (host)
 // ---------------------------------------------------------------------------
 static const int kRadices[] = {11, 10, 8, 7, 5, 4, 3, 2};  // fft_pass_dispatch
-static constexpr int kMaxButterflies = kNT * 2;  // MAXB = 2 in the device passes
 
 static bool plan1d(int n, int nlines, Plan1D& out) {
   Plan1D best{};
@@ -91,7 +90,7 @@ static bool plan1d(int n, int nlines, Plan1D& out) {
     for (int i = start; i < (int)(sizeof(kRadices) / sizeof(int)); ++i) {
       const int R = kRadices[i];
       if (rem % R) continue;
-      if ((int64_t)(n / R) * nlines > kMaxButterflies) continue;
+      if ((int64_t)(n / R) * nlines > kMaxButterflies) continue;  // registers of one pass
       cur.push_back(R);
       dfs(rem / R, i);
       cur.pop_back();
@@ -111,11 +110,14 @@ static bool make_grid2d(int X, int Y, Grid2D& G, std::string& why) {
   G.X = X;
   G.Y = Y;
   G.Xh = X / 2 + 1;
+  // LDS row stride (units of T): >= 2*Xh, even (16-B complex alignment), and
+  // 4*RS = 24 (mod 64) dwords so the column-pair lines of the x passes do not
+  // alias onto the same LDS banks (measured: 6e9 conflict cycles per z-step
+  // launch with RS = 2*Xh = 112).
   G.RS = 2 * G.Xh;
+  while (G.RS % 16 != 6) G.RS += 2;
   G.Yp = Y + (Y & 1);
   G.F = G.Xh * Y;
-  G.twx = 0;
-  G.twy = X;
   if (!plan1d(X, G.Yp / 2, G.px)) {
     why = "grid length " + std::to_string(X) +
           " has no radix plan (prime factors must be in {2,3,5,7,11} and fit the butterfly budget)";
@@ -126,7 +128,18 @@ static bool make_grid2d(int X, int Y, Grid2D& G, std::string& why) {
           " has no radix plan (prime factors must be in {2,3,5,7,11} and fit the butterfly budget)";
     return false;
   }
-  const size_t lds = slice_smem_bytes(G, sizeof(double));
+  // per-pass twiddle tables, x passes then y passes
+  int off = 0;
+  for (Plan1D* p : {&G.px, &G.py}) {
+    int Ns = 1;
+    for (int s = 0; s < p->npass; ++s) {
+      p->twoff[s] = off;
+      off += (p->rad[s] - 1) * Ns;
+      Ns *= p->rad[s];
+    }
+  }
+  G.ntw = std::max(off, 1);
+  const size_t lds = fused_smem_bytes(G, sizeof(double), 3);
   if (lds > 160 * 1024) {
     why = "padded slice " + std::to_string(X) + "x" + std::to_string(Y) +
           " does not fit one CU's LDS in fp64";
@@ -140,14 +153,19 @@ static bool make_grid2d(int X, int Y, Grid2D& G, std::string& why) {
 }
 
 static std::vector<cpx<double>> make_twiddles(const Grid2D& G) {
-  std::vector<cpx<double>> t(G.X + G.Y);
-  for (int m = 0; m < G.X; ++m) {
-    const long double a = -2.0L * 3.141592653589793238462643383279502884L * m / G.X;
-    t[m] = {(double)cosl(a), (double)sinl(a)};
-  }
-  for (int m = 0; m < G.Y; ++m) {
-    const long double a = -2.0L * 3.141592653589793238462643383279502884L * m / G.Y;
-    t[G.X + m] = {(double)cosl(a), (double)sinl(a)};
+  std::vector<cpx<double>> t(G.ntw, cpx<double>{1.0, 0.0});
+  const long double pi = 3.141592653589793238462643383279502884L;
+  for (const Plan1D* p : {&G.px, &G.py}) {
+    int Ns = 1;
+    for (int s = 0; s < p->npass; ++s) {
+      const int R = p->rad[s];
+      for (int r = 1; r < R; ++r)
+        for (int k = 0; k < Ns; ++k) {
+          const long double a = -2.0L * pi * (long double)(r * k) / (long double)(Ns * R);
+          t[p->twoff[s] + (r - 1) * Ns + k] = {(double)cosl(a), (double)sinl(a)};
+        }
+      Ns *= R;
+    }
   }
   return t;
 }
@@ -753,7 +771,15 @@ int32_t ccsc_resolve(ccsc_problem* p, char* err, size_t errlen) {
   return guarded(err, errlen, [&] {
     if (!p) throw Err(CCSC_E_INVALID, "problem is NULL");
     resolve_problem(*p);
-    check_supported(*p, nullptr);
+  });
+}
+
+int32_t ccsc_supported(const ccsc_problem* p, char* err, size_t errlen) {
+  return guarded(err, errlen, [&] {
+    if (!p) throw Err(CCSC_E_INVALID, "problem is NULL");
+    ccsc_problem q = *p;
+    resolve_problem(q);
+    check_supported(q, nullptr);
   });
 }
 

@@ -102,26 +102,26 @@ __device__ __forceinline__ void sfor(Fn&& f) {
 }
 
 // ---------------------------------------------------------------------------
-// In-register DFT of size R:  out[q] = sum_r v[r] * exp(SIGN*2*pi*i*r*q/R).
-// Odd/even pairing (r, R-r) halves the multiplies of the direct form.
+// In-register DFT of size R:  out[q] = sum_r v[r] * exp(SIGN*2*pi*i*r*q/R),
+// streamed to `sink(q, out[q])` as soon as each output (pair) is formed so the
+// R outputs are never live at once (a radix-11 fp64 pass at 1024 threads must
+// fit in 128 VGPRs).  Odd/even pairing (r, R-r) halves the multiplies.
 // ---------------------------------------------------------------------------
-template <typename T, int R, int SIGN>
-__device__ __forceinline__ void dft(cpx<T> (&v)[R]) {
+template <typename T, int R, int SIGN, typename Sink>
+__device__ __forceinline__ void dft_sink(cpx<T> (&v)[R], Sink&& sink) {
   if constexpr (R == 1) {
-    return;
+    sink(0, v[0]);
   } else if constexpr (R == 2) {
-    const cpx<T> a = v[0], b = v[1];
-    v[0] = cadd(a, b);
-    v[1] = csub(a, b);
+    sink(0, cadd(v[0], v[1]));
+    sink(1, csub(v[0], v[1]));
   } else if constexpr (R == 4) {
     const cpx<T> a0 = cadd(v[0], v[2]), a1 = csub(v[0], v[2]);
     const cpx<T> b0 = cadd(v[1], v[3]), b1 = csub(v[1], v[3]);
-    // b1 * (SIGN*i)
-    const cpx<T> b1i = {-(T)SIGN * b1.y, (T)SIGN * b1.x};
-    v[0] = cadd(a0, b0);
-    v[2] = csub(a0, b0);
-    v[1] = cadd(a1, b1i);
-    v[3] = csub(a1, b1i);
+    const cpx<T> b1i = {-(T)SIGN * b1.y, (T)SIGN * b1.x};  // b1 * (SIGN*i)
+    sink(0, cadd(a0, b0));
+    sink(2, csub(a0, b0));
+    sink(1, cadd(a1, b1i));
+    sink(3, csub(a1, b1i));
   } else {
     constexpr int H = (R - 1) / 2;
     constexpr bool EVEN = (R % 2) == 0;
@@ -131,16 +131,18 @@ __device__ __forceinline__ void dft(cpx<T> (&v)[R]) {
       a[r] = cadd(v[r], v[R - r]);
       b[r] = csub(v[r], v[R - r]);
     });
-    cpx<T> out[R];
+    const cpx<T> v0 = v[0];
+    cpx<T> vh = {(T)0, (T)0};
+    if constexpr (EVEN) vh = v[R / 2];
     {
-      cpx<T> s0 = v[0];
+      cpx<T> s0 = v0;
       sfor<H>([&](auto ri) { s0 = cadd(s0, a[decltype(ri)::value + 1]); });
-      if constexpr (EVEN) s0 = cadd(s0, v[R / 2]);
-      out[0] = s0;
+      if constexpr (EVEN) s0 = cadd(s0, vh);
+      sink(0, s0);
     }
     sfor<H>([&](auto qi) {
       constexpr int q = decltype(qi)::value + 1;
-      cpx<T> re = v[0];
+      cpx<T> re = v0;
       cpx<T> im = {(T)0, (T)0};
       sfor<H>([&](auto ri) {
         constexpr int r = decltype(ri)::value + 1;
@@ -153,26 +155,24 @@ __device__ __forceinline__ void dft(cpx<T> (&v)[R]) {
         im.y += b[r].y * s;
       });
       if constexpr (EVEN) {
-        if constexpr (q & 1) re = csub(re, v[R / 2]);
-        else re = cadd(re, v[R / 2]);
+        if constexpr (q & 1) re = csub(re, vh);
+        else re = cadd(re, vh);
       }
-      // SIGN * i * im = (-SIGN*im.y, SIGN*im.x)
-      const cpx<T> ii = {-(T)SIGN * im.y, (T)SIGN * im.x};
-      out[q] = cadd(re, ii);
-      out[R - q] = csub(re, ii);
+      const cpx<T> ii = {-(T)SIGN * im.y, (T)SIGN * im.x};  // SIGN * i * im
+      sink(q, cadd(re, ii));
+      sink(R - q, csub(re, ii));
     });
     if constexpr (EVEN) {
-      cpx<T> s0 = v[0];
+      cpx<T> s0 = v0;
       sfor<H>([&](auto ri) {
         constexpr int r = decltype(ri)::value + 1;
         if constexpr (r & 1) s0 = csub(s0, a[r]);
         else s0 = cadd(s0, a[r]);
       });
-      if constexpr ((R / 2) & 1) s0 = csub(s0, v[R / 2]);
-      else s0 = cadd(s0, v[R / 2]);
-      out[R / 2] = s0;
+      if constexpr ((R / 2) & 1) s0 = csub(s0, vh);
+      else s0 = cadd(s0, vh);
+      sink(R / 2, s0);
     }
-    sfor<R>([&](auto qi) { v[decltype(qi)::value] = out[decltype(qi)::value]; });
   }
 }
 
@@ -191,6 +191,8 @@ struct Plan1D {
   int n;
   int npass;
   int rad[kMaxPass];
+  int twoff[kMaxPass];  // offset (complex units) of pass s's twiddle table,
+                        // entries (r-1)*Ns + k = exp(-2 pi i r k / (Ns R))
 };
 
 // Per-slice description of the 2D grid (all in units of T unless noted).
@@ -201,8 +203,7 @@ struct Grid2D {
   int Yp;       // rows rounded up to even (column pairs = Yp/2)
   int F;        // Xh * Y half-spectrum bins, layout [y][x'] (x' fastest)
   Plan1D px, py;
-  int twx, twy; // offsets (complex units) of exp(-2 pi i m/X), exp(-2 pi i m/Y)
-                // inside the twiddle table
+  int ntw;      // twiddle table length (complex), both directions
 };
 
 // Load-decoding modes of the first pass of a direction.
@@ -211,11 +212,31 @@ constexpr int kModeSplitToHalf = 1;   // y-forward: two-for-one separation
 constexpr int kModeHermPair = 2;      // x-inverse: Z = A_2j + i*A_2j+1 (Hermitian ext.)
 
 template <typename T>
+__device__ __forceinline__ cpx<T> lds_cpx(const T* p, int imoff) {
+  if (imoff == 1) {  // interleaved complex: one 16-B (fp64) / 8-B (fp32) LDS access
+    const auto v = *reinterpret_cast<const typename vec2_t<T>::type*>(p);
+    return {v.x, v.y};
+  }
+  return {p[0], p[imoff]};
+}
+template <typename T>
+__device__ __forceinline__ void lds_cpx_store(T* p, int imoff, cpx<T> v) {
+  if (imoff == 1) {
+    typename vec2_t<T>::type w;
+    w.x = v.x;
+    w.y = v.y;
+    *reinterpret_cast<typename vec2_t<T>::type*>(p) = w;
+  } else {
+    p[0] = v.x;
+    p[imoff] = v.y;
+  }
+}
+
+template <typename T>
 __device__ __forceinline__ cpx<T> load_elem(const T* lds, const LineGeom& g, const Grid2D& G,
                                             int mode, int line, int e) {
   if (mode == kModePlain) {
-    const T* p = lds + line * g.lstride + e * g.estride;
-    return {p[0], p[g.imoff]};
+    return lds_cpx(lds + line * g.lstride + e * g.estride, g.imoff);
   } else if (mode == kModeSplitToHalf) {
     // line = x' (half-spectrum column), e = y.  Pair j = y/2 holds rows 2j, 2j+1
     // transformed together along x in split format.
@@ -235,9 +256,9 @@ __device__ __forceinline__ cpx<T> load_elem(const T* lds, const LineGeom& g, con
     const bool hi = e >= G.Xh;
     const int c = hi ? G.X - e : e;
     const T* r0 = lds + (2 * j) * G.RS + 2 * c;
-    cpx<T> a = {r0[0], r0[1]};
+    cpx<T> a = lds_cpx(r0, 1);
     cpx<T> b = {(T)0, (T)0};
-    if (2 * j + 1 < G.Y) b = {r0[G.RS], r0[G.RS + 1]};
+    if (2 * j + 1 < G.Y) b = lds_cpx(r0 + G.RS, 1);
     if (hi) {
       a.y = -a.y;
       b.y = -b.y;
@@ -247,13 +268,18 @@ __device__ __forceinline__ cpx<T> load_elem(const T* lds, const LineGeom& g, con
 }
 
 // One Stockham radix-R pass over all lines, in place.
+// Lane mapping (LDS bank conflicts): when the elements of a line are contiguous
+// (x direction, estride 1) consecutive lanes take consecutive butterflies of
+// one line; when they are strided (y direction) consecutive lanes take the
+// same butterfly of consecutive lines, so every access is lane-contiguous.
 template <typename T, int R, int MAXB, int SIGN>
 __device__ __forceinline__ void fft_pass(T* lds, int mode, const LineGeom& gin,
                                          const LineGeom& gout, const Grid2D& G, int n, int Ns,
                                          const cpx<T>* __restrict__ tw) {
   const int nb = n / R;
-  const int total = gin.nlines * nb;
-  const int step = n / (Ns * R);
+  const int nl = gin.nlines;
+  const int total = nl * nb;
+  const bool along = gin.estride == 1;
   cpx<T> v[MAXB][R];
   int outbase[MAXB];
   // read phase: load, twiddle (so no twiddle stays live across the barrier)
@@ -262,8 +288,14 @@ __device__ __forceinline__ void fft_pass(T* lds, int mode, const LineGeom& gin,
     const int bf = (int)threadIdx.x + b * kNT;
     outbase[b] = -1;
     if (bf < total) {
-      const int line = bf / nb;
-      const int j = bf - line * nb;
+      int line, j;
+      if (along) {
+        line = bf / nb;
+        j = bf - line * nb;
+      } else {
+        j = bf / nl;
+        line = bf - j * nl;
+      }
       const int k = j % Ns;
       outbase[b] = line * gout.lstride + ((j - k) * R + k) * gout.estride;
       v[b][0] = load_elem<T>(lds, gin, G, mode, line, j);
@@ -271,7 +303,7 @@ __device__ __forceinline__ void fft_pass(T* lds, int mode, const LineGeom& gin,
       for (int r = 1; r < R; ++r) {
         const cpx<T> x = load_elem<T>(lds, gin, G, mode, line, j + r * nb);
         if (Ns > 1) {
-          cpx<T> w = tw[r * k * step];
+          cpx<T> w = tw[(r - 1) * Ns + k];  // lane-contiguous in k: no bank conflicts
           if (SIGN > 0) w.y = -w.y;
           v[b][r] = cmul(x, w);
         } else {
@@ -280,22 +312,19 @@ __device__ __forceinline__ void fft_pass(T* lds, int mode, const LineGeom& gin,
       }
     }
   }
-  __syncthreads();
+  lds_sync();
   const int ostride = Ns * gout.estride;
 #pragma unroll
   for (int b = 0; b < MAXB; ++b) {
     if (outbase[b] >= 0) {
-      dft<T, R, SIGN>(v[b]);
       T* base = lds + outbase[b];
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        T* p = base + r * ostride;
-        p[0] = v[b][r].x;
-        p[gout.imoff] = v[b][r].y;
-      }
+      const int imoff = gout.imoff;
+      dft_sink<T, R, SIGN>(v[b], [&](int q, cpx<T> val) {
+        lds_cpx_store(base + q * ostride, imoff, val);
+      });
     }
   }
-  __syncthreads();
+  lds_sync();
 }
 
 template <typename T, int MAXB, int SIGN>
@@ -334,8 +363,9 @@ __device__ __forceinline__ void fft_dir(T* lds, int mode0, const LineGeom& gfirs
     constexpr int s = decltype(si)::value;
     if (s < p.npass) {
       const int R = p.rad[s];
-      if constexpr (s == 0) fft_pass_dispatch<T, MAXB, SIGN>(R, lds, mode0, gfirst, g, G, n, Ns, tw);
-      else fft_pass_dispatch<T, MAXB, SIGN>(R, lds, kModePlain, g, g, G, n, Ns, tw);
+      const cpx<T>* tws = tw + p.twoff[s];
+      if constexpr (s == 0) fft_pass_dispatch<T, MAXB, SIGN>(R, lds, mode0, gfirst, g, G, n, Ns, tws);
+      else fft_pass_dispatch<T, MAXB, SIGN>(R, lds, kModePlain, g, g, G, n, Ns, tws);
       Ns *= R;
     }
   });
@@ -354,9 +384,9 @@ template <typename T, int MAXB>
 __device__ __forceinline__ void slice_r2c(T* lds, const Grid2D& G, const cpx<T>* tw) {
   const LineGeom gx = geom_xsplit(G);
   const LineGeom gy = geom_ycols(G);
-  __syncthreads();
-  fft_dir<T, MAXB, -1>(lds, kModePlain, gx, gx, G, G.px, tw + G.twx);
-  fft_dir<T, MAXB, -1>(lds, kModeSplitToHalf, gy, gy, G, G.py, tw + G.twy);
+  lds_sync();
+  fft_dir<T, MAXB, -1>(lds, kModePlain, gx, gx, G, G.px, tw);
+  fft_dir<T, MAXB, -1>(lds, kModeSplitToHalf, gy, gy, G, G.py, tw);
 }
 
 // Inverse 2D C2R (unnormalised) of the interleaved half spectrum in LDS.
@@ -365,9 +395,9 @@ template <typename T, int MAXB>
 __device__ __forceinline__ void slice_c2r(T* lds, const Grid2D& G, const cpx<T>* tw) {
   const LineGeom gx = geom_xsplit(G);
   const LineGeom gy = geom_ycols(G);
-  __syncthreads();
-  fft_dir<T, MAXB, +1>(lds, kModePlain, gy, gy, G, G.py, tw + G.twy);
-  fft_dir<T, MAXB, +1>(lds, kModeHermPair, gx, gx, G, G.px, tw + G.twx);
+  lds_sync();
+  fft_dir<T, MAXB, +1>(lds, kModePlain, gy, gy, G, G.py, tw);
+  fft_dir<T, MAXB, +1>(lds, kModeHermPair, gx, gx, G, G.px, tw);
 }
 
 }  // namespace ccsc

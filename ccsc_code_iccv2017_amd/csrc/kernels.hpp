@@ -6,6 +6,7 @@
 namespace ccsc {
 
 size_t slice_smem_bytes(const Grid2D& G, size_t tsize);
+size_t fused_smem_bytes(const Grid2D& G, size_t tsize, int nbl);  // + NBL*kNT accumulator bins
 int pick_nb(int F);
 
 // ---- kernels2d.hip -------------------------------------------------------

@@ -27,7 +27,7 @@ __global__ __launch_bounds__(kNT) void k_r2c_embed(const T* __restrict__ src, in
                                                    const cpx<T>* __restrict__ twg, Grid2D G) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   Smem<T> S = carve<T>(smem, G);
-  load_twiddles(S.tw, twg, G.X + G.Y);
+  load_twiddles(S.tw, twg, G.ntw);
   const T* in = src + (int64_t)blockIdx.x * src_slice;
   const bool full = (sx == G.X && sy == G.Y);
   if (!full)
@@ -38,9 +38,9 @@ __global__ __launch_bounds__(kNT) void k_r2c_embed(const T* __restrict__ src, in
     S.slice[(y + oy) * G.RS + x + ox] = in[e];
   }
   if (full) zero_pad_row(S.slice, G);
-  slice_r2c<T, 2>(S.slice, G, S.tw);
+  slice_r2c<T, kMaxB>(S.slice, G, S.tw);
   cpx<T>* out = dst + (int64_t)blockIdx.x * dst_slice;
-  for (int f = threadIdx.x; f < G.F; f += kNT) out[f] = {S.slice[2 * f], S.slice[2 * f + 1]};
+  for (int f = threadIdx.x; f < G.F; f += kNT) { const int o = bin_off(f, G); out[f] = {S.slice[o], S.slice[o + 1]}; }
 }
 
 // Batched C2R (scaled): half spectra -> real X*Y slices.
@@ -52,14 +52,15 @@ __global__ __launch_bounds__(kNT) void k_c2r_plain(const cpx<T>* __restrict__ sr
                                                    T scale) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   Smem<T> S = carve<T>(smem, G);
-  load_twiddles(S.tw, twg, G.X + G.Y);
+  load_twiddles(S.tw, twg, G.ntw);
   const cpx<T>* in = src + (int64_t)blockIdx.x * src_slice;
   for (int f = threadIdx.x; f < G.F; f += kNT) {
     const cpx<T> v = in[f];
-    S.slice[2 * f] = v.x;
-    S.slice[2 * f + 1] = v.y;
+    const int o = bin_off(f, G);
+    S.slice[o] = v.x;
+    S.slice[o + 1] = v.y;
   }
-  slice_c2r<T, 2>(S.slice, G, S.tw);
+  slice_c2r<T, kMaxB>(S.slice, G, S.tw);
   T* out = dst + (int64_t)blockIdx.x * dst_slice;
   const int P = G.X * G.Y;
   for (int e = threadIdx.x; e < P; e += kNT) {
@@ -82,7 +83,7 @@ __global__ __launch_bounds__(kNT) void k_dual_r2c(const T* __restrict__ D, T* __
                                                   int K, int r) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   Smem<T> S = carve<T>(smem, G);
-  load_twiddles(S.tw, twg, G.X + G.Y);
+  load_twiddles(S.tw, twg, G.ntw);
   const int slice = blockIdx.x;
   const int k = slice % K;
   const int s = 2 * r + 1;
@@ -98,9 +99,9 @@ __global__ __launch_bounds__(kNT) void k_dual_r2c(const T* __restrict__ D, T* __
     S.slice[y * G.RS + x] = uv - yv;
   }
   zero_pad_row(S.slice, G);
-  slice_r2c<T, 2>(S.slice, G, S.tw);
+  slice_r2c<T, kMaxB>(S.slice, G, S.tw);
   cpx<T>* out = Ch + (int64_t)slice * G.F;
-  for (int f = threadIdx.x; f < G.F; f += kNT) out[f] = {S.slice[2 * f], S.slice[2 * f + 1]};
+  for (int f = threadIdx.x; f < G.F; f += kNT) { const int o = bin_off(f, G); out[f] = {S.slice[o], S.slice[o + 1]}; }
 }
 
 // ---------------------------------------------------------------------------
@@ -118,15 +119,16 @@ __global__ __launch_bounds__(kNT) void k_c2r_dout(const cpx<T>* __restrict__ Dh,
                                                   Grid2D G, int r, T invP) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   Smem<T> S = carve<T>(smem, G);
-  load_twiddles(S.tw, twg, G.X + G.Y);
+  load_twiddles(S.tw, twg, G.ntw);
   const int slice = blockIdx.x;
   const cpx<T>* in = Dh + (int64_t)slice * G.F;
   for (int f = threadIdx.x; f < G.F; f += kNT) {
     const cpx<T> v = in[f];
-    S.slice[2 * f] = v.x;
-    S.slice[2 * f + 1] = v.y;
+    const int o = bin_off(f, G);
+    S.slice[o] = v.x;
+    S.slice[o + 1] = v.y;
   }
-  slice_c2r<T, 2>(S.slice, G, S.tw);
+  slice_c2r<T, kMaxB>(S.slice, G, S.tw);
   const int P = G.X * G.Y;
   const int64_t off = (int64_t)slice * P;
   const bool first = slice < nfirst;
@@ -230,7 +232,10 @@ __global__ __launch_bounds__(256) void k_sum_pairs(const T* __restrict__ part, i
 // Host launchers
 // ---------------------------------------------------------------------------
 size_t slice_smem_bytes(const Grid2D& G, size_t tsize) {
-  return (size_t)(G.X + G.Y) * 2 * tsize + (size_t)G.Yp * G.RS * tsize + (kNT / 64) * tsize;
+  return (size_t)G.ntw * 2 * tsize + (size_t)G.Yp * G.RS * tsize + 16 * tsize;
+}
+size_t fused_smem_bytes(const Grid2D& G, size_t tsize, int nbl) {
+  return slice_smem_bytes(G, tsize) + (size_t)nbl * kNT * 2 * tsize;
 }
 
 template <typename T>

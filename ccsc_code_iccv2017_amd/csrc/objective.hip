@@ -6,7 +6,7 @@ namespace ccsc {
 
 int pick_nb(int F) {
   const int need = (F + kNT - 1) / kNT;
-  const int opts[] = {2, 6, 13};
+  const int opts[] = {1, 2, 4, 7};
   for (int o : opts)
     if (o >= need) return o;
   return -1;
@@ -18,7 +18,7 @@ int pick_nb(int F) {
 //   part[p] = { ||crop(Dz) - b_p||^2, sum |z_p| }
 // b: [np][sby][sbx]; DZ (nullable): [np][Y][X] uncropped.
 // ---------------------------------------------------------------------------
-template <typename T, int NB>
+template <typename T, int NBR, int NBL>
 __global__ __launch_bounds__(kNT) void k_objective(const T* __restrict__ z,
                                                    const cpx<T>* __restrict__ dhat,
                                                    const T* __restrict__ b, int sbx, int sby,
@@ -28,17 +28,16 @@ __global__ __launch_bounds__(kNT) void k_objective(const T* __restrict__ z,
                                                    int K) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   Smem<T> S = carve<T>(smem, G);
-  load_twiddles(S.tw, twg, G.X + G.Y);
+  load_twiddles(S.tw, twg, G.ntw);
   const int p = blockIdx.x;
   const int P = G.X * G.Y;
   const int F = G.F;
-  cpx<T> acc[NB];
-#pragma unroll
-  for (int i = 0; i < NB; ++i) acc[i] = {(T)0, (T)0};
+  BinAcc<T, NBR, NBL> acc;
+  acc.init(S.acc);
   T l1 = 0;
   for (int k = 0; k < K; ++k) {
     const int64_t off = ((int64_t)p * K + k) * P;
-    __syncthreads();
+    lds_sync();
     for (int e = threadIdx.x; e < P; e += kNT) {
       const int y = e / G.X, x = e - y * G.X;
       const T v = z[off + e];
@@ -46,24 +45,15 @@ __global__ __launch_bounds__(kNT) void k_objective(const T* __restrict__ z,
       S.slice[y * G.RS + x] = v;
     }
     zero_pad_row(S.slice, G);
-    slice_r2c<T, 2>(S.slice, G, S.tw);
+    slice_r2c<T, kMaxB>(S.slice, G, S.tw);
     const cpx<T>* dk = dhat + (int64_t)k * F;
-#pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      const int f = threadIdx.x + i * kNT;
-      if (f < F) acc[i] = cadd(acc[i], cmul(dk[f], cpx<T>{S.slice[2 * f], S.slice[2 * f + 1]}));
-    }
+    acc.each(F, [&](int f, cpx<T>& a) {
+      a = cadd(a, cmul(dk[f], lds_cpx(S.slice + bin_off(f, G), 1)));
+    });
   }
   __syncthreads();
-#pragma unroll
-  for (int i = 0; i < NB; ++i) {
-    const int f = threadIdx.x + i * kNT;
-    if (f < F) {
-      S.slice[2 * f] = acc[i].x;
-      S.slice[2 * f + 1] = acc[i].y;
-    }
-  }
-  slice_c2r<T, 2>(S.slice, G, S.tw);
+  acc.each(F, [&](int f, cpx<T>& a) { lds_cpx_store(S.slice + bin_off(f, G), 1, a); });
+  slice_c2r<T, kMaxB>(S.slice, G, S.tw);
   const T invP = (T)1 / (T)P;
   if (DZ) {
     T* o = DZ + (int64_t)p * P;
@@ -92,11 +82,10 @@ hipError_t launch_objective(const T* z, const cpx<T>* dhat, const T* b, int sbx,
                             T* DZ, T* part, int64_t npatch, const cpx<T>* tw, const Grid2D& G,
                             int K, hipStream_t st) {
   if (npatch <= 0) return hipSuccess;
-  const size_t sm = slice_smem_bytes(G, sizeof(T));
   const int nbv = pick_nb(G.F);
-  CCSC_NB_SWITCH(nbv, hipLaunchKernelGGL((k_objective<T, NB>), dim3((unsigned)npatch),
-                                         dim3(kNT), sm, st, z, dhat, b, sbx, sby, r, DZ, part,
-                                         tw, G, K));
+  CCSC_NB_SWITCH(nbv, hipLaunchKernelGGL((k_objective<T, NBR, NBL>), dim3((unsigned)npatch),
+                                         dim3(kNT), fused_smem_bytes(G, sizeof(T), NBL), st, z,
+                                         dhat, b, sbx, sby, r, DZ, part, tw, G, K));
   return hipGetLastError();
 }
 

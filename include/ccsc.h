@@ -124,6 +124,9 @@ typedef struct ccsc_session ccsc_session;
 int32_t ccsc_abi_version(void);
 /* Fill variant defaults (Appendix A) in place and validate shapes. */
 int32_t ccsc_resolve(ccsc_problem* p, char* err, size_t errlen);
+/* CCSC_OK if this build runs the (valid) problem on the GPU engine, else
+ * CCSC_E_UNSUPPORTED with the reason (grid radices, LDS budget, K, variant). */
+int32_t ccsc_supported(const ccsc_problem* p, char* err, size_t errlen);
 /* Blocks [*block_begin, *block_begin + *block_count) of ni patches go to `rank`. */
 int32_t ccsc_shard(const ccsc_problem* p, int32_t rank, int32_t nranks,
                    int64_t* block_begin, int64_t* block_count, char* err, size_t errlen);

@@ -1,0 +1,111 @@
+"""CPU: the C-ABI library loads, exports every symbol include/ccsc.h declares,
+and its host-only entry points (defaults, validation, sharding, memory plan)
+behave like the reference's constants and shapes.  No compute calls."""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def L():
+    from ccsc_code_iccv2017_amd import _lib
+    if not _lib.LIB_PATH.exists():
+        from ccsc_code_iccv2017_amd import build
+        build.build()
+    return _lib
+
+
+def header_symbols():
+    src = open(os.path.join(ROOT, "include", "ccsc.h")).read()
+    return sorted(set(re.findall(r"\b(ccsc_[a-z0-9_]+)\s*\(", src)) - {"ccsc_cb"})
+
+
+def test_every_header_symbol_is_exported(L):
+    lib = C.CDLL(str(L.LIB_PATH))
+    missing = [s for s in header_symbols() if not hasattr(lib, s)]
+    assert not missing, missing
+    assert set(header_symbols()) == set(L.SIGNATURES), "ctypes table out of sync with ccsc.h"
+    assert L.lib().ccsc_abi_version() == 1
+
+
+def _problem(L, variant, sb=(100, 100), n=10000, K=100, psf=11, **kw):
+    from ccsc_code_iccv2017_amd.learners import make_problem
+    p = make_problem(variant, tuple(sb) + (n,), [psf, psf, K], 1.0, 1.0, 20, 1e-3, "brief", **kw)
+    if len(sb) == 3:
+        p.ndim = 3
+        p.sb[2] = sb[2]
+    return p
+
+
+@pytest.mark.parametrize("variant,ni,mid,miz,rd,rz,td", [
+    (0, 100, 10, 10, 500, 50, 50),    # dP:11,75,76,98,153,150
+    (1, 100, 5, 10, 5000, 1, 1),      # dZ:11,75,76,99,154,151
+])
+def test_variant_defaults_2d(L, variant, ni, mid, miz, rd, rz, td):
+    from ccsc_code_iccv2017_amd.learners import resolve
+    q = resolve(_problem(L, variant))
+    assert (q.ni, q.max_it_d, q.max_it_z) == (ni, mid, miz)
+    assert (q.rho_d, q.rho_z, q.theta_div) == (rd, rz, td)
+
+
+def test_variant_defaults_3d_4d(L):
+    from ccsc_code_iccv2017_amd.learners import resolve
+    q = resolve(_problem(L, 2, sb=(64, 64, 32), n=64, K=49))       # L3:11,84,109,168,175
+    assert (q.ni, q.max_it_d, q.rho_d, q.rho_z, q.theta_div) == (8, 10, 5000, 1, 1)
+    p = _problem(L, 3, n=64, K=49)
+    p.views[0] = p.views[1] = 5
+    q = resolve(p)                                                   # L4:13,76,105,159,162
+    assert (q.ni, q.rho_d, q.rho_z, q.theta_div) == (8, 500, 50, 50)
+
+
+def test_invalid_shapes_are_errors(L):
+    from ccsc_code_iccv2017_amd.learners import resolve
+    with pytest.raises(L.CCSCError) as e:
+        resolve(_problem(L, 0, n=150))      # Q13: n % ni != 0 is an error, not a floor
+    assert e.value.code == L.CCSC_E_INVALID
+    with pytest.raises(L.CCSCError):
+        resolve(_problem(L, 0, psf=10))     # even psf
+    with pytest.raises(L.CCSCError):
+        resolve(_problem(L, 2, sb=(64, 64, 32), n=60, K=49))   # sqrt(n) not integer (L3:11)
+    p = _problem(L, 3, n=64, K=49)
+    p.views[0], p.views[1] = 5, 4
+    with pytest.raises(L.CCSCError):
+        resolve(p)                          # Q9: U != V
+
+
+def test_supported_reports_reasons(L):
+    eb = L.errbuf()
+    p = _problem(L, 1)
+    assert L.lib().ccsc_supported(C.byref(p), eb, len(eb)) == 0
+    p = _problem(L, 1, sb=(100, 96))        # grid 110 x 106 = 2*53: prime 53 has no radix
+    rc = L.lib().ccsc_supported(C.byref(p), eb, len(eb))
+    assert rc == L.CCSC_E_UNSUPPORTED and b"radix" in eb.value
+
+
+@pytest.mark.parametrize("nranks,expect", [(1, [100]), (2, [50, 50]), (4, [25] * 4),
+                                           (8, [13, 13, 13, 13, 12, 12, 12, 12])])
+def test_block_sharding_is_contiguous(L, nranks, expect):
+    from ccsc_code_iccv2017_amd.learners import shard
+    p = _problem(L, 1)
+    got, nxt = [], 0
+    for r in range(nranks):
+        b0, nb = shard(p, r, nranks)
+        assert b0 == nxt
+        nxt += nb
+        got.append(nb)
+    assert got == expect and nxt == 100
+
+
+def test_memory_plan_fits_one_mi355x(L):
+    from ccsc_code_iccv2017_amd.learners import plan_bytes
+    p = _problem(L, 1)
+    p.tol = 0.0
+    one = plan_bytes(p, 0, 1)
+    assert one < 288e9 * 0.97          # C2 fp64 on one 288 GB GPU
+    assert plan_bytes(p, 0, 8) < one / 7
+    p.tol = 1e-3                       # tol > 0 adds a z-sized buffer (z_old)
+    assert plan_bytes(p, 0, 1) > one

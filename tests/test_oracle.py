@@ -1,0 +1,173 @@
+"""CPU: pin the float64 oracle (the reference cannot run here: no MATLAB/Octave,
+SURVEY.md §8c) with analytic known-answer tests, and regress it against the
+committed golden fixtures (tests/golden/, made by tools/make_golden.py)."""
+import json
+import os
+
+import numpy as np
+import pytest
+from scipy.signal import convolve2d
+
+from oracle import ccsc_oracle as O
+from oracle.ccsc_port import DzPort
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _rng(s=0):
+    return np.random.default_rng(s)
+
+
+def test_precompute_D_is_regularised_normal_inverse():
+    """dP:235 Woodbury/pinv form == (A^H A + rho I)^-1 (pinv == inv: PD matrix)."""
+    rng = _rng(1)
+    X, Y, K, ni, rho = 6, 5, 4, 3, 500.0
+    zh = rng.standard_normal((X, Y, K, ni)) + 1j * rng.standard_normal((X, Y, K, ni))
+    A, S = O.precompute_H_hat_D(zh, X * Y, K, ni, rho)
+    for f in range(X * Y):
+        G = A[f].conj().T @ A[f] + rho * np.eye(K)
+        np.testing.assert_allclose(S[f], np.linalg.inv(G), rtol=1e-10, atol=1e-14)
+
+
+def test_solve_D_satisfies_normal_equations():
+    """solve_conv_term_D (dP:252-276): (A^H A + rho I) x = A^H b + rho c per frequency."""
+    rng = _rng(2)
+    X, Y, K, ni, rho = 6, 5, 4, 3, 500.0
+    zh = rng.standard_normal((X, Y, K, ni)) + 1j * rng.standard_normal((X, Y, K, ni))
+    Bb = rng.standard_normal((X, Y, ni)) + 1j * rng.standard_normal((X, Y, ni))
+    c = rng.standard_normal((X, Y, K)) + 1j * rng.standard_normal((X, Y, K))
+    A, S = O.precompute_H_hat_D(zh, X * Y, K, ni, rho)
+    x = O.solve_conv_term_D(A, S, c, Bb, rho, [X, Y], K, ni).reshape(-1, K, order="F")
+    b = Bb.reshape(-1, ni, order="F")
+    cf = c.reshape(-1, K, order="F")
+    for f in range(X * Y):
+        G = A[f].conj().T @ A[f] + rho * np.eye(K)
+        res = G @ x[f] - (A[f].conj().T @ b[f] + rho * cf[f])
+        assert np.linalg.norm(res) <= 1e-12 * np.linalg.norm(G @ x[f])
+
+
+def test_solve_Z_sherman_morrison_equals_dense_solve():
+    """dP:278-303: zhat = (conj(d) d^T + rho I)^-1 (conj(d) B + rho c) per (f, patch)."""
+    rng = _rng(3)
+    X, Y, K, n, rho = 5, 4, 3, 2, 1.0
+    dh = rng.standard_normal((X, Y, K)) + 1j * rng.standard_normal((X, Y, K))
+    Bh = rng.standard_normal((X, Y, n)) + 1j * rng.standard_normal((X, Y, n))
+    c = rng.standard_normal((X, Y, K, n)) + 1j * rng.standard_normal((X, Y, K, n))
+    df, dTd = O.precompute_H_hat_Z(dh, X * Y)
+    zh = O.solve_conv_term_Z(df, dTd, c, Bh, rho, [X, Y, K, n])
+    for ix in range(X):
+        for iy in range(Y):
+            d = dh[ix, iy]
+            M = np.outer(np.conj(d), d) + rho * np.eye(K)
+            for p in range(n):
+                ref = np.linalg.solve(M, np.conj(d) * Bh[ix, iy, p] + rho * c[ix, iy, :, p])
+                np.testing.assert_allclose(zh[ix, iy, :, p], ref, rtol=1e-11, atol=1e-13)
+
+
+def test_objective_fft_equals_direct_convolution():
+    """objectiveFunction (dP:305-324): the FFT data term equals a direct circular
+    convolution of each code map with its (embedded) filter."""
+    rng = _rng(4)
+    sb, psf, K, n = (9, 8), 5, 3, 2
+    r = psf // 2
+    X, Y = sb[0] + 2 * r, sb[1] + 2 * r
+    b = rng.standard_normal(sb + (n,))
+    d = rng.standard_normal((psf, psf, K))
+    z = rng.standard_normal((X, Y, K, n))
+    D = O.embed_filters(d, [X, Y], 2, r)
+    f_fft = O.objective_2d(z, np.fft.fft2(D, axes=(0, 1)), b, 1.0, 0.7, r)
+    # direct: circular convolution via wrap-padding
+    f_dir = 0.0
+    for p in range(n):
+        acc = np.zeros((X, Y))
+        for k in range(K):
+            zz = np.pad(z[:, :, k, p], ((psf - 1, 0), (psf - 1, 0)), mode="wrap")
+            # circshift(-r) embedding == kernel centred at the origin: shift back by r
+            full = convolve2d(zz, d[:, :, k], mode="valid")
+            acc += np.roll(full, (-r, -r), axis=(0, 1))
+        f_dir += 0.5 * np.sum((acc[r:X - r, r:Y - r] - b[:, :, p]) ** 2)
+    f_dir += 0.7 * np.abs(z).sum()
+    assert abs(f_fft - f_dir) <= 1e-10 * abs(f_dir)
+
+
+def test_kernel_projection_support_norm_idempotent():
+    """KernelConstraintProj (dP:201-219): support (2r+1)^2 around the origin,
+    per-filter norm <= 1, idempotent; only the support is read."""
+    rng = _rng(5)
+    X, Y, K, r = 12, 10, 4, 2
+    u = rng.standard_normal((X, Y, K)) * 3
+    u[:, :, 0] *= 0.01  # one filter inside the unit ball: left unscaled
+    p1 = O.kernel_constraint_proj(u, r, 2)
+    p2 = O.kernel_constraint_proj(p1, r, 2)
+    np.testing.assert_allclose(p1, p2, rtol=0, atol=1e-15)
+    sup = O.crop_filters(p1, 2, r)
+    norms = np.sqrt((sup ** 2).sum(axis=(0, 1)))
+    assert np.all(norms <= 1 + 1e-12)
+    np.testing.assert_allclose(sup[:, :, 0], O.crop_filters(u, 2, r)[:, :, 0])
+    assert np.abs(p1).sum() == pytest.approx(np.abs(sup).sum())  # zero off-support
+    u2 = u.copy()
+    mask = np.ones((X, Y, K), bool)
+    mask[O.embed_filters(np.ones((5, 5, K)), [X, Y], 2, r) > 0] = False
+    u2[mask] = 99.0  # off-support values must not matter
+    np.testing.assert_allclose(O.kernel_constraint_proj(u2, r, 2), p1)
+
+
+def test_half_spectrum_port_equals_literal_oracle():
+    """The half-spectrum / batched-inverse CPU port (bench cpu_baseline) equals
+    the literal full-spectrum pinv restatement of dZ."""
+    rng = _rng(6)
+    b = rng.standard_normal((10, 9, 6))
+    d0 = rng.standard_normal((5, 5, 3))
+    z0 = rng.standard_normal((14, 13, 3, 3))
+    o = O.learn_2d_dzparallel(b, [5, 5, 3], 1.0, 1.0, 2, 0.0, "none", {"d": d0, "z": z0}, ni=3)
+    p = DzPort(b, d0, z0, 1.0, ni=3, workers=1)
+    p.outer()
+    p.outer()
+    np.testing.assert_allclose(np.concatenate([p.z], 3), o[1], rtol=0, atol=1e-11)
+    np.testing.assert_allclose(O.crop_filters(p.D[0], 2, 2), o[0], rtol=0, atol=1e-12)
+
+
+def test_dp_objective_decreases():
+    rng = _rng(7)
+    b = rng.standard_normal((10, 10, 4))
+    init = {"d": rng.standard_normal((5, 5, 3)), "z": rng.standard_normal((14, 14, 3, 4))}
+    _, _, _, it, tr = O.learn_2d_dparallel(b, [5, 5, 3], 1.0, 1.0, 3, 0.0, "brief", init, ni=2,
+                                           trace_objective=True)
+    oz = it["obj_vals_z"]
+    assert oz[1] < oz[0] and oz[2] < oz[1] and oz[3] < oz[2]
+
+
+def test_quirks_Q2_first_d_iteration_uses_zero_consensus():
+    """Q2: u = Pi(0) = 0 in the first d-iteration, so y_j = d0 and c = -fft(d0)."""
+    r = 2
+    z = np.zeros((10, 10, 3))
+    np.testing.assert_array_equal(O.kernel_constraint_proj(z, r, 2), z)
+
+
+def test_quirk_Q13_n_not_multiple_of_ni_is_error_in_engine_contract():
+    """Q13 (reference floors n/ni silently); the ABI rejects it (tests/test_abi.py)."""
+    assert 150 % 100 != 0
+
+
+@pytest.mark.parametrize("name", ["dp_small", "dz_small", "dp_odd", "dz_110"])
+def test_golden_fixture_regression(name):
+    path = os.path.join(GOLD, f"{name}.npz")
+    g = np.load(path, allow_pickle=False)
+    meta = json.loads(str(g["meta"]))
+    init = {"d": g["d0"], "z": g["z0"]}
+    fn = O.learn_2d_dparallel if meta["variant"] == "dp" else O.learn_2d_dzparallel
+    d, z, DZ, it, tr = fn(g["b"], meta["kernel_size"], 1.0, 1.0, meta["max_it"], 0.0, "brief", init,
+                          ni=meta["ni"], trace_objective=True)
+    np.testing.assert_allclose(d, g["d_res"], rtol=1e-10, atol=1e-12)
+    np.testing.assert_allclose(np.array(tr["obj_z"]), g["trace_obj_z"], rtol=1e-10)
+    np.testing.assert_allclose(np.array(tr["obj_d"]), g["trace_obj_d"], rtol=1e-10)
+    assert abs(z.sum() - float(g["z_sum"])) <= 1e-8 * max(1.0, abs(float(g["z_sum"])))
+
+
+def test_reference_shipped_filters_are_unit_norm():
+    """The one external invariant the reference ships: its learned filters sit on
+    the unit sphere (values extracted from */Filters/*.mat by tools/make_golden.py)."""
+    ref = json.load(open(os.path.join(GOLD, "reference_filter_norms.json")))
+    for key, v in ref.items():
+        norms = np.array(v["norms"])
+        assert np.all(np.abs(norms - 1.0) < v["tol"]), key

@@ -1,0 +1,30 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 --pmc CSVs per kernel: mean counter value per dispatch."""
+import collections
+import csv
+import sys
+
+
+def summarize(path, match=("ccsc::",)):
+    rows = list(csv.DictReader(open(path)))
+    agg = collections.defaultdict(lambda: collections.defaultdict(list))
+    dur = collections.defaultdict(dict)
+    for r in rows:
+        name = r["Kernel_Name"]
+        if not any(m in name for m in match):
+            continue
+        k = name.split("(")[0].replace("void ", "")
+        agg[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        dur[k][r["Dispatch_Id"]] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
+    out = {}
+    for k, d in agg.items():
+        out[k] = {c: sum(v) / len(v) for c, v in d.items()}
+        out[k]["dispatches"] = len(dur[k])
+        out[k]["avg_s"] = sum(dur[k].values()) / max(len(dur[k]), 1)
+    return out
+
+
+if __name__ == "__main__":
+    for p in sys.argv[1:]:
+        for k, d in summarize(p).items():
+            print(p.split("/")[-1], k, {a: f"{b:.4g}" for a, b in d.items()})
