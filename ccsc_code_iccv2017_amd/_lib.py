@@ -75,6 +75,7 @@ class IterLog(C.Structure):
 
 
 CB = C.CFUNCTYPE(None, C.c_void_p, C.c_int32, C.c_double, C.c_double, C.c_double)
+COMM_FN = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.c_int32, C.POINTER(C.c_double), C.c_int64)
 
 # name -> (restype, argtypes); mirrors include/ccsc.h exactly
 SIGNATURES = {
@@ -89,6 +90,8 @@ SIGNATURES = {
     "ccsc_get_unique_id": (C.c_int32, [C.c_char_p, C.c_char_p, C.c_size_t]),
     "ccsc_create": (C.c_void_p, [C.c_int32, C.c_int32, C.c_int32, C.c_char_p, C.c_char_p,
                                  C.c_size_t]),
+    "ccsc_create_hostcomm": (C.c_void_p, [C.c_int32, C.c_int32, C.c_int32, COMM_FN, C.c_void_p,
+                                          C.c_char_p, C.c_size_t]),
     "ccsc_destroy": (None, [C.c_void_p]),
     "ccsc_learn": (C.c_int32, [C.c_void_p, C.POINTER(Problem), _dp, _dp, _dp,
                                C.POINTER(Outputs), C.POINTER(IterLog), CB, C.c_void_p,

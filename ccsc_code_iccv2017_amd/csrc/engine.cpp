@@ -280,7 +280,10 @@ struct ccsc_ctx {
   int rank = 0;
   int nranks = 1;
   hipStream_t stream = nullptr;
-  ncclComm_t comm = nullptr;
+  ncclComm_t comm = nullptr;       // RCCL over xGMI (production)
+  ccsc_comm_fn hostfn = nullptr;   // host-staged transport (tests)
+  void* hostuser = nullptr;
+  std::vector<double> stage;
 };
 
 namespace ccsc {
@@ -506,12 +509,24 @@ struct Session2D {
   }
 
   // ---- collectives ----------------------------------------------------------
+  void host_exchange(int op, double* buf, size_t count) {
+    ctx->stage.resize(count);
+    HIPCHK(hipMemcpyAsync(ctx->stage.data(), buf, count * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (ctx->hostfn(ctx->hostuser, op, ctx->stage.data(), (int64_t)count) != 0)
+      throw Err(CCSC_E_RCCL, "host communicator callback failed");
+    HIPCHK(hipMemcpyAsync(buf, ctx->stage.data(), count * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipStreamSynchronize(st));
+  }
   void allreduce(double* buf, size_t count) {
-    if (ctx->nranks > 1)
-      NCCLCHK(ncclAllReduce(buf, buf, count, ncclDouble, ncclSum, ctx->comm, st));
+    if (ctx->nranks <= 1) return;
+    if (ctx->comm) NCCLCHK(ncclAllReduce(buf, buf, count, ncclDouble, ncclSum, ctx->comm, st));
+    else host_exchange(CCSC_COMM_ALLREDUCE_SUM, buf, count);
   }
   void bcast0(double* buf, size_t count) {
-    if (ctx->nranks > 1) NCCLCHK(ncclBroadcast(buf, buf, count, ncclDouble, 0, ctx->comm, st));
+    if (ctx->nranks <= 1) return;
+    if (ctx->comm) NCCLCHK(ncclBroadcast(buf, buf, count, ncclDouble, 0, ctx->comm, st));
+    else host_exchange(CCSC_COMM_BCAST0, buf, count);
   }
   void pair_to_host(double* out2) {
     HIPCHK(hipMemcpyAsync(out2, pair.p, 2 * sizeof(double), hipMemcpyDeviceToHost, st));
@@ -839,6 +854,25 @@ ccsc_ctx* ccsc_create(int32_t device, int32_t rank, int32_t nranks, const uint8_
       std::memcpy(&id, uid128, 128);
       NCCLCHK(ncclCommInitRank(&c->comm, nranks, id, rank));
     }
+    ctx = c.release();
+  });
+  return rc == CCSC_OK ? ctx : nullptr;
+}
+
+ccsc_ctx* ccsc_create_hostcomm(int32_t device, int32_t rank, int32_t nranks, ccsc_comm_fn fn,
+                               void* user, char* err, size_t errlen) {
+  ccsc_ctx* ctx = nullptr;
+  const int rc = guarded(err, errlen, [&] {
+    if (nranks < 1 || rank < 0 || rank >= nranks) throw Err(CCSC_E_INVALID, "bad rank/nranks");
+    if (nranks > 1 && !fn) throw Err(CCSC_E_INVALID, "host communicator needs a callback");
+    std::unique_ptr<ccsc_ctx> c(new ccsc_ctx());
+    c->device = device;
+    c->rank = rank;
+    c->nranks = nranks;
+    c->hostfn = fn;
+    c->hostuser = user;
+    HIPCHK(hipSetDevice(device));
+    HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     ctx = c.release();
   });
   return rc == CCSC_OK ? ctx : nullptr;

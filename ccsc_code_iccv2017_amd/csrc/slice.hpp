@@ -53,7 +53,7 @@ __device__ __forceinline__ int bin_off(int f, const Grid2D& G) {
     case 1: { constexpr int NBR = 1, NBL = 0; CALL; } break;                 \
     case 2: { constexpr int NBR = 2, NBL = 0; CALL; } break;                 \
     case 4: { constexpr int NBR = 4, NBL = 0; CALL; } break;                 \
-    case 7: { constexpr int NBR = 7, NBL = 0; CALL; } break;                 \
+    case 7: { constexpr int NBR = 4, NBL = 3; CALL; } break;                 \
     default: return hipErrorInvalidValue;                                    \
   }
 

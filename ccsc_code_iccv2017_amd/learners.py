@@ -32,12 +32,30 @@ from . import _lib as L
 
 class Context:
     """One GPU (one rank).  ``uid`` (128 bytes from ``unique_id()`` on rank 0)
-    is needed when ``nranks > 1``; the consensus then runs over RCCL."""
+    is needed when ``nranks > 1``; the consensus then runs over RCCL.
 
-    def __init__(self, device: int = 0, rank: int = 0, nranks: int = 1, uid: bytes | None = None):
+    ``host_comm(op, array) -> None`` instead selects the host-staged transport
+    (op 0: in-place sum all-reduce, op 1: in-place broadcast from rank 0), e.g.
+    torch.distributed over gloo: used by the multi-rank GPU tests, which share
+    one GPU between ranks."""
+
+    def __init__(self, device: int = 0, rank: int = 0, nranks: int = 1, uid: bytes | None = None,
+                 host_comm=None):
         self._lib = L.lib()
         eb = L.errbuf()
-        self.ptr = self._lib.ccsc_create(device, rank, nranks, uid, eb, len(eb))
+        if host_comm is not None:
+            def _fn(user, op, buf, count):
+                try:
+                    arr = np.ctypeslib.as_array(buf, shape=(count,))
+                    host_comm(op, arr)
+                    return 0
+                except Exception:  # noqa: BLE001 -- reported to the engine as a status
+                    return 1
+            self._cfn = L.COMM_FN(_fn)   # keep the trampoline alive
+            self.ptr = self._lib.ccsc_create_hostcomm(device, rank, nranks, self._cfn, None, eb,
+                                                      len(eb))
+        else:
+            self.ptr = self._lib.ccsc_create(device, rank, nranks, uid, eb, len(eb))
         if not self.ptr:
             raise L.CCSCError(L.CCSC_E_HIP, eb.value.decode(errors="replace"))
         self.device, self.rank, self.nranks = device, rank, nranks

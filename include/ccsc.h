@@ -141,6 +141,15 @@ int32_t ccsc_get_unique_id(uint8_t* uid128, char* err, size_t errlen);
 /* nranks == 1: uid may be NULL and no communicator is created. */
 ccsc_ctx* ccsc_create(int32_t device, int32_t rank, int32_t nranks, const uint8_t* uid128,
                       char* err, size_t errlen);
+/* Host-transport communicator (testing / hosts without RCCL): the engine stages
+ * each exchange through host memory and calls fn on the calling thread.
+ * op 0 = in-place sum all-reduce, op 1 = in-place broadcast from rank 0.
+ * fn returns 0 on success. */
+#define CCSC_COMM_ALLREDUCE_SUM 0
+#define CCSC_COMM_BCAST0 1
+typedef int32_t (*ccsc_comm_fn)(void* user, int32_t op, double* buf, int64_t count);
+ccsc_ctx* ccsc_create_hostcomm(int32_t device, int32_t rank, int32_t nranks, ccsc_comm_fn fn,
+                               void* user, char* err, size_t errlen);
 void ccsc_destroy(ccsc_ctx* ctx);
 
 /* ---- one-shot learner: the literal drop-in for the .m functions --------- */

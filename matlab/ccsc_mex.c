@@ -1,0 +1,127 @@
+/*
+ * ccsc_mex.c -- MEX gateway over libccsc (include/ccsc.h).  Thin by design:
+ * marshal mxArrays (already column-major float64) into the C-ABI and back.
+ * NOT compiled in this repository (no MATLAB / mex.h here); build on a MATLAB
+ * host with:   mex -R2018a ccsc_mex.c -I../include -L../ccsc_code_iccv2017_amd -lccsc
+ *
+ * Called by the .m wrappers in this directory, which keep the reference
+ * signatures (2D/admm_learn_conv2D_large_dParallel.m:1-4 etc.):
+ *   [d_res, z_res, DZ, obj_val, iter] = ccsc_mex(variant, b, kernel_size,
+ *        lambda_residual, lambda_prior, max_it, tol, verbose, d0, z0, device)
+ */
+#include "mex.h"
+#include "ccsc.h"
+
+#include <string.h>
+
+static ccsc_ctx* g_ctx = NULL;
+static int g_dev = -1;
+
+static void cleanup(void) {
+  if (g_ctx) ccsc_destroy(g_ctx);
+  g_ctx = NULL;
+}
+
+static void progress(void* user, int32_t it, double od, double oz, double t) {
+  (void)user;
+  mexPrintf("Iter %d, Obj %3.3g / %3.3g, %.2f s\n", it, od, oz, t);  /* calling thread only */
+  mexEvalString("drawnow;");
+}
+
+void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
+  char err[1024] = {0};
+  if (nrhs < 11) mexErrMsgIdAndTxt("ccsc:args", "ccsc_mex needs 11 arguments");
+  const int variant = (int)mxGetScalar(prhs[0]);
+  const mxArray* b = prhs[1];
+  if (!mxIsDouble(b) || mxIsComplex(b)) mexErrMsgIdAndTxt("ccsc:b", "b must be real double");
+  const double* ks = mxGetDoubles(prhs[2]);
+  const mwSize nks = mxGetNumberOfElements(prhs[2]);
+  const mwSize* bd = mxGetDimensions(b);
+  const mwSize bn = mxGetNumberOfDimensions(b);
+
+  ccsc_problem p;
+  memset(&p, 0, sizeof p);
+  p.variant = variant;
+  p.ndim = (variant == CCSC_L3D) ? 3 : 2;
+  for (int i = 0; i < p.ndim; ++i) p.sb[i] = (int64_t)bd[i];
+  p.views[0] = p.views[1] = 1;
+  if (variant == CCSC_L4D) { p.views[0] = (int32_t)ks[2]; p.views[1] = (int32_t)ks[3]; }
+  p.n = (int64_t)(bn > (mwSize)p.ndim ? bd[bn - 1] : 1);
+  p.K = (int32_t)ks[nks - 1];
+  p.psf = (int32_t)ks[0];
+  p.lambda_residual = mxGetScalar(prhs[3]);
+  p.lambda_prior = mxGetScalar(prhs[4]);
+  p.max_it = (int32_t)mxGetScalar(prhs[5]);
+  p.tol = mxGetScalar(prhs[6]);
+  {
+    char v[16] = {0};
+    mxGetString(prhs[7], v, sizeof v);
+    p.verbose = !strcmp(v, "all") ? CCSC_VERBOSE_ALL : !strcmp(v, "brief") ? CCSC_VERBOSE_BRIEF
+                                                                           : CCSC_VERBOSE_NONE;
+  }
+  p.precision = CCSC_FP64;
+  if (ccsc_resolve(&p, err, sizeof err)) mexErrMsgIdAndTxt("ccsc:invalid", "%s", err);
+
+  const int dev = (int)mxGetScalar(prhs[10]);
+  if (!g_ctx || g_dev != dev) {
+    cleanup();
+    g_ctx = ccsc_create(dev, 0, 1, NULL, err, sizeof err);
+    if (!g_ctx) mexErrMsgIdAndTxt("ccsc:hip", "%s", err);
+    g_dev = dev;
+    mexAtExit(cleanup);
+  }
+  const double* d0 = mxIsEmpty(prhs[8]) ? NULL : mxGetDoubles(prhs[8]);
+  const double* z0 = mxIsEmpty(prhs[9]) ? NULL : mxGetDoubles(prhs[9]);
+
+  /* outputs: allocate only what nargout asks for (z_res is ~97 GB at C2) */
+  const int64_t r = p.psf / 2;
+  const mwSize X = (mwSize)(p.sb[0] + 2 * r), Y = (mwSize)(p.sb[1] + 2 * r);
+  ccsc_outputs out;
+  memset(&out, 0, sizeof out);
+  mwSize dd[5] = {(mwSize)p.psf, (mwSize)p.psf, (mwSize)p.K, 1, 1};
+  plhs[0] = mxCreateNumericArray(3, dd, mxDOUBLE_CLASS, mxREAL);
+  out.d_res = mxGetDoubles(plhs[0]);
+  if (nlhs > 1) {
+    mwSize zd[4] = {X, Y, (mwSize)p.K, (mwSize)p.n};
+    plhs[1] = mxCreateNumericArray(4, zd, mxDOUBLE_CLASS, mxREAL);
+    out.z_res = mxGetDoubles(plhs[1]);
+  }
+  if (nlhs > 2) {
+    mwSize zd[4] = {X, Y, 1, (mwSize)p.n};
+    plhs[2] = mxCreateNumericArray(4, zd, mxDOUBLE_CLASS, mxREAL);
+    out.DZ = mxGetDoubles(plhs[2]);
+  }
+  double obj = 0;
+  if (nlhs > 3) out.obj_val = &obj;
+
+  const int cap = p.max_it + 1;
+  mxArray* od = mxCreateDoubleMatrix(1, cap, mxREAL);
+  mxArray* oz = mxCreateDoubleMatrix(1, cap, mxREAL);
+  mxArray* tv = mxCreateDoubleMatrix(1, cap, mxREAL);
+  ccsc_iterlog lg;
+  memset(&lg, 0, sizeof lg);
+  lg.capacity = cap;
+  lg.obj_vals_d = mxGetDoubles(od);
+  lg.obj_vals_z = mxGetDoubles(oz);
+  lg.tim_vals = mxGetDoubles(tv);
+
+  const int rc = ccsc_learn(g_ctx, &p, mxGetDoubles(b), d0, z0, &out, &lg,
+                            p.verbose == CCSC_VERBOSE_NONE ? NULL : progress, NULL, err,
+                            sizeof err);
+  if (rc) mexErrMsgIdAndTxt("ccsc:learn", "%s (code %d)", err, rc);
+  mxSetN(od, lg.count);
+  mxSetN(oz, lg.count);
+  mxSetN(tv, lg.count);
+  if (nlhs > 3) plhs[3] = mxCreateDoubleScalar(obj);
+  if (nlhs > 4) {
+    const char* f[] = {"obj_vals_d", "obj_vals_z", "tim_vals"};
+    plhs[4] = mxCreateStructMatrix(1, 1, 3, f);
+    mxSetField(plhs[4], 0, "obj_vals_d", od);
+    mxSetField(plhs[4], 0, "obj_vals_z", oz);
+    mxSetField(plhs[4], 0, "tim_vals", tv);
+  } else {
+    mxDestroyArray(od);
+    mxDestroyArray(oz);
+    mxDestroyArray(tv);
+  }
+}

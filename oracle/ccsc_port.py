@@ -31,11 +31,28 @@ def _c2r(a, X, Y, workers):
     return sfft.irfftn(a, s=(Y, X), axes=(1, 0), workers=workers)
 
 
+def shard(N, rank, world):
+    """Contiguous block split (same rule as ccsc_shard in the engine)."""
+    base, rem = divmod(N, world)
+    nb = base + (1 if rank < rem else 0)
+    return rank * base + min(rank, rem), nb
+
+
 class DzPort:
-    """State of the dzParallel learner with tol = 0 (fixed inner counts)."""
+    """State of the dzParallel learner with tol = 0 (fixed inner counts).
+
+    Multi-rank restatement: with ``world > 1`` this instance
+    owns the contiguous blocks ``shard(N, rank, world)`` (``b`` is then the
+    rank-local patches) and the two exchanges of the engine are injected:
+    ``allreduce(x)`` sums the support-restricted sum_j (D_j + y_j) over ranks
+    (KernelConstraintProj reads only the support, dP:208-209) and
+    ``bcast(x)`` ships rank 0's block-1 filter spectrum to every rank
+    (the z-step uses block 1's D, dP:143).
+    """
 
     def __init__(self, b, d0, z0, lambda_prior, *, ni, rho_d=5000.0, rho_z=1.0, theta_div=1.0,
-                 max_it_d=5, max_it_z=10, workers=None):
+                 max_it_d=5, max_it_z=10, workers=None, N=None, rank=0, world=1,
+                 allreduce=None, bcast=None):
         self.w = workers if workers is not None else (os.cpu_count() or 1)
         b = np.asarray(b, dtype=np.float64)
         psf = d0.shape[0]
@@ -43,7 +60,11 @@ class DzPort:
         self.K = K = d0.shape[-1]
         self.n = n = b.shape[-1]
         self.ni = ni
-        self.N = n // ni
+        self.Nloc = n // ni
+        self.N = N if N is not None else self.Nloc          # global block count
+        self.rank, self.world = rank, world
+        self.allreduce = allreduce or (lambda x: x)
+        self.bcast = bcast or (lambda x: x)
         self.X, self.Y = b.shape[0] + 2 * r, b.shape[1] + 2 * r
         self.rho_d, self.rho_z = rho_d, rho_z
         self.theta = lambda_prior / theta_div
@@ -51,12 +72,11 @@ class DzPort:
         B = np.pad(b, ((r, r), (r, r), (0, 0)))
         self.Bh = _r2c(B, self.w)                                   # [Xh, Y, n]
         d = embed_filters(np.asarray(d0, float), [self.X, self.Y], 2, r)
-        self.D = [d.copy() for _ in range(self.N)]
-        self.yD = [np.zeros_like(d) for _ in range(self.N)]
-        self.Dbar = np.zeros_like(d)
-        self.Udbar = np.zeros_like(d)
+        self.D = [d.copy() for _ in range(self.Nloc)]
+        self.yD = [np.zeros_like(d) for _ in range(self.Nloc)]
+        self.u = np.zeros_like(d)                                    # Pi(Dbar + Udbar), Q2
         z0 = np.asarray(z0, float)
-        self.z = np.concatenate([z0] * self.N, axis=3)             # dZ:44-47
+        self.z = np.concatenate([z0] * self.Nloc, axis=3)          # dZ:44-47
         self.yz = np.zeros_like(self.z)
         self.dhat = None
 
@@ -65,7 +85,7 @@ class DzPort:
         # precompute (dZ:96-100): S_f = (A^H A + rho I)^-1, h_f = A^H b_f
         Zh = _r2c(self.z, w)                                        # [Xh, Y, K, n]
         S, h = [], []
-        for nn in range(self.N):
+        for nn in range(self.Nloc):
             A = Zh[..., nn * ni:(nn + 1) * ni].reshape(-1, K, ni).transpose(0, 2, 1)   # [F, ni, K]
             AH = np.conj(A.transpose(0, 2, 1))
             G = AH @ A
@@ -74,18 +94,26 @@ class DzPort:
             bb = self.Bh[..., nn * ni:(nn + 1) * ni].reshape(-1, ni)
             h.append(np.einsum("fkp,fp->fk", AH, bb))
         # D iterations (dZ:104-135)
+        r, s = self.r, 2 * self.r + 1
+        sup = (np.r_[X - r:X, 0:r + 1][:, None], np.r_[Y - r:Y, 0:r + 1][None, :])
+        dh_loc = None
         for _ in range(self.mid):
-            u = kernel_constraint_proj(self.Dbar + self.Udbar, self.r, 2)
-            for nn in range(self.N):
+            u = self.u
+            for nn in range(self.Nloc):
                 self.yD[nn] = self.yD[nn] + (self.D[nn] - u)
                 C = _r2c(u - self.yD[nn], w).reshape(-1, K)
                 x = np.einsum("fkj,fj->fk", S[nn], h[nn] + self.rho_d * C)
                 xh = x.reshape(X // 2 + 1, Y, K)
                 if nn == 0:
-                    self.dhat = xh
+                    dh_loc = xh
                 self.D[nn] = _c2r(xh, X, Y, w)
-            self.Dbar = sum(self.D) / self.N
-            self.Udbar = sum(self.yD) / self.N
+            # consensus (dP:114-121, 106): only the support of Dbar + Udbar is read
+            loc = sum((Dj + yj)[sup[0], sup[1]] for Dj, yj in zip(self.D, self.yD))
+            tot = self.allreduce(np.ascontiguousarray(loc))
+            full = np.zeros_like(u)
+            full[sup[0], sup[1]] = tot / self.N
+            self.u = kernel_constraint_proj(full, r, 2)
+        self.dhat = self.bcast(np.ascontiguousarray(dh_loc))         # block 1 lives on rank 0
         # Z iterations (dZ:147-172) with the simplified Sherman-Morrison solve
         dh = self.dhat                                              # [Xh, Y, K]
         s = np.sum(np.abs(dh) ** 2, axis=2)

@@ -1,0 +1,90 @@
+"""GPU, 2 ranks sharing the box's one MI355X: the engine's sharded path
+(contiguous block shards, owner-of-block-1 logic, per-d-iteration consensus
+all-reduce, per-outer broadcast of block 1's filter spectrum, tol norms)
+through the C-ABI, with the exchanges carried by the host-staged transport
+over gloo.  Must equal the single-rank engine and the oracle.  (8-GPU RCCL runs
+are the driver's; RCCL differs only in the transport calls.)"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _case(variant):
+    rng = np.random.default_rng(99)
+    ni, N, psf, K = 2, 3, 5, 3          # 3 blocks over 2 ranks: 2 + 1
+    b = rng.standard_normal((12, 11, ni * N))
+    d0 = rng.standard_normal((psf, psf, K))
+    X, Y = 16, 15
+    z0 = rng.standard_normal((X, Y, K, ni if variant == "dz" else ni * N))
+    return b, d0, z0, ni, N, [psf, psf, K]
+
+
+def _worker(rank, world, port, out_dir, variant, tol):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from ccsc_code_iccv2017_amd import learners as E
+
+    def host_comm(op, arr):
+        t = torch.from_numpy(arr)        # shares memory with the engine's staging buffer
+        if op == 0:
+            dist.all_reduce(t)
+        else:
+            dist.broadcast(t, src=0)
+
+    b, d0, z0, ni, N, ks = _case(variant)
+    v = E.L.CCSC_DZPAR if variant == "dz" else E.L.CCSC_DPAR
+    p = E.make_problem(v, b.shape, ks, 1.0, 1.0, 2, tol, "brief", ni=ni, trace_objective=True)
+    ctx = E.Context(0, rank, world, host_comm=host_comm)
+    b0, nb = E.shard(E.resolve(p), rank, world)
+    bl = b[:, :, b0 * ni:(b0 + nb) * ni]
+    zl = z0 if variant == "dz" else z0[..., b0 * ni:(b0 + nb) * ni]
+    s = E.Session(ctx, p, bl, d0, zl)
+    s.step(2)
+    d_res, z_res, DZ, _ = s.results()
+    it = s.iterlog()
+    np.savez(os.path.join(out_dir, f"{variant}_r{rank}.npz"), d=d_res, z=z_res, DZ=DZ,
+             oz=it["trace"]["obj_z"], od=it["trace"]["obj_d"], zd=it["trace"]["z_diff"])
+    s.close()
+    ctx.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("variant,tol", [("dz", 0.0), ("dp", 1e-12)])
+def test_two_ranks_equal_one_rank(tmp_path, gpu_ctx, variant, tol):
+    import torch.multiprocessing as mp
+    from ccsc_code_iccv2017_amd import learners as E
+    from oracle import ccsc_oracle as O
+
+    mp.start_processes(_worker, args=(2, _free_port(), str(tmp_path), variant, tol), nprocs=2,
+                       join=True, start_method="spawn")
+    parts = [np.load(tmp_path / f"{variant}_r{r}.npz") for r in range(2)]
+    b, d0, z0, ni, N, ks = _case(variant)
+    fn = O.learn_2d_dzparallel if variant == "dz" else O.learn_2d_dparallel
+    d_o, z_o, DZ_o, it_o, tr_o = fn(b, ks, 1.0, 1.0, 2, tol, "brief", {"d": d0, "z": z0}, ni=ni,
+                                    trace_objective=True)
+    z = np.concatenate([q["z"] for q in parts], axis=3)
+    DZ = np.concatenate([q["DZ"] for q in parts], axis=3)
+    for q in parts:   # every rank returns block 1's filters and the global objectives
+        np.testing.assert_allclose(q["d"], d_o, rtol=0, atol=1e-9 * np.abs(d_o).max())
+        np.testing.assert_allclose(q["oz"], np.array(tr_o["obj_z"]), rtol=1e-9)
+        np.testing.assert_allclose(q["od"], np.array(tr_o["obj_d"]), rtol=1e-9)
+    np.testing.assert_allclose(z, z_o, rtol=0, atol=1e-9 * np.abs(z_o).max())
+    np.testing.assert_allclose(DZ, DZ_o, rtol=0, atol=1e-9 * np.abs(DZ_o).max())
+    if tol > 0:
+        np.testing.assert_allclose(parts[0]["zd"], np.array(tr_o["z_diff"]), rtol=1e-6)
