@@ -53,12 +53,16 @@ def build(force: bool = False, jobs: int | None = None) -> Path:
     jobs = jobs or min(len(srcs), max(1, min(8, os.cpu_count() or 1)))
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         objs = list(ex.map(lambda s: _compile(s, force), srcs))
-    if force or _needs(LIB, objs):
+    stamp = OBJ / "libccsc.objs"
+    sig = "\n".join(f"{o}:{o.stat().st_mtime_ns}" for o in objs)
+    stale = not stamp.exists() or stamp.read_text() != sig
+    if force or stale or _needs(LIB, objs):
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-o", str(LIB)] + [str(o) for o in objs]
         cmd += [f"-L{ROCM / 'lib'}", "-lrccl", f"-Wl,-rpath,{ROCM / 'lib'}"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr[-6000:]}")
+        stamp.write_text(sig)
     return LIB
 
 
