@@ -55,14 +55,16 @@ def build(force: bool = False, jobs: int | None = None) -> Path:
         objs = list(ex.map(lambda s: _compile(s, force), srcs))
     stamp = OBJ / "libccsc.objs"
     sig = "\n".join(f"{o}:{o.stat().st_mtime_ns}" for o in objs)
-    stale = not stamp.exists() or stamp.read_text() != sig
+    libsig = f"{LIB.stat().st_mtime_ns}:{LIB.stat().st_size}" if LIB.exists() else "none"
+    # stale if the object set changed or the library was replaced behind our back
+    stale = not stamp.exists() or stamp.read_text() != sig + "\n" + libsig
     if force or stale or _needs(LIB, objs):
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-o", str(LIB)] + [str(o) for o in objs]
         cmd += [f"-L{ROCM / 'lib'}", "-lrccl", f"-Wl,-rpath,{ROCM / 'lib'}"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr[-6000:]}")
-        stamp.write_text(sig)
+        stamp.write_text(sig + "\n" + f"{LIB.stat().st_mtime_ns}:{LIB.stat().st_size}")
     return LIB
 
 

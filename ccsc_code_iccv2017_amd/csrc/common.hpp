@@ -42,6 +42,11 @@ constexpr int kNT = CCSC_NT;
 // write barriers); MAXB = kMaxButterflies / kNT per thread.
 constexpr int kMaxButterflies = 1024;
 constexpr int kMaxB = kMaxButterflies / kNT;
+// Small radices cost few registers per butterfly, so a thread may hold more of
+// them (needed e.g. by the radix-2 pass of the 74-point grids: 37 x 37 = 1369).
+__host__ __device__ constexpr int maxb_for_radix(int R) {
+  return (R <= 4 ? 4 : (R <= 8 ? 2 : 1)) * kMaxB;
+}
 
 // Workgroup barrier for LDS hand-offs only.  __syncthreads() also waits
 // vmcnt(0), i.e. it drains every outstanding global load/store of the wave at

@@ -20,12 +20,16 @@ constexpr int kGramPC = 16;  // patches staged in LDS per chunk
 __device__ __forceinline__ int pk_off(int j, int K) { return j * K - (j * (j - 1)) / 2; }
 
 // one workgroup per frequency (XCD-aware: consecutive f share an XCD's L2)
+constexpr int kGramHPT = 8;  // (view, filter) right-hand-side entries per thread
+
+// h[f][uv][k] = sum_p conj(A[p][k]) B[p][uv][f] for NV views (4D: the same A_f
+// serves every view, L4:252 replicates it, so one Cholesky per spatial f).
 template <typename T>
 __global__ __launch_bounds__(kGramNT) void k_gram_chol(const cpx<T>* __restrict__ Zh,
                                                        const cpx<T>* __restrict__ Bh,
                                                        cpx<T>* __restrict__ L,
                                                        cpx<T>* __restrict__ h, int F, int K,
-                                                       int ni, T rho) {
+                                                       int ni, T rho, int NV) {
   const int per = gridDim.x >> 3;
   const int f = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
   if (f >= F) return;
@@ -33,7 +37,7 @@ __global__ __launch_bounds__(kGramNT) void k_gram_chol(const cpx<T>* __restrict_
   cpx<T>* sG = reinterpret_cast<cpx<T>*>(smem);           // packed G, Kp entries
   const int Kp = K * (K + 1) / 2;
   cpx<T>* sA = sG;                                          // chunk [PC][K] (aliases sG)
-  cpx<T>* sB = sA + kGramPC * K;                            // [PC]
+  cpx<T>* sB = sA + kGramPC * K;                            // [PC][NV]
   const int tid = threadIdx.x;
   const int Kt = (K + kGramTS - 1) / kGramTS;
   const int ntiles = Kt * (Kt + 1) / 2;
@@ -50,7 +54,10 @@ __global__ __launch_bounds__(kGramNT) void k_gram_chol(const cpx<T>* __restrict_
   for (int a = 0; a < kGramTS; ++a)
 #pragma unroll
     for (int b = 0; b < kGramTS; ++b) acc[a][b] = {(T)0, (T)0};
-  cpx<T> hacc = {(T)0, (T)0};
+  cpx<T> hacc[kGramHPT];
+#pragma unroll
+  for (int i = 0; i < kGramHPT; ++i) hacc[i] = {(T)0, (T)0};
+  const int KV = K * NV;
 
   for (int p0 = 0; p0 < ni; p0 += kGramPC) {
     const int pc = min(kGramPC, ni - p0);
@@ -59,7 +66,8 @@ __global__ __launch_bounds__(kGramNT) void k_gram_chol(const cpx<T>* __restrict_
       const int pp = idx / K, k = idx - pp * K;
       sA[idx] = Zh[((int64_t)(p0 + pp) * K + k) * F + f];
     }
-    if (tid < pc) sB[tid] = Bh[(int64_t)(p0 + tid) * F + f];
+    for (int q = tid; q < pc * NV; q += kGramNT)
+      sB[q] = Bh[(int64_t)(p0 * NV + q) * F + f];   // B[p][uv][f], q = pp*NV + uv
     __syncthreads();
     if (act) {
       for (int pp = 0; pp < pc; ++pp) {
@@ -77,8 +85,15 @@ __global__ __launch_bounds__(kGramNT) void k_gram_chol(const cpx<T>* __restrict_
           for (int v = 0; v < kGramTS; ++v) acc[u][v] = cadd(acc[u][v], cmulc(ai[u], aj[v]));
       }
     }
-    if (tid < K)
-      for (int pp = 0; pp < pc; ++pp) hacc = cadd(hacc, cmulc(sA[pp * K + tid], sB[pp]));
+#pragma unroll
+    for (int i = 0; i < kGramHPT; ++i) {
+      const int q = tid + i * kGramNT;   // q = uv*K + k
+      if (q < KV) {
+        const int uv = q / K, k = q - uv * K;
+        for (int pp = 0; pp < pc; ++pp)
+          hacc[i] = cadd(hacc[i], cmulc(sA[pp * K + k], sB[pp * NV + uv]));
+      }
+    }
   }
   __syncthreads();  // chunk buffer (aliasing sG) no longer read
   if (act) {
@@ -97,7 +112,11 @@ __global__ __launch_bounds__(kGramNT) void k_gram_chol(const cpx<T>* __restrict_
         }
       }
   }
-  if (tid < K) h[(int64_t)f * K + tid] = hacc;
+#pragma unroll
+  for (int i = 0; i < kGramHPT; ++i) {
+    const int q = tid + i * kGramNT;
+    if (q < KV) h[(int64_t)f * KV + q] = hacc[i];
+  }
   __syncthreads();
 
   // right-looking Cholesky in LDS: G = L L^H
@@ -133,16 +152,17 @@ __global__ __launch_bounds__(kGramNT) void k_gram_chol(const cpx<T>* __restrict_
 
 template <typename T>
 hipError_t launch_gram_chol(const cpx<T>* Zh, const cpx<T>* Bh, cpx<T>* L, cpx<T>* h, int F,
-                            int K, int ni, T rho, hipStream_t st) {
+                            int K, int ni, T rho, int NV, hipStream_t st) {
   const int Kt = (K + kGramTS - 1) / kGramTS;
   if (Kt * (Kt + 1) / 2 > kGramNT) return hipErrorInvalidValue;
+  if (K * NV > kGramHPT * kGramNT) return hipErrorInvalidValue;
   const int Kp = K * (K + 1) / 2;
   size_t sm = (size_t)Kp * sizeof(cpx<T>);
-  const size_t sm2 = (size_t)(kGramPC * K + kGramPC) * sizeof(cpx<T>);
+  const size_t sm2 = (size_t)(kGramPC * K + kGramPC * NV) * sizeof(cpx<T>);
   if (sm2 > sm) sm = sm2;
   const int grid = ((F + 7) / 8) * 8;
   hipLaunchKernelGGL(k_gram_chol<T>, dim3(grid), dim3(kGramNT), sm, st, Zh, Bh, L, h, F, K, ni,
-                     rho);
+                     rho, NV);
   return hipGetLastError();
 }
 
@@ -156,26 +176,28 @@ __device__ __forceinline__ cpx<T> shfl_c(cpx<T> v, int src) {
   return {__shfl(v.x, src, 64), __shfl(v.y, src, 64)};
 }
 
+// NV right-hand sides per (block, f) share one factor (4D views, L4:281-308).
 template <typename T, int RPL>
 __global__ __launch_bounds__(256) void k_dsolve(const cpx<T>* __restrict__ L,
                                                 const cpx<T>* __restrict__ h,
                                                 const cpx<T>* __restrict__ Ch,
                                                 cpx<T>* __restrict__ Dh, int F, int K, T rho,
-                                                int fgroups) {
+                                                int fgroups, int NV) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int blk = blockIdx.x / fgroups;
   const int f = (blockIdx.x - blk * fgroups) * 4 + wave;
   if (f >= F) return;
   const int Kp = K * (K + 1) / 2;
   const cpx<T>* Lf = L + ((int64_t)blk * F + f) * Kp;
-  const cpx<T>* hf = h + ((int64_t)blk * F + f) * K;
-  const cpx<T>* Cb = Ch + (int64_t)blk * K * F;
+  for (int uv = 0; uv < NV; ++uv) {
+  const cpx<T>* hf = h + (((int64_t)blk * F + f) * NV + uv) * K;
+  const cpx<T>* Cb = Ch + (int64_t)blk * K * NV * F + (int64_t)uv * F;   // [blk][k][uv][F]
   cpx<T> x[RPL];
 #pragma unroll
   for (int t = 0; t < RPL; ++t) {
     const int i = lane + 64 * t;
     if (i < K) {
-      const cpx<T> c = Cb[(int64_t)i * F + f];
+      const cpx<T> c = Cb[(int64_t)i * NV * F + f];
       const cpx<T> hh = hf[i];
       x[t] = {hh.x + rho * c.x, hh.y + rho * c.y};
     } else {
@@ -219,26 +241,27 @@ __global__ __launch_bounds__(256) void k_dsolve(const cpx<T>* __restrict__ L,
       if (lane == jl) x[t] = cscale(csub(x[t], part), (T)1 / Lf[oj].x);
     }
   }
-  cpx<T>* Db = Dh + (int64_t)blk * K * F;
+  cpx<T>* Db = Dh + (int64_t)blk * K * NV * F + (int64_t)uv * F;
 #pragma unroll
   for (int t = 0; t < RPL; ++t) {
     const int i = lane + 64 * t;
-    if (i < K) Db[(int64_t)i * F + f] = x[t];
+    if (i < K) Db[(int64_t)i * NV * F + f] = x[t];
   }
+  }  // views
 }
 
 template <typename T>
 hipError_t launch_dsolve(const cpx<T>* L, const cpx<T>* h, const cpx<T>* Ch, cpx<T>* Dh,
-                         int nblocks, int F, int K, T rho, hipStream_t st) {
+                         int nblocks, int F, int K, T rho, int NV, hipStream_t st) {
   if (nblocks <= 0) return hipSuccess;
   const int fgroups = (F + 3) / 4;
   const dim3 grid((unsigned)(nblocks * fgroups));
   if (K <= 64)
     hipLaunchKernelGGL((k_dsolve<T, 1>), grid, dim3(256), 0, st, L, h, Ch, Dh, F, K, rho,
-                       fgroups);
+                       fgroups, NV);
   else if (K <= 128)
     hipLaunchKernelGGL((k_dsolve<T, 2>), grid, dim3(256), 0, st, L, h, Ch, Dh, F, K, rho,
-                       fgroups);
+                       fgroups, NV);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();
@@ -246,9 +269,9 @@ hipError_t launch_dsolve(const cpx<T>* L, const cpx<T>* h, const cpx<T>* Ch, cpx
 
 template hipError_t launch_gram_chol<double>(const cpx<double>*, const cpx<double>*,
                                              cpx<double>*, cpx<double>*, int, int, int, double,
-                                             hipStream_t);
+                                             int, hipStream_t);
 template hipError_t launch_dsolve<double>(const cpx<double>*, const cpx<double>*,
                                           const cpx<double>*, cpx<double>*, int, int, int,
-                                          double, hipStream_t);
+                                          double, int, hipStream_t);
 
 }  // namespace ccsc

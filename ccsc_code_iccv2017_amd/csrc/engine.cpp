@@ -73,6 +73,16 @@ static int32_t guarded(char* err, size_t errlen, F&& f) {
 // ---------------------------------------------------------------------------
 static const int kRadices[] = {11, 10, 8, 7, 5, 4, 3, 2};  // fft_pass_dispatch
 
+static bool is_native_radix(int R) {
+  for (int r : kRadices)
+    if (r == R) return true;
+  return false;
+}
+
+// Fewest passes; native (unrolled) radices first, then at most one generic
+// prime radix <= kMaxGenericRadix (e.g. 74 = 2 * 37).  Register budget: a native
+// pass holds n/R butterflies per line (<= kMaxButterflies), a generic pass n
+// outputs per line (<= kMaxGenericOut * kNT).
 static bool plan1d(int n, int nlines, Plan1D& out) {
   Plan1D best{};
   best.npass = 99;
@@ -90,17 +100,41 @@ static bool plan1d(int n, int nlines, Plan1D& out) {
     for (int i = start; i < (int)(sizeof(kRadices) / sizeof(int)); ++i) {
       const int R = kRadices[i];
       if (rem % R) continue;
-      if ((int64_t)(n / R) * nlines > kMaxButterflies) continue;  // registers of one pass
+      if ((int64_t)(n / R) * nlines > (int64_t)maxb_for_radix(R) * kNT) continue;  // registers
       cur.push_back(R);
       dfs(rem / R, i);
       cur.pop_back();
     }
   };
   if (n == 1) {
-    out = Plan1D{1, 0, {0}};
+    out = Plan1D{1, 0, {0}, {0}};
     return true;
   }
   dfs(n, 0);
+  if (best.npass == 99) {
+    // one generic prime factor p, the rest native
+    for (int p = 13; p <= kMaxGenericRadix; ++p) {
+      bool prime = true;
+      for (int d = 2; d * d <= p; ++d)
+        if (p % d == 0) prime = false;
+      if (!prime || n % p) continue;
+      if ((int64_t)n * nlines > (int64_t)kMaxGenericOut * kNT) continue;
+      Plan1D rest{};
+      if (!plan1d(n / p, nlines, rest) && n / p != 1) continue;
+      if (rest.npass + 1 > kMaxPass) continue;
+      // the native passes keep their own budget at length n: re-check
+      bool ok = true;
+      for (int s = 0; s < rest.npass; ++s)
+        if ((int64_t)(n / rest.rad[s]) * nlines > (int64_t)maxb_for_radix(rest.rad[s]) * kNT)
+          ok = false;
+      if (!ok) continue;
+      best.n = n;
+      best.npass = rest.npass + 1;
+      for (int s = 0; s < rest.npass; ++s) best.rad[s] = rest.rad[s];
+      best.rad[rest.npass] = p;
+      break;
+    }
+  }
   if (best.npass == 99) return false;
   out = best;
   return true;
@@ -120,12 +154,12 @@ static bool make_grid2d(int X, int Y, Grid2D& G, std::string& why) {
   G.F = G.Xh * Y;
   if (!plan1d(X, G.Yp / 2, G.px)) {
     why = "grid length " + std::to_string(X) +
-          " has no radix plan (prime factors must be in {2,3,5,7,11} and fit the butterfly budget)";
+          " has no radix plan (factors 2,3,5,7,11 plus at most one prime <= 64, within the register budget)";
     return false;
   }
   if (!plan1d(Y, G.Xh, G.py)) {
     why = "grid length " + std::to_string(Y) +
-          " has no radix plan (prime factors must be in {2,3,5,7,11} and fit the butterfly budget)";
+          " has no radix plan (factors 2,3,5,7,11 plus at most one prime <= 64, within the register budget)";
     return false;
   }
   // per-pass twiddle tables, x passes then y passes
@@ -134,7 +168,7 @@ static bool make_grid2d(int X, int Y, Grid2D& G, std::string& why) {
     int Ns = 1;
     for (int s = 0; s < p->npass; ++s) {
       p->twoff[s] = off;
-      off += (p->rad[s] - 1) * Ns;
+      off += (p->rad[s] - 1) * Ns + (is_native_radix(p->rad[s]) ? 0 : p->rad[s]);
       Ns *= p->rad[s];
     }
   }
@@ -163,6 +197,11 @@ static std::vector<cpx<double>> make_twiddles(const Grid2D& G) {
         for (int k = 0; k < Ns; ++k) {
           const long double a = -2.0L * pi * (long double)(r * k) / (long double)(Ns * R);
           t[p->twoff[s] + (r - 1) * Ns + k] = {(double)cosl(a), (double)sinl(a)};
+        }
+      if (!is_native_radix(R))
+        for (int m = 0; m < R; ++m) {
+          const long double a = -2.0L * pi * (long double)m / (long double)R;
+          t[p->twoff[s] + (R - 1) * Ns + m] = {(double)cosl(a), (double)sinl(a)};
         }
       Ns *= R;
     }
@@ -226,8 +265,10 @@ static void resolve_problem(ccsc_problem& p) {
 // engine capability check (separate from validity: valid reference inputs we
 // do not run yet return CCSC_E_UNSUPPORTED)
 static void check_supported(const ccsc_problem& p, Grid2D* Gout) {
-  if (p.variant == CCSC_L3D || p.variant == CCSC_L4D)
-    throw Err(CCSC_E_UNSUPPORTED, "3D/4D learners are not on the GPU engine yet (SURVEY §8f)");
+  if (p.variant == CCSC_L3D)
+    throw Err(CCSC_E_UNSUPPORTED, "the 3D learner is not on the GPU engine yet (SURVEY §8f)");
+  if ((int64_t)p.K * p.views[0] * p.views[1] > 2048)
+    throw Err(CCSC_E_UNSUPPORTED, "K * views > 2048 exceeds the gram kernel's RHS budget");
   if (p.precision != CCSC_FP64) throw Err(CCSC_E_UNSUPPORTED, "only CCSC_FP64 is built");
   if (p.K > 110) throw Err(CCSC_E_UNSUPPORTED, "K > 110 exceeds the gram kernel's tile budget");
   const int r = p.psf / 2;
@@ -291,8 +332,10 @@ namespace ccsc {
 // memory plan shared by ccsc_plan_bytes and the session
 struct Plan2D {
   int64_t np, nbl, b0;
-  size_t z, yz, cbuf, D, yD, Bhat, b, L, h, Ch, Dh, Zh, misc;
-  size_t total() const { return z + yz + cbuf + D + yD + Bhat + b + L + h + Ch + Dh + Zh + misc; }
+  size_t z, yz, cbuf, D, yD, Bhat, b, L, h, Ch, Dh, Zh, E, misc;
+  size_t total() const {
+    return z + yz + cbuf + D + yD + Bhat + b + L + h + Ch + Dh + Zh + E + misc;
+  }
 };
 
 static Plan2D plan2d(const ccsc_problem& p, const Grid2D& G, int rank, int nranks) {
@@ -300,22 +343,25 @@ static Plan2D plan2d(const ccsc_problem& p, const Grid2D& G, int rank, int nrank
   shard(p, rank, nranks, m.b0, m.nbl);
   m.np = m.nbl * p.ni;
   const size_t P = (size_t)G.X * G.Y, F = G.F, K = p.K;
+  const size_t NV = (size_t)p.views[0] * p.views[1];
   const size_t Kp = K * (K + 1) / 2;
   const size_t s = p.psf;
+  const bool is4 = p.variant == CCSC_L4D;
   m.z = m.np * K * P * 8;
   m.yz = m.z;
-  m.cbuf = (p.tol > 0) ? m.z : 0;
-  m.D = m.nbl * K * P * 8;
+  m.cbuf = (p.tol > 0 && !is4) ? m.z : 0;   // 4D z-step needs no z_old copy (per-slice kernel)
+  m.D = m.nbl * K * NV * P * 8;
   m.yD = m.D;
-  m.Bhat = m.np * F * 16;
-  m.b = m.np * (size_t)p.sb[0] * p.sb[1] * 8;
+  m.Bhat = m.np * NV * F * 16;
+  m.b = m.np * NV * (size_t)p.sb[0] * p.sb[1] * 8;
   m.L = m.nbl * F * Kp * 16;
-  m.h = m.nbl * F * K * 16;
-  m.Ch = m.nbl * K * F * 16;
+  m.h = m.nbl * F * NV * K * 16;
+  m.Ch = m.nbl * K * NV * F * 16;
   m.Dh = m.Ch;
   m.Zh = (size_t)p.ni * K * F * 16;
-  m.misc = (2 * K * F) * 16 + F * 8 + (m.nbl + 2) * K * s * s * 8 * 2 + (4 * m.np + 4 * K + 64) * 8 +
-           (G.X + G.Y) * 16;
+  m.E = is4 ? m.np * K * F * 16 : 0;
+  m.misc = (2 * K * NV * F) * 16 + F * 8 + (m.nbl + 2) * K * NV * s * s * 8 * 2 +
+           (4 * m.np * NV + 4 * K * NV + 64) * 8 + (size_t)G.ntw * 16;
   return m;
 }
 
@@ -324,19 +370,23 @@ static const char* kKernelNames[5] = {"zstep", "gram_chol", "dsolve", "dual_r2c"
 // ---------------------------------------------------------------------------
 // Session: 2D consensus learners (dP / dZ)
 // ---------------------------------------------------------------------------
+// Session for the learners with 2D spatial convolution: dP, dZ and the 4D
+// light-field learner (NV = U*V views share the codes, L4:18-21).
 struct Session2D {
   ccsc_ctx* ctx;
   ccsc_problem p;
   Grid2D G;
   Plan2D m;
   int r, s, K, ni, P, F, Kp;
+  int NV, KG;   // views, filter slices per block (K * NV)
+  bool is4;
   int64_t N, nbl, b0, np;
   bool owner0;
   double theta;
   hipStream_t st;
 
   DevBuf tw, bdev, Bhat, z, yz, cbuf, D, yD, Usup, ssum, supp, Ch, Dh, L, h, Zh, dhat, dtmp, sden,
-      dnorm, znorm, part, pair;
+      dnorm, znorm, part, pair, E;
 
   // host-side log
   int outer_done = 0;
@@ -402,10 +452,12 @@ struct Session2D {
 
   bool verbose_refresh_d() const {
     if (p.variant == CCSC_DPAR) return p.verbose == CCSC_VERBOSE_BRIEF;  // dP:126
+    if (p.variant == CCSC_L4D) return p.verbose == CCSC_VERBOSE_ALL;     // L4:135
     return p.verbose != CCSC_VERBOSE_NONE;                               // dZ:127
   }
   bool verbose_refresh_z() const {
     if (p.variant == CCSC_DPAR) return p.verbose == CCSC_VERBOSE_BRIEF;  // dP:161
+    if (p.variant == CCSC_L4D) return p.verbose == CCSC_VERBOSE_ALL;     // L4:170
     return p.verbose != CCSC_VERBOSE_NONE;                               // dZ:165
   }
 
@@ -422,6 +474,9 @@ struct Session2D {
     P = G.X * G.Y;
     F = G.F;
     Kp = K * (K + 1) / 2;
+    NV = p.views[0] * p.views[1];
+    KG = K * NV;
+    is4 = p.variant == CCSC_L4D;
     N = p.n / ni;
     nbl = m.nbl;
     b0 = m.b0;
@@ -447,34 +502,36 @@ struct Session2D {
     if (m.cbuf) cbuf.alloc(m.cbuf);
     D.alloc(m.D);
     yD.alloc(m.yD);
-    Usup.alloc((size_t)K * s * s * 8);
-    ssum.alloc((size_t)K * s * s * 8);
-    supp.alloc((size_t)nbl * K * s * s * 8);
+    Usup.alloc((size_t)KG * s * s * 8);
+    ssum.alloc((size_t)KG * s * s * 8);
+    supp.alloc((size_t)nbl * KG * s * s * 8);
     Ch.alloc(m.Ch);
     Dh.alloc(m.Dh);
     L.alloc(m.L);
     h.alloc(m.h);
     Zh.alloc(m.Zh);
-    dhat.alloc((size_t)K * F * 16);
-    dtmp.alloc((size_t)K * F * 16);
+    dhat.alloc((size_t)KG * F * 16);
+    dtmp.alloc((size_t)KG * F * 16);
     sden.alloc((size_t)F * 8);
-    dnorm.alloc((size_t)2 * K * 8);
-    znorm.alloc((size_t)2 * std::max<int64_t>(np, 1) * 8);
-    part.alloc((size_t)2 * std::max<int64_t>(np, 1) * 8);
+    dnorm.alloc((size_t)2 * KG * 8);
+    znorm.alloc((size_t)2 * std::max<int64_t>(np * K, 1) * 8);
+    part.alloc((size_t)2 * std::max<int64_t>(np * NV, 1) * 8);
     pair.alloc(4 * 8);
+    if (m.E) E.alloc(m.E);
 
     // data: b (rank-local, [sbx, sby, np] column-major) and its padded spectrum
     const int sbx = (int)p.sb[0], sby = (int)p.sb[1];
     HIPCHK(hipMemcpy(bdev.p, b, m.b, hipMemcpyHostToDevice));
     HIPCHK(launch_r2c_embed<double>(bdev.as<double>(), (int64_t)sbx * sby, sbx, sby, r, r,
-                                    Bhat.as<cpx<double>>(), F, np, tw.as<cpx<double>>(), G, st));
-    // filters: init.d or device RNG (dP:38-39)
+                                    Bhat.as<cpx<double>>(), F, np * NV, tw.as<cpx<double>>(), G,
+                                    st));
+    // filters: init.d or device RNG (dP:38-39; 4D: [psf,psf,U,V,K], L4:39-40)
     DevBuf d0dev;
-    const size_t nd0 = (size_t)s * s * K;
+    const size_t nd0 = (size_t)s * s * KG;
     d0dev.alloc(nd0 * 8);
     if (d0) HIPCHK(hipMemcpy(d0dev.p, d0, nd0 * 8, hipMemcpyHostToDevice));
     else HIPCHK(launch_randn<double>(d0dev.as<double>(), (int64_t)nd0, p.seed ^ 0xd0d0d0d0ULL, 0, st));
-    HIPCHK(launch_embed_filters<double>(d0dev.as<double>(), D.as<double>(), (int)nbl, K, s, G, st));
+    HIPCHK(launch_embed_filters<double>(d0dev.as<double>(), D.as<double>(), (int)nbl, KG, s, G, st));
     HIPCHK(hipMemsetAsync(yD.p, 0, m.yD, st));
     HIPCHK(hipMemsetAsync(Usup.p, 0, Usup.bytes, st));  // u = Pi(0) = 0 (Q2)
     HIPCHK(hipMemsetAsync(yz.p, 0, m.yz, st));
@@ -494,7 +551,7 @@ struct Session2D {
     }
     // dhat = fft2(d) of the initial filters (all blocks share d0, dP:41-42)
     HIPCHK(launch_r2c_embed<double>(D.as<double>(), P, G.X, G.Y, 0, 0, dhat.as<cpx<double>>(),
-                                    F, K, tw.as<cpx<double>>(), G, st));
+                                    F, KG, tw.as<cpx<double>>(), G, st));
     HIPCHK(hipStreamSynchronize(st));
 
     v_obj_d.push_back(std::numeric_limits<double>::quiet_NaN());
@@ -537,8 +594,8 @@ struct Session2D {
   double objective(const cpx<double>* dsp, double* DZdev) {
     HIPCHK(launch_objective<double>(z.as<double>(), dsp, bdev.as<double>(), (int)p.sb[0],
                                     (int)p.sb[1], r, DZdev, part.as<double>(), np,
-                                    tw.as<cpx<double>>(), G, K, st));
-    HIPCHK(launch_sum_pairs<double>(part.as<double>(), (int)np, pair.as<double>(), st));
+                                    tw.as<cpx<double>>(), G, K, NV, st));
+    HIPCHK(launch_sum_pairs<double>(part.as<double>(), (int)(np * NV), pair.as<double>(), st));
     allreduce(pair.as<double>(), 2);
     double h2[2];
     pair_to_host(h2);
@@ -547,8 +604,8 @@ struct Session2D {
   // current filter spectrum of global block 1 into dtmp on every rank
   const cpx<double>* current_dhat() {
     if (owner0)
-      HIPCHK(hipMemcpyAsync(dtmp.p, Dh.p, (size_t)K * F * 16, hipMemcpyDeviceToDevice, st));
-    bcast0(dtmp.as<double>(), (size_t)2 * K * F);
+      HIPCHK(hipMemcpyAsync(dtmp.p, Dh.p, (size_t)KG * F * 16, hipMemcpyDeviceToDevice, st));
+    bcast0(dtmp.as<double>(), (size_t)2 * KG * F);
     return dtmp.as<cpx<double>>();
   }
 
@@ -579,10 +636,10 @@ struct Session2D {
                                       Zh.as<cpx<double>>(), F, (int64_t)ni * K, twc, G, st));
       timed(1, [&] {
         HIPCHK(launch_gram_chol<double>(Zh.as<cpx<double>>(),
-                                        Bhat.as<cpx<double>>() + (size_t)jl * ni * F,
+                                        Bhat.as<cpx<double>>() + (size_t)jl * ni * NV * F,
                                         L.as<cpx<double>>() + (size_t)jl * F * Kp,
-                                        h.as<cpx<double>>() + (size_t)jl * F * K, F, K, ni,
-                                        p.rho_d, st));
+                                        h.as<cpx<double>>() + (size_t)jl * F * NV * K, F, K,
+                                        ni, p.rho_d, NV, st));
       });
     }
     // ---- D iterations (dP:103-134) ----
@@ -592,27 +649,28 @@ struct Session2D {
     for (int id = 0; id < p.max_it_d; ++id) {
       timed(3, [&] {
         HIPCHK(launch_dual_r2c<double>(D.as<double>(), yD.as<double>(), Usup.as<double>(),
-                                       Ch.as<cpx<double>>(), nbl * K, twc, G, K, r, st));
+                                       Ch.as<cpx<double>>(), nbl * KG, twc, G, KG, r, st));
       });
       timed(2, [&] {
         HIPCHK(launch_dsolve<double>(L.as<cpx<double>>(), h.as<cpx<double>>(),
                                      Ch.as<cpx<double>>(), Dh.as<cpx<double>>(), (int)nbl, F, K,
-                                     p.rho_d, st));
+                                     p.rho_d, NV, st));
       });
       timed(4, [&] {
         HIPCHK(launch_c2r_dout<double>(Dh.as<cpx<double>>(), D.as<double>(), yD.as<double>(),
                                        supp.as<double>(), dnorm.as<double>(),
-                                       owner0 ? K : 0, nbl * K, twc, G, r, st));
+                                       owner0 ? KG : 0, nbl * KG, twc, G, r, st));
       });
       HIPCHK(launch_supp_reduce<double>(supp.as<double>(), ssum.as<double>(), (int)nbl,
-                                        K * s * s, st));
-      allreduce(ssum.as<double>(), (size_t)K * s * s);
-      HIPCHK(launch_project<double>(ssum.as<double>(), Usup.as<double>(), K, s * s,
+                                        KG * s * s, st));
+      allreduce(ssum.as<double>(), (size_t)KG * s * s);
+      // Pi normalises per filter (2D, dP:212-213) / per (u,v,k) slice (4D, L4:224-225)
+      HIPCHK(launch_project<double>(ssum.as<double>(), Usup.as<double>(), KG, s * s,
                                     1.0 / (double)N, st));
       ++nd;
       double dd = std::numeric_limits<double>::quiet_NaN();
       if (tol_on) {
-        if (owner0) HIPCHK(launch_sum_pairs<double>(dnorm.as<double>(), K, pair.as<double>(), st));
+        if (owner0) HIPCHK(launch_sum_pairs<double>(dnorm.as<double>(), KG, pair.as<double>(), st));
         else HIPCHK(hipMemsetAsync(pair.p, 0, 2 * sizeof(double), st));
         allreduce(pair.as<double>(), 2);
         double h2[2];
@@ -629,24 +687,34 @@ struct Session2D {
       if (tol_on && dd < p.tol) break;  // dP:130-132
     }
     // ---- Z precompute (dP:143-144): d = Dhat of block 1 ----
-    if (owner0) HIPCHK(hipMemcpyAsync(dhat.p, Dh.p, (size_t)K * F * 16, hipMemcpyDeviceToDevice, st));
-    bcast0(dhat.as<double>(), (size_t)2 * K * F);
-    HIPCHK(launch_sden<double>(dhat.as<cpx<double>>(), sden.as<double>(), F, K, p.rho_z,
+    if (owner0) HIPCHK(hipMemcpyAsync(dhat.p, Dh.p, (size_t)KG * F * 16, hipMemcpyDeviceToDevice, st));
+    bcast0(dhat.as<double>(), (size_t)2 * KG * F);
+    // s(f) = sum over filters (and views, L4:277,330) of |dhat|^2
+    HIPCHK(launch_sden<double>(dhat.as<cpx<double>>(), sden.as<double>(), F, KG, p.rho_z,
                                1.0 / (double)P, st));
+    if (is4)   // L4:327 first term, constant over the z-iterations
+      HIPCHK(launch_view_corr<double>(dhat.as<cpx<double>>(), Bhat.as<cpx<double>>(),
+                                      E.as<cpx<double>>(), np, F, K, NV, st));
     // ---- Z iterations (dP:147-168) ----
     const bool want_oz = verbose_refresh_z() || p.trace_objective;
     int nz = 0;
     for (int iz = 0; iz < p.max_it_z; ++iz) {
       timed(0, [&] {
-        HIPCHK(launch_zstep<double>(z.as<double>(), yz.as<double>(), cbuf.as<double>(),
-                                    Bhat.as<cpx<double>>(), dhat.as<cpx<double>>(),
-                                    sden.as<double>(), np, twc, G, K, theta, znorm.as<double>(),
-                                    tol_on, st));
+        if (is4)
+          HIPCHK(launch_zstep_diag<double>(z.as<double>(), yz.as<double>(), E.as<cpx<double>>(),
+                                           sden.as<double>(), np * K, twc, G, theta, p.rho_z,
+                                           znorm.as<double>(), tol_on, st));
+        else
+          HIPCHK(launch_zstep<double>(z.as<double>(), yz.as<double>(), cbuf.as<double>(),
+                                      Bhat.as<cpx<double>>(), dhat.as<cpx<double>>(),
+                                      sden.as<double>(), np, twc, G, K, theta,
+                                      znorm.as<double>(), tol_on, st));
       });
       ++nz;
       double zd = std::numeric_limits<double>::quiet_NaN();
       if (tol_on) {
-        HIPCHK(launch_sum_pairs<double>(znorm.as<double>(), (int)np, pair.as<double>(), st));
+        HIPCHK(launch_sum_pairs<double>(znorm.as<double>(), (int)(is4 ? np * K : np),
+                                        pair.as<double>(), st));
         allreduce(pair.as<double>(), 2);
         double h2[2];
         pair_to_host(h2);
@@ -697,15 +765,15 @@ struct Session2D {
     if (!out) return;
     if (out->d_res) {
       // D1 lives on rank 0 (block 1); broadcast so every rank returns it.
-      std::vector<double> D1((size_t)K * P);
+      std::vector<double> D1((size_t)KG * P);
       DevBuf tmp;
-      tmp.alloc((size_t)K * P * 8);
+      tmp.alloc((size_t)KG * P * 8);
       if (owner0) HIPCHK(hipMemcpyAsync(tmp.p, D.p, tmp.bytes, hipMemcpyDeviceToDevice, st));
-      bcast0(tmp.as<double>(), (size_t)K * P);
+      bcast0(tmp.as<double>(), (size_t)KG * P);
       HIPCHK(hipMemcpyAsync(D1.data(), tmp.p, tmp.bytes, hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));
-      // d_res = circshift(D1, +r)(1:psf, 1:psf, :)   (dP:195-196)
-      for (int k = 0; k < K; ++k)
+      // d_res = circshift(D1, +r)(1:psf, 1:psf, :)   (dP:195-196; 4D L4:208-209: per view)
+      for (int k = 0; k < KG; ++k)
         for (int j = 0; j < s; ++j)
           for (int i = 0; i < s; ++i) {
             const int x = (i - r + G.X) % G.X, y = (j - r + G.Y) % G.Y;
@@ -718,7 +786,7 @@ struct Session2D {
     if (out->DZ) {
       // DZ = real(ifft2(sum_k zhat .* dup{1}))  (dP:193), uncropped [X,Y,1,n]
       DevBuf dz;
-      dz.alloc((size_t)np * P * 8);
+      dz.alloc(is4 ? (size_t)np * NV * p.sb[0] * p.sb[1] * 8 : (size_t)np * P * 8);
       objective(dhat.as<cpx<double>>(), dz.as<double>());
       HIPCHK(hipMemcpy(out->DZ, dz.p, dz.bytes, hipMemcpyDeviceToHost));
     }
@@ -755,6 +823,8 @@ struct Session2D {
     const double Pd = P, Fd = F, Kd = K;
     switch (id) {
       case 0:  // z-iteration compulsory state traffic: read z,y + write z,y (fp64), B per patch
+        if (is4)  // + E per slice
+          return (double)np * Kd * (4.0 * 8.0 * Pd + 16.0 * Fd) + Fd * 8.0;
         return (double)np * Kd * 4.0 * 8.0 * Pd + (double)np * 16.0 * Fd + Kd * Fd * 16.0;
       case 1:  // gram+chol per block: read A (ni x K x F) + b, write L, h
         return (double)ni * Kd * Fd * 16.0 + ni * Fd * 16.0 + Fd * Kp * 16.0 + Fd * Kd * 16.0;

@@ -192,8 +192,14 @@ struct Plan1D {
   int npass;
   int rad[kMaxPass];
   int twoff[kMaxPass];  // offset (complex units) of pass s's twiddle table,
-                        // entries (r-1)*Ns + k = exp(-2 pi i r k / (Ns R))
+                        // entries (r-1)*Ns + k = exp(-2 pi i r k / (Ns R)); a
+                        // generic-radix pass appends its R roots exp(-2 pi i m/R)
 };
+// Radices with an unrolled in-register butterfly; any other prime factor (up
+// to kMaxGenericRadix, e.g. 37 for the 74-point grids of the 3D/4D configs)
+// runs through fft_pass_generic.
+constexpr int kMaxGenericRadix = 64;
+constexpr int kMaxGenericOut = 4;  // outputs per thread of a generic pass
 
 // Per-slice description of the 2D grid (all in units of T unless noted).
 struct Grid2D {
@@ -327,20 +333,77 @@ __device__ __forceinline__ void fft_pass(T* lds, int mode, const LineGeom& gin,
   lds_sync();
 }
 
+// Generic radix-R Stockham pass (R not unrolled): every output element is an
+// R-term sum read straight from LDS,
+//   out[(j-k)R + k + q Ns] = sum_r x[j + r nb] tw(r, k) w^(r q),   w = e^(SIGN 2 pi i/R),
+// so a thread only keeps its (<= kMaxGenericOut) outputs across the barrier.
+template <typename T, int SIGN>
+__device__ __forceinline__ void fft_pass_generic(T* lds, int R, int mode, const LineGeom& gin,
+                                              const LineGeom& gout, const Grid2D& G, int n,
+                                              int Ns, const cpx<T>* __restrict__ tw) {
+  const int nb = n / R;
+  const int nl = gin.nlines;
+  const int total = nl * n;
+  const bool along = gin.estride == 1;
+  const cpx<T>* roots = tw + (R - 1) * Ns;
+  cpx<T> acc[kMaxGenericOut];
+  int dst[kMaxGenericOut];
+#pragma unroll
+  for (int i = 0; i < kMaxGenericOut; ++i) {
+    const int o = (int)threadIdx.x + i * kNT;
+    dst[i] = -1;
+    if (o < total) {
+      int line, t;
+      if (along) {
+        line = o / n;
+        t = o - line * n;
+      } else {
+        t = o / nl;
+        line = o - t * nl;
+      }
+      const int k = t % Ns;
+      const int q = (t / Ns) % R;
+      const int j = (t / (Ns * R)) * Ns + k;
+      cpx<T> a = load_elem<T>(lds, gin, G, mode, line, j);
+      int m = 0;
+      for (int r = 1; r < R; ++r) {
+        cpx<T> x = load_elem<T>(lds, gin, G, mode, line, j + r * nb);
+        if (Ns > 1) {
+          cpx<T> w = tw[(r - 1) * Ns + k];
+          if (SIGN > 0) w.y = -w.y;
+          x = cmul(x, w);
+        }
+        m += q;
+        if (m >= R) m -= R;
+        cpx<T> rt = roots[m];
+        if (SIGN > 0) rt.y = -rt.y;
+        a = cadd(a, cmul(x, rt));
+      }
+      acc[i] = a;
+      dst[i] = line * gout.lstride + t * gout.estride;
+    }
+  }
+  lds_sync();
+#pragma unroll
+  for (int i = 0; i < kMaxGenericOut; ++i)
+    if (dst[i] >= 0) lds_cpx_store(lds + dst[i], gout.imoff, acc[i]);
+  lds_sync();
+}
+
 template <typename T, int MAXB, int SIGN>
 __device__ __forceinline__ void fft_pass_dispatch(int R, T* lds, int mode, const LineGeom& gin,
                                                   const LineGeom& gout, const Grid2D& G, int n,
                                                   int Ns, const cpx<T>* tw) {
   switch (R) {
-    case 2: fft_pass<T, 2, MAXB, SIGN>(lds, mode, gin, gout, G, n, Ns, tw); break;
-    case 3: fft_pass<T, 3, MAXB, SIGN>(lds, mode, gin, gout, G, n, Ns, tw); break;
-    case 4: fft_pass<T, 4, MAXB, SIGN>(lds, mode, gin, gout, G, n, Ns, tw); break;
-    case 5: fft_pass<T, 5, MAXB, SIGN>(lds, mode, gin, gout, G, n, Ns, tw); break;
-    case 7: fft_pass<T, 7, MAXB, SIGN>(lds, mode, gin, gout, G, n, Ns, tw); break;
-    case 8: fft_pass<T, 8, MAXB, SIGN>(lds, mode, gin, gout, G, n, Ns, tw); break;
-    case 10: fft_pass<T, 10, MAXB, SIGN>(lds, mode, gin, gout, G, n, Ns, tw); break;
-    case 11: fft_pass<T, 11, MAXB, SIGN>(lds, mode, gin, gout, G, n, Ns, tw); break;
-    default: break;  // host planner only emits the radices above (kRadices in engine.cpp)
+    case 2: fft_pass<T, 2, maxb_for_radix(2), SIGN>(lds, mode, gin, gout, G, n, Ns, tw); break;
+    case 3: fft_pass<T, 3, maxb_for_radix(3), SIGN>(lds, mode, gin, gout, G, n, Ns, tw); break;
+    case 4: fft_pass<T, 4, maxb_for_radix(4), SIGN>(lds, mode, gin, gout, G, n, Ns, tw); break;
+    case 5: fft_pass<T, 5, maxb_for_radix(5), SIGN>(lds, mode, gin, gout, G, n, Ns, tw); break;
+    case 7: fft_pass<T, 7, maxb_for_radix(7), SIGN>(lds, mode, gin, gout, G, n, Ns, tw); break;
+    case 8: fft_pass<T, 8, maxb_for_radix(8), SIGN>(lds, mode, gin, gout, G, n, Ns, tw); break;
+    case 10: fft_pass<T, 10, maxb_for_radix(10), SIGN>(lds, mode, gin, gout, G, n, Ns, tw); break;
+    case 11: fft_pass<T, 11, maxb_for_radix(11), SIGN>(lds, mode, gin, gout, G, n, Ns, tw); break;
+    default: fft_pass_generic<T, SIGN>(lds, R, mode, gin, gout, G, n, Ns, tw); break;
   }
 }
 

@@ -40,20 +40,29 @@ hipError_t launch_zstep(T* z, T* yz, T* cbuf, const cpx<T>* Bhat, const cpx<T>* 
 template <typename T>
 hipError_t launch_objective(const T* z, const cpx<T>* dhat, const T* b, int sbx, int sby, int r,
                             T* DZ, T* part, int64_t npatch, const cpx<T>* tw, const Grid2D& G,
-                            int K, hipStream_t st);
+                            int K, int NV, hipStream_t st);
+template <typename T>
+hipError_t launch_zstep_diag(T* z, T* yz, const cpx<T>* E, const T* sden, int64_t nslices,
+                             const cpx<T>* tw, const Grid2D& G, T theta, T rho, T* znorm,
+                             bool tol, hipStream_t st);
+template <typename T>
+hipError_t launch_view_corr(const cpx<T>* dhat, const cpx<T>* Bhat, cpx<T>* E, int64_t npatch,
+                            int F, int K, int NV, hipStream_t st);
 template <typename T>
 hipError_t launch_sum_pairs(const T* part, int count, T* out, hipStream_t st);
 
 // ---- dstep.hip ------------------------------------------------------------
 // Per frequency f of one block: G = A^H A + rho I (A = ni x K code spectra),
 // h = A^H b, Cholesky G = L L^H; L packed lower column-major per f.
+// NV views: h [F][NV][K], B [ni][NV][F] (NV = 1 in 2D).
 template <typename T>
 hipError_t launch_gram_chol(const cpx<T>* Zh, const cpx<T>* Bh, cpx<T>* L, cpx<T>* h, int F,
-                            int K, int ni, T rho, hipStream_t st);
-// x_f = (L L^H)^{-1} (h_f + rho * C_f) for every (block, f); writes Dh [blk][K][F].
+                            int K, int ni, T rho, int NV, hipStream_t st);
+// x_{f,uv} = (L L^H)^{-1} (h_{f,uv} + rho * C_{f,uv}) for every (block, f, view);
+// C and Dh are [blk][K][NV][F].
 template <typename T>
 hipError_t launch_dsolve(const cpx<T>* L, const cpx<T>* h, const cpx<T>* Ch, cpx<T>* Dh,
-                         int nblocks, int F, int K, T rho, hipStream_t st);
+                         int nblocks, int F, int K, T rho, int NV, hipStream_t st);
 
 // ---- util.hip ---------------------------------------------------------------
 template <typename T>

@@ -72,8 +72,9 @@ __global__ __launch_bounds__(kNT) void k_c2r_plain(const cpx<T>* __restrict__ sr
 // ---------------------------------------------------------------------------
 // D-step, part 1 (dP:109-110): y_j += D_j - u ; C_j = fft2(u - y_j).
 // u is zero off the (2r+1)^2 support; Usup holds its support values
-// [K][s][s] with support coordinate (x + r) mod X (KernelConstraintProj layout).
-// slice = jl*K + k over the local blocks.
+// [KG][s][s] with support coordinate (x + r) mod X (KernelConstraintProj layout).
+// slice = jl*KG + g over the local blocks; g = k*NV + uv (KG = K*NV filter
+// slices per block: NV = 1 in 2D, the U*V views in 4D).
 // ---------------------------------------------------------------------------
 template <typename T>
 __global__ __launch_bounds__(kNT) void k_dual_r2c(const T* __restrict__ D, T* __restrict__ yD,
@@ -85,11 +86,11 @@ __global__ __launch_bounds__(kNT) void k_dual_r2c(const T* __restrict__ D, T* __
   Smem<T> S = carve<T>(smem, G);
   load_twiddles(S.tw, twg, G.ntw);
   const int slice = blockIdx.x;
-  const int k = slice % K;
+  const int g = slice % K;   // K here = KG filter slices per block
   const int s = 2 * r + 1;
   const int P = G.X * G.Y;
   const int64_t off = (int64_t)slice * P;
-  const T* u = Usup + (int64_t)k * s * s;
+  const T* u = Usup + (int64_t)g * s * s;
   for (int e = threadIdx.x; e < P; e += kNT) {
     const int y = e / G.X, x = e - y * G.X;
     const int sxx = (x + r) % G.X, syy = (y + r) % G.Y;
@@ -205,6 +206,22 @@ __global__ void k_sden(const cpx<T>* __restrict__ dhat, T* __restrict__ sden, in
   sden[f] = invP / (rho + s);
 }
 
+// 4D z-step precompute (L4:327 first term): E[p][k][f] = sum_uv conj(d[k][uv][f]) B[p][uv][f]
+template <typename T>
+__global__ void k_view_corr(const cpx<T>* __restrict__ dhat, const cpx<T>* __restrict__ Bhat,
+                            cpx<T>* __restrict__ E, int F, int K, int NV) {
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  const int p = blockIdx.y;
+  if (f >= F) return;
+  const cpx<T>* Bp = Bhat + (int64_t)p * NV * F + f;
+  for (int k = 0; k < K; ++k) {
+    cpx<T> a = {(T)0, (T)0};
+    const cpx<T>* dk = dhat + (int64_t)k * NV * F + f;
+    for (int uv = 0; uv < NV; ++uv) a = cadd(a, cmulc(dk[(int64_t)uv * F], Bp[(int64_t)uv * F]));
+    E[((int64_t)p * K + k) * F + f] = a;
+  }
+}
+
 // sum of pairs: out[0] = sum part[2i], out[1] = sum part[2i+1]  (one block)
 template <typename T>
 __global__ __launch_bounds__(256) void k_sum_pairs(const T* __restrict__ part, int count,
@@ -304,6 +321,15 @@ hipError_t launch_sden(const cpx<T>* dhat, T* sden, int F, int K, T rho, T invP,
 }
 
 template <typename T>
+hipError_t launch_view_corr(const cpx<T>* dhat, const cpx<T>* Bhat, cpx<T>* E, int64_t npatch,
+                            int F, int K, int NV, hipStream_t st) {
+  if (npatch <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_view_corr<T>, dim3((F + 255) / 256, (unsigned)npatch), dim3(256), 0, st,
+                     dhat, Bhat, E, F, K, NV);
+  return hipGetLastError();
+}
+
+template <typename T>
 hipError_t launch_sum_pairs(const T* part, int count, T* out, hipStream_t st) {
   hipLaunchKernelGGL(k_sum_pairs<T>, dim3(1), dim3(256), 0, st, part, count, out);
   return hipGetLastError();
@@ -322,7 +348,9 @@ hipError_t launch_sum_pairs(const T* part, int count, T* out, hipStream_t st) {
   template hipError_t launch_supp_reduce<T>(const T*, T*, int, int, hipStream_t);               \
   template hipError_t launch_project<T>(const T*, T*, int, int, T, hipStream_t);                \
   template hipError_t launch_sden<T>(const cpx<T>*, T*, int, int, T, T, hipStream_t);           \
-  template hipError_t launch_sum_pairs<T>(const T*, int, T*, hipStream_t);
+  template hipError_t launch_sum_pairs<T>(const T*, int, T*, hipStream_t);                       \
+  template hipError_t launch_view_corr<T>(const cpx<T>*, const cpx<T>*, cpx<T>*, int64_t, int,   \
+                                          int, int, hipStream_t);
 
 CCSC_INST2D(double)
 

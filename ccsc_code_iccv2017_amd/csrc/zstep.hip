@@ -194,6 +194,83 @@ __global__ __launch_bounds__(kNT) void k_zstep(T* __restrict__ z, T* __restrict_
   }
 }
 
+// ---------------------------------------------------------------------------
+// 4D z-iteration (L4:159-164 with the diagonal solve of L4:310-347): the
+// reference's z-solve has no coupling across filters,
+//   zhat = (sum_uv conj(d_uv) B_uv + rho C) / (rho + sum_{uv,k} |d_uv,k|^2),
+// so one workgroup per (patch, filter) slice: prox + dual + R2C, scale, C2R.
+// E = sum_uv conj(d) B is precomputed once per outer iteration (k_view_corr);
+// sden = 1/((rho + s) X Y).  z stays real (Q8: the reference's imaginary part
+// is round-off).  Traffic per slice: read z, y, E; write y, z.
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(kNT) void k_zstep_diag(T* __restrict__ z, T* __restrict__ yz,
+                                                    const cpx<T>* __restrict__ E,
+                                                    const T* __restrict__ sden,
+                                                    const cpx<T>* __restrict__ twg, Grid2D G,
+                                                    T theta, T rho, T* __restrict__ znorm,
+                                                    int TOL) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  Smem<T> S = carve<T>(smem, G);
+  load_twiddles(S.tw, twg, G.ntw);
+  const int64_t slice = blockIdx.x;
+  const int P = G.X * G.Y;
+  const int F = G.F;
+  const int64_t off = slice * P;
+  lds_sync();
+  for (int e = threadIdx.x; e < P; e += kNT) {
+    const int y = e / G.X, x = e - y * G.X;
+    const T zv = z[off + e], yv = yz[off + e];
+    const T a = zv + yv;
+    const T aa = fabs(a);
+    const T u = ((aa > theta) ? (T)1 - theta / aa : (T)0) * a;
+    const T yn = yv + zv - u;
+    yz[off + e] = yn;
+    S.slice[y * G.RS + x] = u - yn;
+  }
+  zero_pad_row(S.slice, G);
+  slice_r2c<T, kMaxB>(S.slice, G, S.tw);
+  const cpx<T>* Es = E + slice * F;
+  for (int f = threadIdx.x; f < F; f += kNT) {
+    T* q = S.slice + bin_off(f, G);
+    const cpx<T> c = lds_cpx(q, 1);
+    const cpx<T> e = Es[f];
+    const T sc = sden[f];
+    lds_cpx_store(q, 1, cpx<T>{(e.x + rho * c.x) * sc, (e.y + rho * c.y) * sc});
+  }
+  slice_c2r<T, kMaxB>(S.slice, G, S.tw);
+  T nd = 0, nz = 0;
+  for (int e = threadIdx.x; e < P; e += kNT) {
+    const int y = e / G.X, x = e - y * G.X;
+    const T zn = S.slice[y * G.RS + x];
+    if (TOL) {
+      const T zo = z[off + e];
+      nd += (zn - zo) * (zn - zo);
+      nz += zn * zn;
+    }
+    z[off + e] = zn;
+  }
+  if (TOL) {
+    nd = block_sum(nd, S.red);
+    nz = block_sum(nz, S.red);
+    if (threadIdx.x == 0) {
+      znorm[2 * slice] = nd;
+      znorm[2 * slice + 1] = nz;
+    }
+  }
+}
+
+template <typename T>
+hipError_t launch_zstep_diag(T* z, T* yz, const cpx<T>* E, const T* sden, int64_t nslices,
+                             const cpx<T>* tw, const Grid2D& G, T theta, T rho, T* znorm,
+                             bool tol, hipStream_t st) {
+  if (nslices <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_zstep_diag<T>, dim3((unsigned)nslices), dim3(kNT),
+                     slice_smem_bytes(G, sizeof(T)), st, z, yz, E, sden, tw, G, theta, rho,
+                     znorm, tol ? 1 : 0);
+  return hipGetLastError();
+}
+
 template <typename T>
 hipError_t launch_zstep(T* z, T* yz, T* cbuf, const cpx<T>* Bhat, const cpx<T>* dhat,
                         const T* sden, int64_t npatch, const cpx<T>* tw, const Grid2D& G, int K,
@@ -207,6 +284,10 @@ hipError_t launch_zstep(T* z, T* yz, T* cbuf, const cpx<T>* Bhat, const cpx<T>* 
   return hipGetLastError();
 }
 
+template hipError_t launch_zstep_diag<double>(double*, double*, const cpx<double>*,
+                                              const double*, int64_t, const cpx<double>*,
+                                              const Grid2D&, double, double, double*, bool,
+                                              hipStream_t);
 template hipError_t launch_zstep<double>(double*, double*, double*, const cpx<double>*,
                                          const cpx<double>*, const double*, int64_t,
                                          const cpx<double>*, const Grid2D&, int, double, double*,

@@ -96,9 +96,13 @@ def make_problem(variant, b_shape, kernel_size, lambda_residual, lambda_prior, m
                  theta_div=None, trace_objective=False, seed=0, precision="fp64"):
     p = L.Problem()
     p.variant = variant
-    p.ndim = 2
+    p.ndim = 3 if variant == L.CCSC_L3D else 2
     p.sb[0], p.sb[1] = int(b_shape[0]), int(b_shape[1])
+    if variant == L.CCSC_L3D:
+        p.sb[2] = int(b_shape[2])
     p.views[0] = p.views[1] = 1
+    if variant == L.CCSC_L4D:                  # b: [x, y, U, V, n]; kernel [s, s, U, V, K]
+        p.views[0], p.views[1] = int(kernel_size[2]), int(kernel_size[3])
     p.n = int(b_shape[-1])
     p.K = int(kernel_size[-1])
     p.psf = int(kernel_size[0])
@@ -198,9 +202,16 @@ class Session:
     def results(self, want_z=True, want_DZ=True, want_obj=False):
         X, Y = self.grid()
         p = self.p
-        d_res = np.zeros((p.psf, p.psf, p.K), order="F")
-        z_res = np.zeros((X, Y, p.K, self.n_local), order="F") if want_z else None
-        DZ = np.zeros((X, Y, 1, self.n_local), order="F") if want_DZ else None
+        if p.variant == L.CCSC_L4D:
+            U, V = p.views[0], p.views[1]
+            d_res = np.zeros((p.psf, p.psf, U, V, p.K), order="F")
+            z_res = np.zeros((X, Y, 1, 1, p.K, self.n_local), order="F") if want_z else None
+            DZ = (np.zeros((p.sb[0], p.sb[1], U, V, self.n_local), order="F")
+                  if want_DZ else None)
+        else:
+            d_res = np.zeros((p.psf, p.psf, p.K), order="F")
+            z_res = np.zeros((X, Y, p.K, self.n_local), order="F") if want_z else None
+            DZ = np.zeros((X, Y, 1, self.n_local), order="F") if want_DZ else None
         obj = np.zeros(1) if want_obj else None
         out = L.Outputs(L.dptr(d_res), L.dptr(z_res), L.dptr(DZ), L.dptr(obj))
         eb = L.errbuf()
@@ -293,6 +304,53 @@ def admm_learn_conv2D_large_dzParallel(b, kernel_size, lambda_residual, lambda_p
     """Drop-in for 2D/admm_learn_conv2D_large_dzParallel.m:1-206."""
     return _learn_2d(L.CCSC_DZPAR, b, kernel_size, lambda_residual, lambda_prior, max_it, tol,
                      verbose, init, **kw)
+
+
+def admm_learn_conv4D_lightfield(b, kernel_size, lambda_residual, lambda_prior, max_it, tol,
+                                 verbose, init=None, ctx=None, device=0, want_z=True,
+                                 want_DZ=True, **kw):
+    """Drop-in for 4D/admm_learn_conv4D_lightfield.m:1-212.
+
+    b: [x, y, U, V, n] (single in the reference driver, Q15: widened to double);
+    kernel_size = [psf, psf, U, V, K].  Returns (d_res [psf,psf,U,V,K],
+    z_res [X,Y,1,1,K,n] complex (real part computed, Q8), DZ [x,y,U,V,n],
+    obj_val, iterations) -- iterations carries empty fields like the reference
+    (L4:64-72) plus the engine's 'trace'.
+    """
+    b = np.asarray(b, dtype=np.float64)
+    if b.ndim == 4:
+        b = b[..., None]
+    if b.ndim != 5:
+        raise ValueError("b must be [x, y, U, V, n]")
+    own = ctx is None
+    if own:
+        ctx = Context(device)
+    try:
+        p = make_problem(L.CCSC_L4D, b.shape, kernel_size, lambda_residual, lambda_prior,
+                         max_it, tol, verbose, **kw)
+        d0 = z0 = None
+        if init is not None and len(init) > 0:
+            d0 = init.get("d")
+            z0 = init.get("z")
+            if z0 is not None:
+                z0 = np.real(np.asarray(z0))
+        s = Session(ctx, p, b, d0, z0)
+        try:
+            done = False
+            while s.outer < s.p.max_it and not done:
+                done = s.step(1)
+            d_res, z_res, DZ, obj = s.results(want_z=want_z, want_DZ=want_DZ, want_obj=True)
+            log = s.iterlog()
+        finally:
+            s.close()
+    finally:
+        if own:
+            ctx.close()
+    iterations = {"obj_vals_d": [], "obj_vals_z": [], "tim_vals": [], "it_vals": [],
+                  "trace": log["trace"], "engine_tim_vals": log["tim_vals"]}
+    if z_res is not None:
+        z_res = z_res.astype(np.complex128)
+    return d_res, z_res, DZ, obj, iterations
 
 
 def fft2d_test(ctx: Context, slices):

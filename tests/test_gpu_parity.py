@@ -20,7 +20,8 @@ def _rel(a, b):
     return np.linalg.norm((a - b).ravel()) / max(np.linalg.norm(b.ravel()), 1e-300)
 
 
-@pytest.mark.parametrize("X,Y", [(16, 16), (110, 110), (15, 14), (14, 15), (24, 20)])
+@pytest.mark.parametrize("X,Y", [(16, 16), (110, 110), (15, 14), (14, 15), (24, 20), (74, 74),
+                                 (26, 37), (60, 60)])
 def test_fft2d_r2c_c2r(gpu_ctx, X, Y):
     from ccsc_code_iccv2017_amd.learners import fft2d_test
     rng = np.random.default_rng(X * 1000 + Y)
@@ -70,5 +71,33 @@ def test_learn_2d_matches_oracle(gpu_ctx, variant, sb, psf, K, n, ni):
     assert _rel(DZ_e, DZ_o) < 1e-7
     np.testing.assert_allclose(it_e["obj_vals_d"], it_o["obj_vals_d"], rtol=1e-9)
     np.testing.assert_allclose(it_e["obj_vals_z"], it_o["obj_vals_z"], rtol=1e-9)
+    np.testing.assert_allclose(it_e["trace"]["obj_d"], np.array(tr_o["obj_d"]), rtol=1e-9)
+    np.testing.assert_allclose(it_e["trace"]["obj_z"], np.array(tr_o["obj_z"]), rtol=1e-9)
+
+
+@pytest.mark.parametrize("sb,UV,psf,K,n", [((10, 9), 2, 5, 3, 4), ((9, 9), 3, 5, 2, 9),
+                                           ((64, 64), 5, 11, 4, 4)])
+def test_learn_4d_matches_oracle(gpu_ctx, sb, UV, psf, K, n):
+    """4D light-field learner (L4:1-212): spatial-only convolution over U x V views,
+    per-view D-solves sharing one factor, diagonal z-solve (Q7), per-slice projection (Q10)."""
+    from ccsc_code_iccv2017_amd import learners as E
+    rng = np.random.default_rng(11)
+    r = psf // 2
+    X, Y = sb[0] + 2 * r, sb[1] + 2 * r
+    b = rng.standard_normal((sb[0], sb[1], UV, UV, n))
+    d0 = rng.standard_normal((psf, psf, UV, UV, K))
+    z0 = rng.standard_normal((X, Y, 1, 1, K, n))
+    ks = [psf, psf, UV, UV, K]
+    init = {"d": d0, "z": z0}
+    d_o, z_o, DZ_o, obj_o, it_o, tr_o = O.learn_4d(b, ks, 1.0, 1.0, 2, 0.0, "all", init,
+                                                   trace_objective=True)
+    d_e, z_e, DZ_e, obj_e, it_e = E.admm_learn_conv4D_lightfield(b, ks, 1.0, 1.0, 2, 0.0, "all",
+                                                                 init, trace_objective=True,
+                                                                 ctx=gpu_ctx)
+    assert _rel(d_e, d_o) < 1e-7
+    assert _rel(z_e.real, z_o.real) < 1e-7
+    assert np.abs(z_o.imag).max() < 1e-9 * np.abs(z_o.real).max()   # Q8: round-off only
+    assert _rel(DZ_e, DZ_o) < 1e-7
+    assert abs(obj_e - obj_o) <= 1e-9 * abs(obj_o)
     np.testing.assert_allclose(it_e["trace"]["obj_d"], np.array(tr_o["obj_d"]), rtol=1e-9)
     np.testing.assert_allclose(it_e["trace"]["obj_z"], np.array(tr_o["obj_z"]), rtol=1e-9)
