@@ -186,6 +186,33 @@ static bool make_grid2d(int X, int Y, Grid2D& G, std::string& why) {
   return true;
 }
 
+// Tile of the t-direction FFT of the 3D learner: Tn rows of Xh complex lines
+// (plan in Gt.py; Gt.px unused).
+static bool make_gridt(int Tn, int Xh, Grid2D& Gt, std::string& why) {
+  Gt = Grid2D{};
+  Gt.Y = Gt.Yp = Tn;
+  Gt.Xh = Xh;
+  Gt.RS = 2 * Xh;  // lanes run along x' (lines): 16-B consecutive, conflict-free
+  Gt.F = Xh * Tn;
+  Gt.px = Plan1D{1, 0, {0}, {0}};
+  if (!plan1d(Tn, Xh, Gt.py)) {
+    why = "grid length " + std::to_string(Tn) + " has no radix plan for the t-direction FFT";
+    return false;
+  }
+  int off = 0, Ns = 1;
+  for (int s = 0; s < Gt.py.npass; ++s) {
+    Gt.py.twoff[s] = off;
+    off += (Gt.py.rad[s] - 1) * Ns + (is_native_radix(Gt.py.rad[s]) ? 0 : Gt.py.rad[s]);
+    Ns *= Gt.py.rad[s];
+  }
+  Gt.ntw = std::max(off, 1);
+  if (tfft_smem_bytes(Gt, sizeof(double)) > 160 * 1024) {
+    why = "t-direction tile does not fit one CU's LDS";
+    return false;
+  }
+  return true;
+}
+
 static std::vector<cpx<double>> make_twiddles(const Grid2D& G) {
   std::vector<cpx<double>> t(G.ntw, cpx<double>{1.0, 0.0});
   const long double pi = 3.141592653589793238462643383279502884L;
@@ -262,21 +289,34 @@ static void resolve_problem(ccsc_problem& p) {
     if (p.sb[i] + 2 * r < p.psf) throw Err(CCSC_E_INVALID, "grid smaller than the filter");
 }
 
+// Transform geometry of one slice: the (x, y) plane grid and, for the 3D
+// learner, the t-direction tile (Tn = 1 otherwise).
+struct Geom {
+  Grid2D G{};
+  Grid2D Gt{};
+  int Tn = 1;
+  int64_t P() const { return (int64_t)G.X * G.Y * Tn; }   // voxels per slice
+  int64_t F() const { return (int64_t)G.F * Tn; }         // half-spectrum bins per slice
+};
+
 // engine capability check (separate from validity: valid reference inputs we
 // do not run yet return CCSC_E_UNSUPPORTED)
-static void check_supported(const ccsc_problem& p, Grid2D* Gout) {
-  if (p.variant == CCSC_L3D)
-    throw Err(CCSC_E_UNSUPPORTED, "the 3D learner is not on the GPU engine yet (SURVEY §8f)");
+static void check_supported(const ccsc_problem& p, Geom* Gout) {
   if ((int64_t)p.K * p.views[0] * p.views[1] > 2048)
     throw Err(CCSC_E_UNSUPPORTED, "K * views > 2048 exceeds the gram kernel's RHS budget");
   if (p.precision != CCSC_FP64) throw Err(CCSC_E_UNSUPPORTED, "only CCSC_FP64 is built");
   if (p.K > 110) throw Err(CCSC_E_UNSUPPORTED, "K > 110 exceeds the gram kernel's tile budget");
   const int r = p.psf / 2;
-  Grid2D G{};
+  Geom g;
   std::string why;
-  if (!make_grid2d((int)(p.sb[0] + 2 * r), (int)(p.sb[1] + 2 * r), G, why))
+  if (!make_grid2d((int)(p.sb[0] + 2 * r), (int)(p.sb[1] + 2 * r), g.G, why))
     throw Err(CCSC_E_UNSUPPORTED, why);
-  if (Gout) *Gout = G;
+  if (p.variant == CCSC_L3D) {
+    g.Tn = (int)(p.sb[2] + 2 * r);
+    if (!make_gridt(g.Tn, g.G.Xh, g.Gt, why)) throw Err(CCSC_E_UNSUPPORTED, why);
+    if (g.F() > INT32_MAX / 2) throw Err(CCSC_E_UNSUPPORTED, "3D half spectrum too large");
+  }
+  if (Gout) *Gout = g;
 }
 
 static void shard(const ccsc_problem& p, int rank, int nranks, int64_t& b0, int64_t& nb) {
@@ -338,30 +378,35 @@ struct Plan2D {
   }
 };
 
-static Plan2D plan2d(const ccsc_problem& p, const Grid2D& G, int rank, int nranks) {
+static Plan2D plan2d(const ccsc_problem& p, const Geom& g, int rank, int nranks) {
   Plan2D m{};
   shard(p, rank, nranks, m.b0, m.nbl);
   m.np = m.nbl * p.ni;
-  const size_t P = (size_t)G.X * G.Y, F = G.F, K = p.K;
+  const Grid2D& G = g.G;
+  const size_t P = g.P(), F = g.F(), K = p.K;
   const size_t NV = (size_t)p.views[0] * p.views[1];
   const size_t Kp = K * (K + 1) / 2;
   const size_t s = p.psf;
-  const bool is4 = p.variant == CCSC_L4D;
+  const size_t SS = s * s * (g.Tn > 1 ? s : 1);   // filter support (2r+1)^ndim
+  const bool is4 = p.variant == CCSC_L4D, is3 = p.variant == CCSC_L3D;
   m.z = m.np * K * P * 8;
   m.yz = m.z;
-  m.cbuf = (p.tol > 0 && !is4) ? m.z : 0;   // 4D z-step needs no z_old copy (per-slice kernel)
+  // z_old copy of the fused 2D z-step (the 4D and 3D z-steps compare per slice/plane)
+  m.cbuf = (p.tol > 0 && !is4 && !is3) ? m.z : 0;
   m.D = m.nbl * K * NV * P * 8;
   m.yD = m.D;
   m.Bhat = m.np * NV * F * 16;
-  m.b = m.np * NV * (size_t)p.sb[0] * p.sb[1] * 8;
+  m.b = m.np * NV * (size_t)p.sb[0] * p.sb[1] * (is3 ? (size_t)p.sb[2] : 1) * 8;
   m.L = m.nbl * F * Kp * 16;
   m.h = m.nbl * F * NV * K * 16;
   m.Ch = m.nbl * K * NV * F * 16;
   m.Dh = m.Ch;
   m.Zh = (size_t)p.ni * K * F * 16;
-  m.E = is4 ? m.np * K * F * 16 : 0;
-  m.misc = (2 * K * NV * F) * 16 + F * 8 + (m.nbl + 2) * K * NV * s * s * 8 * 2 +
-           (4 * m.np * NV + 4 * K * NV + 64) * 8 + (size_t)G.ntw * 16;
+  // 4D: view correlations E; 3D: spectra of the z-step's plane/t transforms
+  m.E = (is4 || is3) ? m.np * K * F * 16 : 0;
+  m.misc = (2 * K * NV * F) * 16 + F * 8 + (m.nbl + 2) * K * NV * SS * 8 * 2 +
+           (4 * m.np * NV * g.Tn + 4 * K * NV * g.Tn + 64) * 8 + (size_t)(G.ntw + g.Gt.ntw) * 16 +
+           (is3 ? F * 16 + P * 8 : 0);
   return m;
 }
 
@@ -370,16 +415,20 @@ static const char* kKernelNames[5] = {"zstep", "gram_chol", "dsolve", "dual_r2c"
 // ---------------------------------------------------------------------------
 // Session: 2D consensus learners (dP / dZ)
 // ---------------------------------------------------------------------------
-// Session for the learners with 2D spatial convolution: dP, dZ and the 4D
-// light-field learner (NV = U*V views share the codes, L4:18-21).
+// Session of every consensus learner: dP, dZ, the 4D light-field learner (2D
+// spatial convolution, NV = U*V views share the codes, L4:18-21) and the 3D
+// learner (Tn > 1: plane transforms + t-direction FFT, L3).
 struct Session2D {
   ccsc_ctx* ctx;
   ccsc_problem p;
-  Grid2D G;
+  Geom g;
+  Grid2D G;     // plane grid (g.G)
   Plan2D m;
-  int r, s, K, ni, P, F, Kp;
+  int r, s, K, ni, P, F, Kp;   // P, F: voxels / half-spectrum bins per slice (all dims)
+  int SS;       // filter support size (2r+1)^ndim
+  int Tn;       // 3D: t extent of the padded grid (1 otherwise)
   int NV, KG;   // views, filter slices per block (K * NV)
-  bool is4;
+  bool is4, is3;
   int64_t N, nbl, b0, np;
   bool owner0;
   double theta;
@@ -387,6 +436,7 @@ struct Session2D {
 
   DevBuf tw, bdev, Bhat, z, yz, cbuf, D, yD, Usup, ssum, supp, Ch, Dh, L, h, Zh, dhat, dtmp, sden,
       dnorm, znorm, part, pair, E;
+  DevBuf twt, oacc, odz;   // 3D: t-FFT twiddles, objective scratch
 
   // host-side log
   int outer_done = 0;
@@ -453,11 +503,13 @@ struct Session2D {
   bool verbose_refresh_d() const {
     if (p.variant == CCSC_DPAR) return p.verbose == CCSC_VERBOSE_BRIEF;  // dP:126
     if (p.variant == CCSC_L4D) return p.verbose == CCSC_VERBOSE_ALL;     // L4:135
+    if (p.variant == CCSC_L3D) return p.verbose == CCSC_VERBOSE_ALL;     // L3:145
     return p.verbose != CCSC_VERBOSE_NONE;                               // dZ:127
   }
   bool verbose_refresh_z() const {
     if (p.variant == CCSC_DPAR) return p.verbose == CCSC_VERBOSE_BRIEF;  // dP:161
     if (p.variant == CCSC_L4D) return p.verbose == CCSC_VERBOSE_ALL;     // L4:170
+    if (p.variant == CCSC_L3D) return p.verbose == CCSC_VERBOSE_ALL;     // L3:185
     return p.verbose != CCSC_VERBOSE_NONE;                               // dZ:165
   }
 
@@ -465,18 +517,22 @@ struct Session2D {
             const double* z0)
       : ctx(c), p(pin), st(c->stream) {
     resolve_problem(p);
-    check_supported(p, &G);
-    m = plan2d(p, G, ctx->rank, ctx->nranks);
+    check_supported(p, &g);
+    G = g.G;
+    m = plan2d(p, g, ctx->rank, ctx->nranks);
     r = p.psf / 2;
     s = p.psf;
     K = p.K;
     ni = p.ni;
-    P = G.X * G.Y;
-    F = G.F;
+    Tn = g.Tn;
+    P = (int)g.P();
+    F = (int)g.F();
+    SS = s * s * (Tn > 1 ? s : 1);
     Kp = K * (K + 1) / 2;
     NV = p.views[0] * p.views[1];
     KG = K * NV;
     is4 = p.variant == CCSC_L4D;
+    is3 = p.variant == CCSC_L3D;
     N = p.n / ni;
     nbl = m.nbl;
     b0 = m.b0;
@@ -494,6 +550,13 @@ struct Session2D {
     auto tws = make_twiddles(G);
     tw.alloc(tws.size() * sizeof(cpx<double>));
     HIPCHK(hipMemcpy(tw.p, tws.data(), tw.bytes, hipMemcpyHostToDevice));
+    if (is3) {
+      auto twts = make_twiddles(g.Gt);
+      twt.alloc(twts.size() * sizeof(cpx<double>));
+      HIPCHK(hipMemcpy(twt.p, twts.data(), twt.bytes, hipMemcpyHostToDevice));
+      oacc.alloc((size_t)F * 16);
+      odz.alloc((size_t)P * 8);
+    }
     const size_t KP = (size_t)K * P;
     bdev.alloc(m.b);
     Bhat.alloc(m.Bhat);
@@ -502,9 +565,9 @@ struct Session2D {
     if (m.cbuf) cbuf.alloc(m.cbuf);
     D.alloc(m.D);
     yD.alloc(m.yD);
-    Usup.alloc((size_t)KG * s * s * 8);
-    ssum.alloc((size_t)KG * s * s * 8);
-    supp.alloc((size_t)nbl * KG * s * s * 8);
+    Usup.alloc((size_t)KG * SS * 8);
+    ssum.alloc((size_t)KG * SS * 8);
+    supp.alloc((size_t)nbl * KG * SS * 8);
     Ch.alloc(m.Ch);
     Dh.alloc(m.Dh);
     L.alloc(m.L);
@@ -513,25 +576,24 @@ struct Session2D {
     dhat.alloc((size_t)KG * F * 16);
     dtmp.alloc((size_t)KG * F * 16);
     sden.alloc((size_t)F * 8);
-    dnorm.alloc((size_t)2 * KG * 8);
-    znorm.alloc((size_t)2 * std::max<int64_t>(np * K, 1) * 8);
+    dnorm.alloc((size_t)2 * KG * Tn * 8);
+    znorm.alloc((size_t)2 * std::max<int64_t>(np * K * Tn, 1) * 8);
     part.alloc((size_t)2 * std::max<int64_t>(np * NV, 1) * 8);
     pair.alloc(4 * 8);
     if (m.E) E.alloc(m.E);
 
-    // data: b (rank-local, [sbx, sby, np] column-major) and its padded spectrum
-    const int sbx = (int)p.sb[0], sby = (int)p.sb[1];
+    // data: b (rank-local, [sbx, sby(, sbt), np] column-major) and its padded spectrum
     HIPCHK(hipMemcpy(bdev.p, b, m.b, hipMemcpyHostToDevice));
-    HIPCHK(launch_r2c_embed<double>(bdev.as<double>(), (int64_t)sbx * sby, sbx, sby, r, r,
-                                    Bhat.as<cpx<double>>(), F, np * NV, tw.as<cpx<double>>(), G,
-                                    st));
-    // filters: init.d or device RNG (dP:38-39; 4D: [psf,psf,U,V,K], L4:39-40)
+    fwd_embed(bdev.as<double>(), (int)p.sb[0], (int)p.sb[1], is3 ? (int)p.sb[2] : 1, r,
+              Bhat.as<cpx<double>>(), np * NV);
+    // filters: init.d or device RNG (dP:38-39; 4D: [psf,psf,U,V,K], L4:39-40; 3D: psf^3, L3:39-40)
     DevBuf d0dev;
-    const size_t nd0 = (size_t)s * s * KG;
+    const size_t nd0 = (size_t)SS * KG;
     d0dev.alloc(nd0 * 8);
     if (d0) HIPCHK(hipMemcpy(d0dev.p, d0, nd0 * 8, hipMemcpyHostToDevice));
     else HIPCHK(launch_randn<double>(d0dev.as<double>(), (int64_t)nd0, p.seed ^ 0xd0d0d0d0ULL, 0, st));
-    HIPCHK(launch_embed_filters<double>(d0dev.as<double>(), D.as<double>(), (int)nbl, KG, s, G, st));
+    HIPCHK(launch_embed_filters<double>(d0dev.as<double>(), D.as<double>(), (int)nbl, KG, s, G, Tn,
+                                        st));
     HIPCHK(hipMemsetAsync(yD.p, 0, m.yD, st));
     HIPCHK(hipMemsetAsync(Usup.p, 0, Usup.bytes, st));  // u = Pi(0) = 0 (Q2)
     HIPCHK(hipMemsetAsync(yz.p, 0, m.yz, st));
@@ -550,8 +612,7 @@ struct Session2D {
                                     (uint64_t)(b0 * ni) * KP, st));
     }
     // dhat = fft2(d) of the initial filters (all blocks share d0, dP:41-42)
-    HIPCHK(launch_r2c_embed<double>(D.as<double>(), P, G.X, G.Y, 0, 0, dhat.as<cpx<double>>(),
-                                    F, KG, tw.as<cpx<double>>(), G, st));
+    fwd_embed(D.as<double>(), G.X, G.Y, Tn, 0, dhat.as<cpx<double>>(), KG);
     HIPCHK(hipStreamSynchronize(st));
 
     v_obj_d.push_back(std::numeric_limits<double>::quiet_NaN());
@@ -590,8 +651,109 @@ struct Session2D {
     HIPCHK(hipStreamSynchronize(st));
   }
 
+  // ---- transforms ------------------------------------------------------------
+  // dst[count][F] = R2C of the zero-padded [sx, sy, st] sub-volumes of src placed at
+  // offset o in every dimension (o = r: padarray of b, dP:23 / L3:23; o = 0: full grid)
+  void fwd_embed(const double* src, int sx, int sy, int stt, int o, cpx<double>* dst,
+                 int64_t count) {
+    const auto* twc = tw.as<cpx<double>>();
+    if (!is3) {
+      HIPCHK(launch_r2c_embed<double>(src, (int64_t)sx * sy, sx, sy, o, o, dst, F, count, twc, G,
+                                      st));
+      return;
+    }
+    HIPCHK(launch_plane_fwd<double>(0, src, nullptr, nullptr, sx, sy, stt, o, 0.0, 1, 0, dst,
+                                    count, Tn, twc, G, st));
+    HIPCHK(launch_tfft<double>(dst, dst, count, G.Y, G.F, -1, twt.as<cpx<double>>(), g.Gt, st));
+  }
+  // D-step dual + R2C of (u - y) into Ch (dP:107-111)
+  void dual_fwd() {
+    const auto* twc = tw.as<cpx<double>>();
+    if (!is3) {
+      HIPCHK(launch_dual_r2c<double>(D.as<double>(), yD.as<double>(), Usup.as<double>(),
+                                     Ch.as<cpx<double>>(), nbl * KG, twc, G, KG, r, st));
+      return;
+    }
+    HIPCHK(launch_plane_fwd<double>(2, D.as<double>(), yD.as<double>(), Usup.as<double>(), 0, 0, 0,
+                                    0, 0.0, KG, r, Ch.as<cpx<double>>(), nbl * KG, Tn, twc, G, st));
+    HIPCHK(launch_tfft<double>(Ch.as<cpx<double>>(), Ch.as<cpx<double>>(), nbl * KG, G.Y, G.F, -1,
+                               twt.as<cpx<double>>(), g.Gt, st));
+  }
+  // C2R of Dh -> D, support of D + y, d-norms of block 1 (dP:112-121)
+  void inv_dout() {
+    const auto* twc = tw.as<cpx<double>>();
+    if (!is3) {
+      HIPCHK(launch_c2r_dout<double>(Dh.as<cpx<double>>(), D.as<double>(), yD.as<double>(),
+                                     supp.as<double>(), dnorm.as<double>(), owner0 ? KG : 0,
+                                     nbl * KG, twc, G, r, st));
+      return;
+    }
+    // Dh stays intact (block 1's spectrum feeds the z-step): t-inverse into Ch
+    HIPCHK(launch_tfft<double>(Dh.as<cpx<double>>(), Ch.as<cpx<double>>(), nbl * KG, G.Y, G.F, +1,
+                               twt.as<cpx<double>>(), g.Gt, st));
+    HIPCHK(launch_plane_inv<double>(2, Ch.as<cpx<double>>(), D.as<double>(), yD.as<double>(),
+                                    supp.as<double>(), dnorm.as<double>(), owner0 ? KG : 0,
+                                    1.0 / (double)P, r, nbl * KG, Tn, twc, G, st));
+  }
+  // one z-iteration over the local patches (dP:147-157; 4D L4:163-167; 3D L3:164-178)
+  void zstep_iter(bool tol_on) {
+    const auto* twc = tw.as<cpx<double>>();
+    if (is4) {
+      HIPCHK(launch_zstep_diag<double>(z.as<double>(), yz.as<double>(), E.as<cpx<double>>(),
+                                       sden.as<double>(), np * K, twc, G, theta, p.rho_z,
+                                       znorm.as<double>(), tol_on, st));
+    } else if (is3) {
+      cpx<double>* C = E.as<cpx<double>>();
+      const auto* twtc = twt.as<cpx<double>>();
+      HIPCHK(launch_plane_fwd<double>(1, z.as<double>(), yz.as<double>(), nullptr, 0, 0, 0, 0,
+                                      theta, 1, r, C, np * K, Tn, twc, G, st));
+      HIPCHK(launch_tfft<double>(C, C, np * K, G.Y, G.F, -1, twtc, g.Gt, st));
+      HIPCHK(launch_zsolve3<double>(C, Bhat.as<cpx<double>>(), dhat.as<cpx<double>>(),
+                                    sden.as<double>(), F, np, K, 1.0 / (double)P, st));
+      HIPCHK(launch_tfft<double>(C, C, np * K, G.Y, G.F, +1, twtc, g.Gt, st));
+      HIPCHK(launch_plane_inv<double>(1, C, z.as<double>(), nullptr, nullptr,
+                                      tol_on ? znorm.as<double>() : nullptr, 0, 1.0, r, np * K,
+                                      Tn, twc, G, st));
+    } else {
+      HIPCHK(launch_zstep<double>(z.as<double>(), yz.as<double>(), cbuf.as<double>(),
+                                  Bhat.as<cpx<double>>(), dhat.as<cpx<double>>(),
+                                  sden.as<double>(), np, twc, G, K, theta, znorm.as<double>(),
+                                  tol_on, st));
+    }
+  }
+
+  // 3D objective (L3:342-355), patch by patch through the z-step's spectrum buffer
+  void objective3_parts(const cpx<double>* dsp, double* DZdev) {
+    const auto* twc = tw.as<cpx<double>>();
+    const auto* twtc = twt.as<cpx<double>>();
+    cpx<double>* C = E.as<cpx<double>>();
+    const int sbx = (int)p.sb[0], sby = (int)p.sb[1], sbt = (int)p.sb[2];
+    HIPCHK(hipMemsetAsync(pair.p, 0, 2 * sizeof(double), st));
+    for (int64_t q = 0; q < np; ++q) {
+      const double* zq = z.as<double>() + (size_t)q * K * P;
+      double* dzq = DZdev ? DZdev + (size_t)q * P : odz.as<double>();
+      HIPCHK(launch_plane_fwd<double>(0, zq, nullptr, nullptr, G.X, G.Y, Tn, 0, 0.0, 1, 0, C, K,
+                                      Tn, twc, G, st));
+      HIPCHK(launch_tfft<double>(C, C, K, G.Y, G.F, -1, twtc, g.Gt, st));
+      HIPCHK(launch_corr_sum<double>(C, dsp, oacc.as<cpx<double>>(), F, K, st));
+      HIPCHK(launch_tfft<double>(oacc.as<cpx<double>>(), oacc.as<cpx<double>>(), 1, G.Y, G.F, +1,
+                                 twtc, g.Gt, st));
+      HIPCHK(launch_plane_inv<double>(0, oacc.as<cpx<double>>(), dzq, nullptr, nullptr, nullptr, 0,
+                                      1.0 / (double)P, r, 1, Tn, twc, G, st));
+      HIPCHK(launch_crop_sq<double>(dzq, bdev.as<double>() + (size_t)q * sbx * sby * sbt, sbx, sby,
+                                    sbt, r, G.X, G.Y, zq, (int64_t)K * P, pair.as<double>(), st));
+    }
+  }
+
   // objective with filter spectrum `dsp` (valid on every rank); DZ optional.
   double objective(const cpx<double>* dsp, double* DZdev) {
+    if (is3) {
+      objective3_parts(dsp, DZdev);
+      allreduce(pair.as<double>(), 2);
+      double h2[2];
+      pair_to_host(h2);
+      return p.lambda_residual * 0.5 * h2[0] + p.lambda_prior * h2[1];
+    }
     HIPCHK(launch_objective<double>(z.as<double>(), dsp, bdev.as<double>(), (int)p.sb[0],
                                     (int)p.sb[1], r, DZdev, part.as<double>(), np,
                                     tw.as<cpx<double>>(), G, K, NV, st));
@@ -612,7 +774,6 @@ struct Session2D {
   // ---- one outer iteration --------------------------------------------------
   void outer_iteration() {
     const int it = outer_done;
-    const auto* twc = tw.as<cpx<double>>();
     hipEvent_t e0 = get_event(), e1 = get_event();
     double obj_ms = 0;
     auto objective_timed = [&](const cpx<double>* dsp) {
@@ -632,8 +793,8 @@ struct Session2D {
 
     // ---- D precompute (dP:95-99) ----
     for (int64_t jl = 0; jl < nbl; ++jl) {
-      HIPCHK(launch_r2c_embed<double>(z.as<double>() + (size_t)jl * ni * K * P, P, G.X, G.Y, 0, 0,
-                                      Zh.as<cpx<double>>(), F, (int64_t)ni * K, twc, G, st));
+      fwd_embed(z.as<double>() + (size_t)jl * ni * K * P, G.X, G.Y, Tn, 0, Zh.as<cpx<double>>(),
+                (int64_t)ni * K);
       timed(1, [&] {
         HIPCHK(launch_gram_chol<double>(Zh.as<cpx<double>>(),
                                         Bhat.as<cpx<double>>() + (size_t)jl * ni * NV * F,
@@ -647,30 +808,25 @@ struct Session2D {
     const bool want_od = verbose_refresh_d() || p.trace_objective;
     int nd = 0;
     for (int id = 0; id < p.max_it_d; ++id) {
-      timed(3, [&] {
-        HIPCHK(launch_dual_r2c<double>(D.as<double>(), yD.as<double>(), Usup.as<double>(),
-                                       Ch.as<cpx<double>>(), nbl * KG, twc, G, KG, r, st));
-      });
+      timed(3, [&] { dual_fwd(); });
       timed(2, [&] {
         HIPCHK(launch_dsolve<double>(L.as<cpx<double>>(), h.as<cpx<double>>(),
                                      Ch.as<cpx<double>>(), Dh.as<cpx<double>>(), (int)nbl, F, K,
                                      p.rho_d, NV, st));
       });
-      timed(4, [&] {
-        HIPCHK(launch_c2r_dout<double>(Dh.as<cpx<double>>(), D.as<double>(), yD.as<double>(),
-                                       supp.as<double>(), dnorm.as<double>(),
-                                       owner0 ? KG : 0, nbl * KG, twc, G, r, st));
-      });
-      HIPCHK(launch_supp_reduce<double>(supp.as<double>(), ssum.as<double>(), (int)nbl,
-                                        KG * s * s, st));
-      allreduce(ssum.as<double>(), (size_t)KG * s * s);
-      // Pi normalises per filter (2D, dP:212-213) / per (u,v,k) slice (4D, L4:224-225)
-      HIPCHK(launch_project<double>(ssum.as<double>(), Usup.as<double>(), KG, s * s,
+      timed(4, [&] { inv_dout(); });
+      HIPCHK(launch_supp_reduce<double>(supp.as<double>(), ssum.as<double>(), (int)nbl, KG * SS,
+                                        st));
+      allreduce(ssum.as<double>(), (size_t)KG * SS);
+      // Pi normalises per filter (2D, dP:212-213; 3D, L3:245-252) / per (u,v,k) slice
+      // (4D, L4:224-225)
+      HIPCHK(launch_project<double>(ssum.as<double>(), Usup.as<double>(), KG, SS,
                                     1.0 / (double)N, st));
       ++nd;
       double dd = std::numeric_limits<double>::quiet_NaN();
       if (tol_on) {
-        if (owner0) HIPCHK(launch_sum_pairs<double>(dnorm.as<double>(), KG, pair.as<double>(), st));
+        if (owner0)
+          HIPCHK(launch_sum_pairs<double>(dnorm.as<double>(), KG * Tn, pair.as<double>(), st));
         else HIPCHK(hipMemsetAsync(pair.p, 0, 2 * sizeof(double), st));
         allreduce(pair.as<double>(), 2);
         double h2[2];
@@ -699,21 +855,12 @@ struct Session2D {
     const bool want_oz = verbose_refresh_z() || p.trace_objective;
     int nz = 0;
     for (int iz = 0; iz < p.max_it_z; ++iz) {
-      timed(0, [&] {
-        if (is4)
-          HIPCHK(launch_zstep_diag<double>(z.as<double>(), yz.as<double>(), E.as<cpx<double>>(),
-                                           sden.as<double>(), np * K, twc, G, theta, p.rho_z,
-                                           znorm.as<double>(), tol_on, st));
-        else
-          HIPCHK(launch_zstep<double>(z.as<double>(), yz.as<double>(), cbuf.as<double>(),
-                                      Bhat.as<cpx<double>>(), dhat.as<cpx<double>>(),
-                                      sden.as<double>(), np, twc, G, K, theta,
-                                      znorm.as<double>(), tol_on, st));
-      });
+      timed(0, [&] { zstep_iter(tol_on); });
       ++nz;
       double zd = std::numeric_limits<double>::quiet_NaN();
       if (tol_on) {
-        HIPCHK(launch_sum_pairs<double>(znorm.as<double>(), (int)(is4 ? np * K : np),
+        HIPCHK(launch_sum_pairs<double>(znorm.as<double>(),
+                                        (int)(is4 ? np * K : is3 ? np * K * Tn : np),
                                         pair.as<double>(), st));
         allreduce(pair.as<double>(), 2);
         double h2[2];
@@ -772,13 +919,18 @@ struct Session2D {
       bcast0(tmp.as<double>(), (size_t)KG * P);
       HIPCHK(hipMemcpyAsync(D1.data(), tmp.p, tmp.bytes, hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));
-      // d_res = circshift(D1, +r)(1:psf, 1:psf, :)   (dP:195-196; 4D L4:208-209: per view)
+      // d_res = circshift(D1, +r)(1:psf, 1:psf(, 1:psf), :)  (dP:195-196; 4D L4:208-209:
+      // per view; 3D L3:226-227)
+      const int st3 = Tn > 1 ? s : 1;
       for (int k = 0; k < KG; ++k)
-        for (int j = 0; j < s; ++j)
-          for (int i = 0; i < s; ++i) {
-            const int x = (i - r + G.X) % G.X, y = (j - r + G.Y) % G.Y;
-            out->d_res[i + (size_t)s * (j + (size_t)s * k)] = D1[(size_t)k * P + (size_t)y * G.X + x];
-          }
+        for (int l = 0; l < st3; ++l)
+          for (int j = 0; j < s; ++j)
+            for (int i = 0; i < s; ++i) {
+              const int x = (i - r + G.X) % G.X, y = (j - r + G.Y) % G.Y;
+              const int t = Tn > 1 ? (l - r + Tn) % Tn : 0;
+              out->d_res[i + (size_t)s * (j + (size_t)s * (l + (size_t)st3 * k))] =
+                  D1[(size_t)k * P + ((size_t)t * G.Y + y) * G.X + x];
+            }
     }
     if (out->z_res) {
       HIPCHK(hipMemcpy(out->z_res, z.p, m.z, hipMemcpyDeviceToHost));
@@ -884,9 +1036,9 @@ int32_t ccsc_plan_bytes(const ccsc_problem* p, int32_t rank, int32_t nranks, uin
     if (!p || !bytes) throw Err(CCSC_E_INVALID, "NULL argument");
     ccsc_problem q = *p;
     resolve_problem(q);
-    Grid2D G{};
-    check_supported(q, &G);
-    *bytes = plan2d(q, G, rank, nranks).total();
+    Geom g;
+    check_supported(q, &g);
+    *bytes = plan2d(q, g, rank, nranks).total();
   });
 }
 

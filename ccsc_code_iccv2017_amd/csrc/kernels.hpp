@@ -64,14 +64,38 @@ template <typename T>
 hipError_t launch_dsolve(const cpx<T>* L, const cpx<T>* h, const cpx<T>* Ch, cpx<T>* Dh,
                          int nblocks, int F, int K, T rho, int NV, hipStream_t st);
 
+// ---- kernels3d.hip: the 3D learner's factored transforms -------------------
+// Spectra [slice][t][F2]; P2 = X*Y plane voxels.  Modes: see kernels3d.hip.
+size_t tfft_smem_bytes(const Grid2D& Gt, size_t tsize);
+template <typename T>
+hipError_t launch_plane_fwd(int mode, const T* a, T* b, const T* usup, int sx, int sy, int st,
+                            int o, T theta, int KG, int r, cpx<T>* dst, int64_t nslices, int Tn,
+                            const cpx<T>* tw, const Grid2D& G, hipStream_t stream);
+template <typename T>
+hipError_t launch_tfft(const cpx<T>* src, cpx<T>* dst, int64_t nslices, int Yn, int F2, int sign,
+                       const cpx<T>* tw, const Grid2D& Gt, hipStream_t stream);
+template <typename T>
+hipError_t launch_plane_inv(int mode, const cpx<T>* src, T* dst, const T* yv, T* supp, T* norms,
+                            int64_t nfirst, T scale, int r, int64_t nslices, int Tn,
+                            const cpx<T>* tw, const Grid2D& G, hipStream_t stream);
+template <typename T>
+hipError_t launch_zsolve3(cpx<T>* C, const cpx<T>* Bhat, const cpx<T>* dhat, const T* sden,
+                          int64_t F3, int64_t npatch, int K, T invP3, hipStream_t stream);
+template <typename T>
+hipError_t launch_corr_sum(const cpx<T>* Zh, const cpx<T>* dhat, cpx<T>* out, int64_t F3, int K,
+                           hipStream_t stream);
+template <typename T>
+hipError_t launch_crop_sq(const T* Dz, const T* b, int sx, int sy, int st, int r, int X, int Y,
+                          const T* z, int64_t zcount, T* part, hipStream_t stream);
+
 // ---- util.hip ---------------------------------------------------------------
 template <typename T>
 hipError_t launch_randn(T* out, int64_t count, uint64_t seed, uint64_t offset, hipStream_t st);
-// Embed [psf,psf,K] filters (column-major) into nrep copies of the [K][Y][X] grid
-// at circshift(-r) positions (dP:38-39).
+// Embed [psf,psf,K] (Tn == 1) or [psf,psf,psf,K] filters (column-major) into nrep
+// copies of the [K][Tn][Y][X] grid at circshift(-r) positions (dP:38-39, L3:39-40).
 template <typename T>
 hipError_t launch_embed_filters(const T* d0, T* D, int nrep, int K, int psf, const Grid2D& G,
-                                hipStream_t st);
+                                int Tn, hipStream_t st);
 template <typename T>
 hipError_t launch_replicate(const T* src, T* dst, int64_t n, int nrep, hipStream_t st);
 

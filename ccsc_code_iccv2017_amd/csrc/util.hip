@@ -44,27 +44,28 @@ hipError_t launch_randn(T* out, int64_t count, uint64_t seed, uint64_t offset, h
 // D[rep][k][y][x] = d0(i, j, k) at x = (i - r) mod X, y = (j - r) mod Y; zero elsewhere.
 template <typename T>
 __global__ void k_embed(const T* __restrict__ d0, T* __restrict__ D, int nrep, int K, int psf,
-                        int X, int Y) {
-  const int64_t P = (int64_t)X * Y;
+                        int X, int Y, int Tn) {
+  const int64_t P = (int64_t)X * Y * Tn;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t total = (int64_t)nrep * K * P;
   if (i >= total) return;
   const int64_t e = i % P;
   const int k = (int)((i / P) % K);
-  const int x = (int)(e % X), y = (int)(e / X);
+  const int x = (int)(e % X), y = (int)((e / X) % Y), t = (int)(e / ((int64_t)X * Y));
   const int r = psf / 2;
-  const int ii = (x + r) % X, jj = (y + r) % Y;
+  const int ii = (x + r) % X, jj = (y + r) % Y, tt = (Tn == 1) ? 0 : (t + r) % Tn;
+  const int pt = (Tn == 1) ? 1 : psf;  // 3D filters are psf^3 (L3:39-40)
   T v = (T)0;
-  if (ii < psf && jj < psf) v = d0[ii + psf * (jj + psf * k)];
+  if (ii < psf && jj < psf && tt < pt) v = d0[ii + psf * (jj + psf * (tt + pt * (int64_t)k))];
   D[i] = v;
 }
 
 template <typename T>
 hipError_t launch_embed_filters(const T* d0, T* D, int nrep, int K, int psf, const Grid2D& G,
-                                hipStream_t st) {
-  const int64_t total = (int64_t)nrep * K * G.X * G.Y;
+                                int Tn, hipStream_t st) {
+  const int64_t total = (int64_t)nrep * K * G.X * G.Y * Tn;
   hipLaunchKernelGGL(k_embed<T>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, d0, D,
-                     nrep, K, psf, G.X, G.Y);
+                     nrep, K, psf, G.X, G.Y, Tn);
   return hipGetLastError();
 }
 
@@ -80,7 +81,7 @@ hipError_t launch_replicate(const T* src, T* dst, int64_t n, int nrep, hipStream
 
 template hipError_t launch_randn<double>(double*, int64_t, uint64_t, uint64_t, hipStream_t);
 template hipError_t launch_embed_filters<double>(const double*, double*, int, int, int,
-                                                 const Grid2D&, hipStream_t);
+                                                 const Grid2D&, int, hipStream_t);
 template hipError_t launch_replicate<double>(const double*, double*, int64_t, int, hipStream_t);
 
 }  // namespace ccsc

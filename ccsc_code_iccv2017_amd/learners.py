@@ -101,7 +101,7 @@ def make_problem(variant, b_shape, kernel_size, lambda_residual, lambda_prior, m
     if variant == L.CCSC_L3D:
         p.sb[2] = int(b_shape[2])
     p.views[0] = p.views[1] = 1
-    if variant == L.CCSC_L4D:                  # b: [x, y, U, V, n]; kernel [s, s, U, V, K]
+    if variant == L.CCSC_L4D and len(kernel_size) == 5:   # b: [x, y, U, V, n]; kernel [s, s, U, V, K]
         p.views[0], p.views[1] = int(kernel_size[2]), int(kernel_size[3])
     p.n = int(b_shape[-1])
     p.K = int(kernel_size[-1])
@@ -197,11 +197,24 @@ class Session:
 
     def grid(self):
         r = self.p.psf // 2
-        return self.p.sb[0] + 2 * r, self.p.sb[1] + 2 * r
+        g = (self.p.sb[0] + 2 * r, self.p.sb[1] + 2 * r)
+        if self.p.variant == L.CCSC_L3D:
+            g += (self.p.sb[2] + 2 * r,)
+        return g
 
     def results(self, want_z=True, want_DZ=True, want_obj=False):
-        X, Y = self.grid()
         p = self.p
+        if p.variant == L.CCSC_L3D:
+            X, Y, T = self.grid()
+            d_res = np.zeros((p.psf, p.psf, p.psf, p.K), order="F")
+            z_res = np.zeros((X, Y, T, p.K, self.n_local), order="F") if want_z else None
+            DZ = np.zeros((X, Y, T, self.n_local), order="F") if want_DZ else None
+            obj = np.zeros(1) if want_obj else None
+            out = L.Outputs(L.dptr(d_res), L.dptr(z_res), L.dptr(DZ), L.dptr(obj))
+            eb = L.errbuf()
+            L.check(L.lib().ccsc_session_results(self.ptr, C.byref(out), eb, len(eb)), eb)
+            return d_res, z_res, DZ, (float(obj[0]) if want_obj else None)
+        X, Y = self.grid()
         if p.variant == L.CCSC_L4D:
             U, V = p.views[0], p.views[1]
             d_res = np.zeros((p.psf, p.psf, U, V, p.K), order="F")
@@ -350,6 +363,46 @@ def admm_learn_conv4D_lightfield(b, kernel_size, lambda_residual, lambda_prior, 
                   "trace": log["trace"], "engine_tim_vals": log["tim_vals"]}
     if z_res is not None:
         z_res = z_res.astype(np.complex128)
+    return d_res, z_res, DZ, obj, iterations
+
+
+def admm_learn_conv3D_large(b, kernel_size, lambda_residual, lambda_prior, max_it, tol, verbose,
+                            init=None, ctx=None, device=0, want_z=True, want_DZ=True, **kw):
+    """Drop-in for 3D/admm_learn_conv3D_large.m:1-230 (function admm_learn_convND_large).
+
+    b: [x, y, t, n]; kernel_size = [psf, psf, psf, K].  Returns (d_res [psf,psf,psf,K],
+    z_res [X,Y,T,K,n], DZ [X,Y,T,n] (uncropped, L3:218-224), obj_val, iterations) --
+    iterations carries the reference's empty fields (L3:72-75) plus the engine's 'trace'.
+    """
+    b = np.asarray(b, dtype=np.float64)
+    if b.ndim == 3:
+        b = b[..., None]
+    if b.ndim != 4:
+        raise ValueError("b must be [x, y, t, n]")
+    own = ctx is None
+    if own:
+        ctx = Context(device)
+    try:
+        p = make_problem(L.CCSC_L3D, b.shape, kernel_size, lambda_residual, lambda_prior,
+                         max_it, tol, verbose, **kw)
+        d0 = z0 = None
+        if init is not None and len(init) > 0:
+            d0 = init.get("d")
+            z0 = init.get("z")
+        s = Session(ctx, p, b, d0, z0)
+        try:
+            done = False
+            while s.outer < s.p.max_it and not done:
+                done = s.step(1)
+            d_res, z_res, DZ, obj = s.results(want_z=want_z, want_DZ=want_DZ, want_obj=True)
+            log = s.iterlog()
+        finally:
+            s.close()
+    finally:
+        if own:
+            ctx.close()
+    iterations = {"obj_vals_d": [], "obj_vals_z": [], "tim_vals": [], "it_vals": [],
+                  "trace": log["trace"], "engine_tim_vals": log["tim_vals"]}
     return d_res, z_res, DZ, obj, iterations
 
 

@@ -109,3 +109,17 @@ def test_memory_plan_fits_one_mi355x(L):
     assert plan_bytes(p, 0, 8) < one / 7
     p.tol = 1e-3                       # tol > 0 adds a z-sized buffer (z_old)
     assert plan_bytes(p, 0, 1) > one
+
+
+def test_3d_and_4d_configs_supported_and_fit(L):
+    """C4 (3D, 64x64x32 patches, 11^3 x 49 filters -> 74x74x42 grid) and C5 (4D) run on the
+    engine (ccsc_supported == OK) and their device plans fit one 288 GB MI355X."""
+    from ccsc_code_iccv2017_amd.learners import plan_bytes
+    eb = L.errbuf()
+    p3 = _problem(L, 2, sb=(64, 64, 32), n=64, K=49)
+    assert L.lib().ccsc_supported(C.byref(p3), eb, len(eb)) == 0, eb.value
+    assert plan_bytes(p3, 0, 1) < 288e9 * 0.9
+    p4 = _problem(L, 3, n=64, K=49)
+    p4.views[0] = p4.views[1] = 5
+    assert L.lib().ccsc_supported(C.byref(p4), eb, len(eb)) == 0, eb.value
+    assert plan_bytes(p4, 0, 1) < 288e9 * 0.9
