@@ -372,9 +372,9 @@ namespace ccsc {
 // memory plan shared by ccsc_plan_bytes and the session
 struct Plan2D {
   int64_t np, nbl, b0;
-  size_t z, yz, cbuf, D, yD, Bhat, b, L, h, Ch, Dh, Zh, E, misc;
+  size_t z, yz, cbuf, W, dhw, D, yD, Bhat, b, L, h, Ch, Dh, Zh, E, misc;
   size_t total() const {
-    return z + yz + cbuf + D + yD + Bhat + b + L + h + Ch + Dh + Zh + E + misc;
+    return z + yz + cbuf + W + dhw + D + yD + Bhat + b + L + h + Ch + Dh + Zh + E + misc;
   }
 };
 
@@ -391,8 +391,12 @@ static Plan2D plan2d(const ccsc_problem& p, const Geom& g, int rank, int nranks)
   const bool is4 = p.variant == CCSC_L4D, is3 = p.variant == CCSC_L3D;
   m.z = m.np * K * P * 8;
   m.yz = m.z;
-  // z_old copy of the fused 2D z-step (the 4D and 3D z-steps compare per slice/plane)
+  // 2D split z-state (zsplit.hip): w per patch + the filter spectrum it was
+  // solved with; with tol > 0 a u buffer so z_old survives for the tol test
+  // (the 4D and 3D z-steps compare per slice/plane)
   m.cbuf = (p.tol > 0 && !is4 && !is3) ? m.z : 0;
+  m.W = (!is4 && !is3) ? m.np * F * 16 : 0;
+  m.dhw = (!is4 && !is3) ? K * F * 16 : 0;
   m.D = m.nbl * K * NV * P * 8;
   m.yD = m.D;
   m.Bhat = m.np * NV * F * 16;
@@ -436,6 +440,12 @@ struct Session2D {
 
   DevBuf tw, bdev, Bhat, z, yz, cbuf, D, yD, Usup, ssum, supp, Ch, Dh, L, h, Zh, dhat, dtmp, sden,
       dnorm, znorm, part, pair, E;
+  // 2D z-phase state (zsplit.hip): zmode 0 = z materialised in `z`; zmode 1 =
+  // split, `z` holds u, W the last w and `dw` the filter spectrum w was solved
+  // with (dhat, or dhatw after the next z-prep replaced dhat).
+  DevBuf W, dhatw;
+  int zmode = 0;
+  const cpx<double>* dw = nullptr;
   DevBuf twt, oacc, odz;   // 3D: t-FFT twiddles, objective scratch
 
   // host-side log
@@ -563,6 +573,8 @@ struct Session2D {
     z.alloc(m.z);
     yz.alloc(m.yz);
     if (m.cbuf) cbuf.alloc(m.cbuf);
+    if (m.W) W.alloc(m.W);
+    if (m.dhw) dhatw.alloc(m.dhw);
     D.alloc(m.D);
     yD.alloc(m.yD);
     Usup.alloc((size_t)KG * SS * 8);
@@ -714,12 +726,34 @@ struct Session2D {
       HIPCHK(launch_plane_inv<double>(1, C, z.as<double>(), nullptr, nullptr,
                                       tol_on ? znorm.as<double>() : nullptr, 0, 1.0, r, np * K,
                                       Tn, twc, G, st));
+    } else if (!tol_on) {
+      // one pass per patch over the split state (zsplit.hip)
+      HIPCHK(launch_zsplit<double>(z.as<double>(), z.as<double>(), yz.as<double>(),
+                                   W.as<cpx<double>>(), Bhat.as<cpx<double>>(), dw,
+                                   dhat.as<cpx<double>>(), sden.as<double>(), np, twc, G, K,
+                                   theta, zmode, st));
+      zmode = 1;
+      dw = dhat.as<cpx<double>>();
     } else {
-      HIPCHK(launch_zstep<double>(z.as<double>(), yz.as<double>(), cbuf.as<double>(),
-                                  Bhat.as<cpx<double>>(), dhat.as<cpx<double>>(),
-                                  sden.as<double>(), np, twc, G, K, theta, znorm.as<double>(),
-                                  tol_on, st));
+      // tol test (dP:156-157): u into cbuf so z_old stays in z, then z = u - y +
+      // ifft2(conj(d) w) with the per-slice change norms
+      HIPCHK(launch_zsplit<double>(z.as<double>(), cbuf.as<double>(), yz.as<double>(),
+                                   W.as<cpx<double>>(), Bhat.as<cpx<double>>(), dw,
+                                   dhat.as<cpx<double>>(), sden.as<double>(), np, twc, G, K,
+                                   theta, zmode, st));
+      HIPCHK(launch_zmat<double>(cbuf.as<double>(), yz.as<double>(), W.as<cpx<double>>(),
+                                 dhat.as<cpx<double>>(), z.as<double>(), z.as<double>(),
+                                 znorm.as<double>(), np, twc, G, K, st));
+      zmode = 0;
     }
+  }
+  // split z-state -> z materialised in place (objective, outputs)
+  void materialize_z() {
+    if (zmode == 0) return;
+    HIPCHK(launch_zmat<double>(z.as<double>(), yz.as<double>(), W.as<cpx<double>>(), dw,
+                               z.as<double>(), nullptr, nullptr, np, tw.as<cpx<double>>(), G, K,
+                               st));
+    zmode = 0;
   }
 
   // 3D objective (L3:342-355), patch by patch through the z-step's spectrum buffer
@@ -745,6 +779,7 @@ struct Session2D {
     }
   }
 
+
   // objective with filter spectrum `dsp` (valid on every rank); DZ optional.
   double objective(const cpx<double>* dsp, double* DZdev) {
     if (is3) {
@@ -754,6 +789,7 @@ struct Session2D {
       pair_to_host(h2);
       return p.lambda_residual * 0.5 * h2[0] + p.lambda_prior * h2[1];
     }
+    materialize_z();
     HIPCHK(launch_objective<double>(z.as<double>(), dsp, bdev.as<double>(), (int)p.sb[0],
                                     (int)p.sb[1], r, DZdev, part.as<double>(), np,
                                     tw.as<cpx<double>>(), G, K, NV, st));
@@ -793,8 +829,15 @@ struct Session2D {
 
     // ---- D precompute (dP:95-99) ----
     for (int64_t jl = 0; jl < nbl; ++jl) {
-      fwd_embed(z.as<double>() + (size_t)jl * ni * K * P, G.X, G.Y, Tn, 0, Zh.as<cpx<double>>(),
-                (int64_t)ni * K);
+      if (zmode)  // fft2(z) of the split state: fft2(u - y) + XY conj(dw) w
+        HIPCHK(launch_zhat_split<double>(z.as<double>() + (size_t)jl * ni * K * P,
+                                         yz.as<double>() + (size_t)jl * ni * K * P,
+                                         W.as<cpx<double>>() + (size_t)jl * ni * F, dw,
+                                         Zh.as<cpx<double>>(), ni, tw.as<cpx<double>>(), G, K,
+                                         st));
+      else
+        fwd_embed(z.as<double>() + (size_t)jl * ni * K * P, G.X, G.Y, Tn, 0,
+                  Zh.as<cpx<double>>(), (int64_t)ni * K);
       timed(1, [&] {
         HIPCHK(launch_gram_chol<double>(Zh.as<cpx<double>>(),
                                         Bhat.as<cpx<double>>() + (size_t)jl * ni * NV * F,
@@ -843,6 +886,10 @@ struct Session2D {
       if (tol_on && dd < p.tol) break;  // dP:130-132
     }
     // ---- Z precompute (dP:143-144): d = Dhat of block 1 ----
+    if (zmode && dw == dhat.as<cpx<double>>()) {  // keep the spectrum w was solved with
+      std::swap(dhat.p, dhatw.p);
+      dw = dhatw.as<cpx<double>>();
+    }
     if (owner0) HIPCHK(hipMemcpyAsync(dhat.p, Dh.p, (size_t)KG * F * 16, hipMemcpyDeviceToDevice, st));
     bcast0(dhat.as<double>(), (size_t)2 * KG * F);
     // s(f) = sum over filters (and views, L4:277,330) of |dhat|^2
@@ -859,8 +906,7 @@ struct Session2D {
       ++nz;
       double zd = std::numeric_limits<double>::quiet_NaN();
       if (tol_on) {
-        HIPCHK(launch_sum_pairs<double>(znorm.as<double>(),
-                                        (int)(is4 ? np * K : is3 ? np * K * Tn : np),
+        HIPCHK(launch_sum_pairs<double>(znorm.as<double>(), (int)(np * K * Tn),
                                         pair.as<double>(), st));
         allreduce(pair.as<double>(), 2);
         double h2[2];
@@ -933,6 +979,7 @@ struct Session2D {
             }
     }
     if (out->z_res) {
+      materialize_z();
       HIPCHK(hipMemcpy(out->z_res, z.p, m.z, hipMemcpyDeviceToHost));
     }
     if (out->DZ) {
@@ -974,10 +1021,9 @@ struct Session2D {
   double alg_bytes(int id) const {
     const double Pd = P, Fd = F, Kd = K;
     switch (id) {
-      case 0:  // z-iteration compulsory state traffic: read z,y + write z,y (fp64), B per patch
-        if (is4)  // + E per slice
-          return (double)np * Kd * (4.0 * 8.0 * Pd + 16.0 * Fd) + Fd * 8.0;
-        return (double)np * Kd * 4.0 * 8.0 * Pd + (double)np * 16.0 * Fd + Kd * Fd * 16.0;
+      case 0:  // z-iteration, SURVEY.md §8(d): n K (4 s P + 4 c F) + n c F V  (s = 8, c = 16):
+               // prox+dual+R2C, solve, C2R stages each reading/writing their operands once
+        return (double)np * Kd * (4.0 * 8.0 * Pd + 4.0 * 16.0 * Fd) + (double)np * NV * 16.0 * Fd;
       case 1:  // gram+chol per block: read A (ni x K x F) + b, write L, h
         return (double)ni * Kd * Fd * 16.0 + ni * Fd * 16.0 + Fd * Kp * 16.0 + Fd * Kd * 16.0;
       case 2:  // dsolve over local blocks: read L, h, C; write Dhat

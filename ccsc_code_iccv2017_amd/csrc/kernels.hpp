@@ -34,10 +34,6 @@ template <typename T>
 hipError_t launch_sden(const cpx<T>* dhat, T* sden, int F, int K, T rho, T invP,
                        hipStream_t st);
 template <typename T>
-hipError_t launch_zstep(T* z, T* yz, T* cbuf, const cpx<T>* Bhat, const cpx<T>* dhat,
-                        const T* sden, int64_t npatch, const cpx<T>* tw, const Grid2D& G, int K,
-                        T theta, T* znorm, bool tol, hipStream_t st);
-template <typename T>
 hipError_t launch_objective(const T* z, const cpx<T>* dhat, const T* b, int sbx, int sby, int r,
                             T* DZ, T* part, int64_t npatch, const cpx<T>* tw, const Grid2D& G,
                             int K, int NV, hipStream_t st);
@@ -50,6 +46,23 @@ hipError_t launch_view_corr(const cpx<T>* dhat, const cpx<T>* Bhat, cpx<T>* E, i
                             int F, int K, int NV, hipStream_t st);
 template <typename T>
 hipError_t launch_sum_pairs(const T* part, int count, T* out, hipStream_t st);
+
+// ---- zsplit.hip: the 2D learners' z-iteration on the split state ----------
+// (u, y) per slice + w per patch, z = u - y + ifft2(conj(dcorr) w); see zsplit.hip.
+size_t zsplit_smem_bytes(const Grid2D& G);
+template <typename T>
+hipError_t launch_zsplit(const T* U, T* Uo, T* Yz, cpx<T>* W, const cpx<T>* Bhat,
+                         const cpx<T>* dcorr, const cpx<T>* dhat, const T* sden, int64_t npatch,
+                         const cpx<T>* tw, const Grid2D& G, int K, T theta, int mode,
+                         hipStream_t st);
+template <typename T>
+hipError_t launch_zmat(const T* Us, const T* Yz, const cpx<T>* W, const cpx<T>* dcorr, T* Zd,
+                       const T* zold, T* znorm, int64_t npatch, const cpx<T>* tw, const Grid2D& G,
+                       int K, hipStream_t st);
+template <typename T>
+hipError_t launch_zhat_split(const T* U, const T* Yz, const cpx<T>* W, const cpx<T>* dcorr,
+                             cpx<T>* dst, int64_t npatch, const cpx<T>* tw, const Grid2D& G,
+                             int K, hipStream_t st);
 
 // ---- dstep.hip ------------------------------------------------------------
 // Per frequency f of one block: G = A^H A + rho I (A = ni x K code spectra),

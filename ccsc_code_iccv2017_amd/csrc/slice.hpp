@@ -23,10 +23,10 @@ __device__ __forceinline__ Smem<T> carve(char* smem, const Grid2D& G) {
   return s;
 }
 
-template <typename T>
+template <typename T, int NT = kNT>
 __device__ __forceinline__ void load_twiddles(cpx<T>* s_tw, const cpx<T>* __restrict__ tw,
                                               int count) {
-  for (int i = threadIdx.x; i < count; i += kNT) s_tw[i] = tw[i];
+  for (int i = threadIdx.x; i < count; i += NT) s_tw[i] = tw[i];
 }
 
 // Zero the padding row of an odd-height grid (the partner of the last row in
@@ -57,35 +57,36 @@ __device__ __forceinline__ int bin_off(int f, const Grid2D& G) {
     default: return hipErrorInvalidValue;                                    \
   }
 
-// Accumulator bins of one thread: NBR in registers, NBL in its private LDS slots.
-template <typename T, int NBR, int NBL>
+// Accumulator bins of one thread: NBR in registers, NBL in its private LDS
+// slots (workgroups of NT threads).
+template <typename T, int NBR, int NBL, int NT = kNT>
 struct BinAcc {
   cpx<T> r[NBR > 0 ? NBR : 1];
-  cpx<T>* l;  // S.acc + threadIdx.x, stride kNT
+  cpx<T>* l;  // S.acc + threadIdx.x, stride NT
   __device__ __forceinline__ void init(cpx<T>* lds_acc) {
     l = lds_acc + threadIdx.x;
 #pragma unroll
     for (int i = 0; i < NBR; ++i) r[i] = {(T)0, (T)0};
 #pragma unroll
-    for (int i = 0; i < NBL; ++i) l[i * kNT] = {(T)0, (T)0};
+    for (int i = 0; i < NBL; ++i) l[i * NT] = {(T)0, (T)0};
   }
-  // apply fn(bin f, acc&) to every bin f = threadIdx.x + i*kNT < F
+  // apply fn(bin f, acc&) to every bin f = threadIdx.x + i*NT < F
   template <typename Fn>
   __device__ __forceinline__ void each(int F, Fn&& fn) {
     int tid = threadIdx.x;
     asm volatile("" : "+v"(tid));  // bin index math stays at the use (LICM)
 #pragma unroll
     for (int i = 0; i < NBR; ++i) {
-      const int f = tid + i * kNT;
+      const int f = tid + i * NT;
       if (f < F) fn(f, r[i]);
     }
 #pragma unroll
     for (int i = 0; i < NBL; ++i) {
-      const int f = tid + (NBR + i) * kNT;
+      const int f = tid + (NBR + i) * NT;
       if (f < F) {
-        cpx<T> a = l[i * kNT];
+        cpx<T> a = l[i * NT];
         fn(f, a);
-        l[i * kNT] = a;
+        l[i * NT] = a;
       }
     }
   }
