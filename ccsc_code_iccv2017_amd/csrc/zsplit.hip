@@ -107,8 +107,13 @@ __global__ __launch_bounds__(NT) void k_zsplit(const T* U, T* Uo, T* __restrict_
       for (int i = 0; i < kZsPrefetch && i < NPR; ++i) {
         const int e2 = tid + i * NT;
         if (e2 < P2) {
+#ifndef CCSC_ABL_NOMEM
           uv[i] = ld16<V2>(U2, (uint32_t)e2 * 16u);
           yv[i] = ld16<V2>(Y2, (uint32_t)e2 * 16u);
+#else
+          uv[i].x = uv[i].y = (T)e2;
+          yv[i].x = yv[i].y = (T)k;
+#endif
         }
       }
     }
@@ -123,7 +128,9 @@ __global__ __launch_bounds__(NT) void k_zsplit(const T* U, T* Uo, T* __restrict_
           lds_cpx_store(S.slice + y * RS + 2 * (f - y * GO::Xh(Gd)), 1, cmulc(dk[f], Wp[f]));
         }
       }
+#ifndef CCSC_ABL_NOFFT
       GO::c2r(S.slice, Gd, S.tw, tid);
+#endif
     }
     asm volatile("" : "+v"(tid));  // elementwise index math after the C2R, not live across it
     if (vec) {
@@ -131,8 +138,13 @@ __global__ __launch_bounds__(NT) void k_zsplit(const T* U, T* Uo, T* __restrict_
       for (int i = kZsPrefetch; i < NPR; ++i) {
         const int e2 = tid + i * NT;
         if (e2 < P2) {
+#ifndef CCSC_ABL_NOMEM
           uv[i] = ld16<V2>(U2, (uint32_t)e2 * 16u);
           yv[i] = ld16<V2>(Y2, (uint32_t)e2 * 16u);
+#else
+          uv[i].x = uv[i].y = (T)e2;
+          yv[i].x = yv[i].y = (T)k;
+#endif
         }
       }
 #pragma unroll
@@ -153,8 +165,12 @@ __global__ __launch_bounds__(NT) void k_zsplit(const T* U, T* Uo, T* __restrict_
           un.y = soft_dual(zv.y, yv[i].y, theta, yn.y);
           cn.x = un.x - yn.x;
           cn.y = un.y - yn.y;
+#ifndef CCSC_ABL_NOMEM
           st16<V2>(Uo2, (uint32_t)e2 * 16u, un);
           st16<V2>(Y2, (uint32_t)e2 * 16u, yn);
+#else
+          if (un.x == (T)-1.2345) st16<V2>(Uo2, (uint32_t)e2 * 16u, un);
+#endif
           *reinterpret_cast<V2*>(q) = cn;
         }
       }
@@ -173,7 +189,11 @@ __global__ __launch_bounds__(NT) void k_zsplit(const T* U, T* Uo, T* __restrict_
     }
     if (GO::Yp(Gd) != GO::Y(Gd))
       for (int x = tid; x < RS; x += NT) S.slice[Yd * RS + x] = (T)0;
+#ifndef CCSC_ABL_NOFFT
     GO::r2c(S.slice, Gd, S.tw, tid);
+#else
+    lds_sync();
+#endif
     const cpx<T>* dk = dhat + (int64_t)k * F;
     acc.each(F, [&](int f, cpx<T>& a) {
       const int y = f / GO::Xh(Gd);
