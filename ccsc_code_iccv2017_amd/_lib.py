@@ -19,7 +19,8 @@ CCSC_E_NOMEM = -4
 CCSC_E_UNSUPPORTED = -5
 CCSC_E_STATE = -6
 
-CCSC_DPAR, CCSC_DZPAR, CCSC_L3D, CCSC_L4D = 0, 1, 2, 3
+CCSC_DPAR, CCSC_DZPAR, CCSC_L3D, CCSC_L4D, CCSC_HS23 = 0, 1, 2, 3, 4
+ABI_VERSION = 2
 VERBOSE = {"none": 0, "brief": 1, "all": 2}
 CCSC_FP64, CCSC_FP32 = 0, 1
 
@@ -71,6 +72,7 @@ class IterLog(C.Structure):
         ("trace_z_diff", _dp),
         ("n_d", _ip),
         ("n_z", _ip),
+        ("flags", _ip),
     ]
 
 
@@ -96,8 +98,13 @@ SIGNATURES = {
     "ccsc_learn": (C.c_int32, [C.c_void_p, C.POINTER(Problem), _dp, _dp, _dp,
                                C.POINTER(Outputs), C.POINTER(IterLog), CB, C.c_void_p,
                                C.c_char_p, C.c_size_t]),
+    "ccsc_learn_hs23": (C.c_int32, [C.c_void_p, C.POINTER(Problem), _dp, _dp, _dp, _dp,
+                                    C.POINTER(Outputs), C.POINTER(IterLog), CB, C.c_void_p,
+                                    C.c_char_p, C.c_size_t]),
     "ccsc_session_create": (C.c_void_p, [C.c_void_p, C.POINTER(Problem), _dp, _dp, _dp,
                                          C.c_char_p, C.c_size_t]),
+    "ccsc_session_create_hs23": (C.c_void_p, [C.c_void_p, C.POINTER(Problem), _dp, _dp, _dp, _dp,
+                                              C.c_char_p, C.c_size_t]),
     "ccsc_session_step": (C.c_int32, [C.c_void_p, C.c_int32, C.POINTER(C.c_int32), C.c_char_p,
                                       C.c_size_t]),
     "ccsc_session_objective": (C.c_int32, [C.c_void_p, _dp, C.c_char_p, C.c_size_t]),

@@ -240,14 +240,22 @@ static std::vector<cpx<double>> make_twiddles(const Grid2D& G) {
 // Problem resolution (Appendix A of SURVEY.md)
 // ---------------------------------------------------------------------------
 static void resolve_problem(ccsc_problem& p) {
-  if (p.variant < CCSC_DPAR || p.variant > CCSC_L4D) throw Err(CCSC_E_INVALID, "unknown variant");
+  if (p.variant < CCSC_DPAR || p.variant > CCSC_HS23) throw Err(CCSC_E_INVALID, "unknown variant");
   const bool is3 = p.variant == CCSC_L3D;
+  const bool isHS = p.variant == CCSC_HS23;
   const int want_ndim = is3 ? 3 : 2;
   if (p.ndim == 0) p.ndim = want_ndim;
   if (p.ndim != want_ndim) throw Err(CCSC_E_INVALID, "ndim does not match the variant");
   for (int i = 0; i < p.ndim; ++i)
     if (p.sb[i] <= 0) throw Err(CCSC_E_INVALID, "spatial size of b must be positive");
-  if (p.variant != CCSC_L4D) {
+  if (isHS) {
+    // W wavelengths = kernel_size(3) = size(b, 3) (L23:6-15); they play the role of views
+    if (p.views[0] <= 0)
+      throw Err(CCSC_E_INVALID, "2-3D learner needs the wavelength count W (kernel_size(3)) in views[0]");
+    p.views[1] = 1;
+    if (!(p.lambda_prior > 0))
+      throw Err(CCSC_E_INVALID, "2-3D learner needs lambda_prior > 0 (gamma_heuristic = 60*lambda/max(b), L23:36)");
+  } else if (p.variant != CCSC_L4D) {
     p.views[0] = p.views[1] = 1;
   } else if (p.views[0] <= 0 || p.views[1] <= 0 || p.views[0] != p.views[1]) {
     throw Err(CCSC_E_INVALID, "4D needs equal positive view counts U == V (L4:9-10, Q9)");
@@ -271,6 +279,16 @@ static void resolve_problem(ccsc_problem& p) {
       if (p.variant == CCSC_L3D) { rd = 5000; rz = 1; td = 1; }  // L3:109,168,175
       break;                                                      // L4:105,159,162
     }
+    case CCSC_HS23:
+      // one non-consensus ADMM over all images; rho_D = gamma_D(2)/gamma_D(1) = 5000
+      // (L23:37,93), rho_Z = W gamma_Z(2)/gamma_Z(1) = 500 W (L23:38,311); the prox
+      // thresholds follow from gamma_heuristic at run time (engine: SessionHS)
+      if (p.n > INT32_MAX) throw Err(CCSC_E_INVALID, "n too large");
+      ni = (int)p.n;
+      rd = 5000;
+      rz = 500.0 * p.views[0];
+      td = 1;
+      break;
   }
   if (p.ni <= 0) p.ni = ni;
   if (p.max_it_d <= 0) p.max_it_d = mid;
@@ -302,7 +320,8 @@ struct Geom {
 // engine capability check (separate from validity: valid reference inputs we
 // do not run yet return CCSC_E_UNSUPPORTED)
 static void check_supported(const ccsc_problem& p, Geom* Gout) {
-  if ((int64_t)p.K * p.views[0] * p.views[1] > 2048)
+  // (the 2-3D learner forms its right-hand sides with the per-bin GEMM, not in the gram kernel)
+  if (p.variant != CCSC_HS23 && (int64_t)p.K * p.views[0] * p.views[1] > 2048)
     throw Err(CCSC_E_UNSUPPORTED, "K * views > 2048 exceeds the gram kernel's RHS budget");
   if (p.precision != CCSC_FP64) throw Err(CCSC_E_UNSUPPORTED, "only CCSC_FP64 is built");
   if (p.K > 110) throw Err(CCSC_E_UNSUPPORTED, "K > 110 exceeds the gram kernel's tile budget");
@@ -980,6 +999,7 @@ struct Session2D {
     }
     if (out->z_res) {
       materialize_z();
+      HIPCHK(hipStreamSynchronize(st));   // st is non-blocking: hipMemcpy does not order after it
       HIPCHK(hipMemcpy(out->z_res, z.p, m.z, hipMemcpyDeviceToHost));
     }
     if (out->DZ) {
@@ -1005,6 +1025,7 @@ struct Session2D {
     for (int i = 0; i < no; ++i) {
       if (lg->n_d) lg->n_d[i] = v_nd[i];
       if (lg->n_z) lg->n_z[i] = v_nz[i];
+      if (lg->flags) lg->flags[i] = 0;
       for (int t = 0; t < p.max_it_d; ++t) {
         const size_t q = (size_t)i * p.max_it_d + t;
         if (lg->trace_obj_d) lg->trace_obj_d[q] = q < tr_od.size() ? tr_od[q] : NAN;
@@ -1037,10 +1058,384 @@ struct Session2D {
   }
 };
 
+// ---------------------------------------------------------------------------
+// Session: 2-3D hyperspectral learner (L23 = 2-3D/DictionaryLearning/admm_learn.m)
+// ---------------------------------------------------------------------------
+// One non-consensus ADMM over all n images (one block).  It runs on one rank:
+// its d-solve sums over every image per frequency, so sharding images needs an
+// all-reduce of K x K Grams ("replicas only at first").
+// Device state (hs23.hip):
+//   real     [X,Y,W,n]  v = H z (= Dz - smoothinit), eD = d_D{1}, eZ = d_Z{1}, smp = smoothinit
+//            [X,Y,W,K]  D, yD = -d_D{2} (the consensus kernels' sign), Dold
+//            [X,Y,K,n]  z, eZ2 = d_Z{2}, zold
+//   spectra  Zh [n][K][F] (zhat; xi_Z{2} in place), Xi [n][W][F] (xi{1}, also H zhat),
+//            Ch [K][W][F] (xi_D{2}), Dh, Dhold [K][W][F] (d_hat), h [F][W][K],
+//            L [F][K(K+1)/2] (Cholesky of Z'Z + rho I per bin)
+struct PlanHS {
+  size_t b, vwn, dwk, zkn, Zh, Xi, dspec, L, h, misc;
+  size_t total() const { return b + 4 * vwn + 3 * dwk + 3 * zkn + Zh + Xi + 3 * dspec + L + h + misc; }
+};
+
+static PlanHS plan_hs(const ccsc_problem& p, const Geom& g) {
+  PlanHS m{};
+  const size_t P = g.P(), F = g.F(), K = p.K, W = p.views[0], n = p.n;
+  const size_t SS = (size_t)p.psf * p.psf;
+  m.b = (size_t)p.sb[0] * p.sb[1] * W * n * 8;
+  m.vwn = P * W * n * 8;
+  m.dwk = P * W * K * 8;
+  m.zkn = P * K * n * 8;
+  m.Zh = F * K * n * 16;
+  m.Xi = F * W * n * 16;
+  m.dspec = F * W * K * 16;
+  m.L = F * (K * (K + 1) / 2) * 16;
+  m.h = F * W * K * 16;
+  // smooth_init staging, sden, support/projection, d0 staging, reduction scratch, twiddles
+  m.misc = m.b + F * 8 + 2 * W * K * SS * 8 + 2 * W * K * 8 + (SS * K + SS * W * K) * 8 +
+           (2 * std::max<size_t>(std::max(W * n, K * n), kNormParts) + 8) * 8 +
+           (size_t)g.G.ntw * 16;
+  return m;
+}
+
+struct SessionHS {
+  ccsc_ctx* ctx;
+  ccsc_problem p;
+  Geom g;
+  Grid2D G;
+  PlanHS m;
+  int r, s, SS, K, W, KG, P, F, sbx, sby;
+  int n;
+  hipStream_t st;
+  double th_D1 = 0, th_Z1 = 0, th_Z2 = 0, gamma_h = 0;
+
+  DevBuf tw, bdev, smp, v, eD, eZ, D, yD, Dold, z, eZ2, zold, Zh, Xi, Ch, Dh, Dhold, L, h, sden,
+      Usup, supp, dnorm, part, pair;
+
+  int outer_done = 0;
+  bool finished = false;
+  double obj = std::numeric_limits<double>::quiet_NaN();
+  double obj_filter = obj, obj_z = obj;
+  std::vector<double> v_obj_d, v_obj_z, v_tim, tr_od, tr_oz, tr_dd, tr_zd;
+  std::vector<int32_t> v_nd, v_nz, v_flags;
+
+  SessionHS(ccsc_ctx* c, const ccsc_problem& pin, const double* b, const double* smooth_init,
+            const double* d0, const double* z0)
+      : ctx(c), p(pin), st(c->stream) {
+    resolve_problem(p);
+    if (p.variant != CCSC_HS23) throw Err(CCSC_E_INVALID, "SessionHS runs the 2-3D learner only");
+    check_supported(p, &g);
+    if (ctx->nranks != 1)
+      throw Err(CCSC_E_UNSUPPORTED, "the 2-3D learner runs on one rank (its d-solve sums over "
+                                    "every image per frequency; SURVEY.md 8e: replicas only)");
+    if (!b || !smooth_init) throw Err(CCSC_E_INVALID, "b and smooth_init must not be NULL");
+    G = g.G;
+    m = plan_hs(p, g);
+    r = p.psf / 2;
+    s = p.psf;
+    SS = s * s;
+    K = p.K;
+    W = p.views[0];
+    KG = K * W;
+    P = G.X * G.Y;
+    F = G.F;
+    sbx = (int)p.sb[0];
+    sby = (int)p.sb[1];
+    n = (int)p.n;
+    if (r > sbx || r > sby)
+      throw Err(CCSC_E_UNSUPPORTED, "symmetric padding wider than the image (L23:19)");
+
+    size_t freeb = 0, totalb = 0;
+    HIPCHK(hipMemGetInfo(&freeb, &totalb));
+    if (m.total() > freeb)
+      throw Err(CCSC_E_NOMEM, "device plan needs " + std::to_string(m.total() >> 20) + " MiB, " +
+                                  std::to_string(freeb >> 20) + " MiB free");
+    auto tws = make_twiddles(G);
+    tw.alloc(tws.size() * sizeof(cpx<double>));
+    HIPCHK(hipMemcpy(tw.p, tws.data(), tw.bytes, hipMemcpyHostToDevice));
+    const size_t vwn = (size_t)P * W * n, dwk = (size_t)P * KG, zkn = (size_t)P * K * n;
+    bdev.alloc(m.b);
+    smp.alloc(vwn * 8);
+    v.alloc(vwn * 8);
+    eD.alloc(vwn * 8);
+    eZ.alloc(vwn * 8);
+    D.alloc(dwk * 8);
+    yD.alloc(dwk * 8);
+    Dold.alloc(dwk * 8);
+    z.alloc(zkn * 8);
+    eZ2.alloc(zkn * 8);
+    zold.alloc(zkn * 8);
+    Zh.alloc(m.Zh);
+    Xi.alloc(m.Xi);
+    Ch.alloc(m.dspec);
+    Dh.alloc(m.dspec);
+    Dhold.alloc(m.dspec);
+    L.alloc(m.L);
+    h.alloc(m.h);
+    sden.alloc((size_t)F * 8);
+    Usup.alloc((size_t)KG * SS * 8);
+    supp.alloc((size_t)KG * SS * 8);
+    dnorm.alloc((size_t)2 * KG * 8);
+    part.alloc((size_t)2 * std::max<int64_t>(std::max<int64_t>((int64_t)W * n, (int64_t)K * n),
+                                             kNormParts) * 8);
+    pair.alloc(8 * 8);
+
+    // data: b and smoothinit = padarray(smooth_init, [r r 0 0], 'symmetric') (L23:19)
+    HIPCHK(hipMemcpy(bdev.p, b, m.b, hipMemcpyHostToDevice));
+    {
+      DevBuf stage;
+      stage.alloc(m.b);
+      HIPCHK(hipMemcpy(stage.p, smooth_init, m.b, hipMemcpyHostToDevice));
+      HIPCHK(launch_pad_symmetric<double>(stage.as<double>(), smp.as<double>(), sbx, sby, r, G.X,
+                                          G.Y, (int64_t)W * n, st));
+      HIPCHK(hipStreamSynchronize(st));
+    }
+    // gammas (L23:35-38): gamma_heuristic = 60 lambda / max(b(:))
+    HIPCHK(launch_max<double>(bdev.as<double>(), (int64_t)((size_t)sbx * sby * W * n),
+                              part.as<double>(), pair.as<double>(), st));
+    double bmax = 0;
+    HIPCHK(hipMemcpyAsync(&bmax, pair.p, sizeof(double), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (!(bmax > 0)) throw Err(CCSC_E_INVALID, "max(b(:)) must be positive (L23:36)");
+    gamma_h = 60.0 * p.lambda_prior / bmax;
+    const double gD1 = gamma_h / p.rho_d;                // gammas_D = [gh/5000, gh]  (L23:37)
+    const double gZ1 = gamma_h * W / p.rho_z;            // gammas_Z = [gh/500, gh]   (L23:38)
+    th_D1 = p.lambda_residual / gD1;                     // lambda(1)/gammas_D(1)     (L23:112)
+    th_Z1 = p.lambda_residual / gZ1;                     // lambda(1)/gammas_Z(1)     (L23:175)
+    th_Z2 = p.lambda_prior / gamma_h;                    // lambda(2)/gammas_Z(2)     (L23:176)
+
+    // filters: d0 [s,s,K] replicated over W, embedded at circshift(-r) (L23:54-56)
+    {
+      DevBuf d0dev, d0w;
+      d0dev.alloc((size_t)SS * K * 8);
+      d0w.alloc((size_t)SS * KG * 8);
+      if (d0) HIPCHK(hipMemcpy(d0dev.p, d0, d0dev.bytes, hipMemcpyHostToDevice));
+      else HIPCHK(launch_randn<double>(d0dev.as<double>(), (int64_t)SS * K, p.seed ^ 0xd0d0d0d0ULL, 0, st));
+      HIPCHK(launch_rep_filters<double>(d0dev.as<double>(), d0w.as<double>(), SS, W, K, st));
+      HIPCHK(launch_embed_filters<double>(d0w.as<double>(), D.as<double>(), 1, KG, s, G, 1, st));
+      HIPCHK(hipStreamSynchronize(st));
+    }
+    HIPCHK(hipMemsetAsync(yD.p, 0, yD.bytes, st));
+    HIPCHK(hipMemsetAsync(eD.p, 0, eD.bytes, st));
+    HIPCHK(hipMemsetAsync(eZ.p, 0, eZ.bytes, st));
+    HIPCHK(hipMemsetAsync(eZ2.p, 0, eZ2.bytes, st));
+    // codes z = randn(size_z) (L23:69)
+    if (z0) HIPCHK(hipMemcpy(z.p, z0, z.bytes, hipMemcpyHostToDevice));
+    else HIPCHK(launch_randn<double>(z.as<double>(), (int64_t)zkn, p.seed, 0, st));
+    // d_hat = fft2(d) (L23:57); u_D{2} of the first d-iteration = Pi(d - 0) (L23:113)
+    HIPCHK(launch_r2c_embed<double>(D.as<double>(), P, G.X, G.Y, 0, 0, Dh.as<cpx<double>>(), F, KG,
+                                    tw.as<cpx<double>>(), G, st));
+    HIPCHK(launch_gather_support<double>(D.as<double>(), yD.as<double>(), supp.as<double>(), KG, r,
+                                         G.X, G.Y, st));
+    HIPCHK(launch_project<double>(supp.as<double>(), Usup.as<double>(), KG, SS, 1.0, st));
+    obj = objective_fresh();                              // L23:72
+    obj_filter = obj_z = obj;                             // L23:82-83
+    v_obj_d.push_back(obj);
+    v_obj_z.push_back(obj);
+    v_tim.push_back(0.0);
+  }
+
+  // v = real(ifft2(H zhat)) from Xi (= H zhat) and the objective of (z, d_hat)
+  // (objectiveFunction, L23:326-343); pair[2] must hold sum |z|.
+  double finish_objective() {
+    HIPCHK(launch_hs_c2r_v<double>(Xi.as<cpx<double>>(), v.as<double>(), bdev.as<double>(),
+                                   smp.as<double>(), nullptr, part.as<double>(), (int64_t)W * n,
+                                   tw.as<cpx<double>>(), G, r, sbx, sby, st));
+    HIPCHK(launch_sum_pairs<double>(part.as<double>(), W * n, pair.as<double>(), st));
+    double h4[4];
+    HIPCHK(hipMemcpyAsync(h4, pair.p, sizeof h4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    return p.lambda_residual * 0.5 * h4[0] + p.lambda_prior * W * h4[2];   // g_z: z repeated W times (L23:332,338)
+  }
+  // zhat = fft2(z) (L23:100,158,234), sum |z|, v = H z and the objective
+  double objective_fresh() {
+    HIPCHK(launch_r2c_embed<double>(z.as<double>(), P, G.X, G.Y, 0, 0, Zh.as<cpx<double>>(), F,
+                                    (int64_t)K * n, tw.as<cpx<double>>(), G, st));
+    HIPCHK(launch_norms<double>(z.as<double>(), nullptr, (int64_t)z.bytes / 8, part.as<double>(),
+                                pair.as<double>() + 2, st));
+    HIPCHK(launch_hs_synth<double>(Dh.as<cpx<double>>(), Zh.as<cpx<double>>(),
+                                   Xi.as<cpx<double>>(), F, W, K, n, st));
+    return finish_objective();
+  }
+  double rel_change(const DevBuf& a, const DevBuf& b) {
+    HIPCHK(launch_norms<double>(a.as<double>(), b.as<double>(), (int64_t)a.bytes / 8,
+                                part.as<double>(), pair.as<double>() + 4, st));
+    double h2[2];
+    HIPCHK(hipMemcpyAsync(h2, pair.as<double>() + 4, sizeof h2, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    return std::sqrt(h2[0]) / std::sqrt(h2[1]);
+  }
+
+  void ensure_trace_capacity(int total_outer) {
+    const double nan = std::numeric_limits<double>::quiet_NaN();
+    const size_t nd = (size_t)total_outer * p.max_it_d, nz = (size_t)total_outer * p.max_it_z;
+    if (tr_od.size() < nd) tr_od.resize(nd, nan);
+    if (tr_dd.size() < nd) tr_dd.resize(nd, nan);
+    if (tr_oz.size() < nz) tr_oz.resize(nz, nan);
+    if (tr_zd.size() < nz) tr_zd.resize(nz, nan);
+  }
+
+  // ---- one outer iteration (L23:86-226) ---------------------------------------
+  void outer_iteration() {
+    const int it = outer_done;
+    const auto t0 = std::chrono::steady_clock::now();
+    const auto* twc = tw.as<cpx<double>>();
+    const double obj_min = std::min(obj_filter, obj_z);   // L23:94
+    HIPCHK(hipMemcpyAsync(Dold.p, D.p, D.bytes, hipMemcpyDeviceToDevice, st));    // d_old (L23:95)
+    HIPCHK(hipMemcpyAsync(Dhold.p, Dh.p, Dh.bytes, hipMemcpyDeviceToDevice, st)); // d_hat_old
+    // z_hat = fft2(z) (L23:100) and v_D{1} = H z of the first d-iteration (L23:108)
+    objective_fresh();
+    // opt_f = (Z_f' Z_f + rho I)^-1 as a Cholesky factor per bin (L23:290)
+    HIPCHK(launch_gram_chol<double>(Zh.as<cpx<double>>(), Zh.as<cpx<double>>(),
+                                    L.as<cpx<double>>(), h.as<cpx<double>>(), F, K, n, p.rho_d, 0,
+                                    st));
+    for (int id = 0; id < p.max_it_d; ++id) {                                    // L23:102
+      // c = 1: masked data split (L23:112, 117, 120-121)
+      HIPCHK(launch_hs_data_r2c<double>(v.as<double>(), eD.as<double>(), bdev.as<double>(),
+                                        smp.as<double>(), Xi.as<cpx<double>>(), (int64_t)W * n,
+                                        twc, G, r, sbx, sby, th_D1, st));
+      // c = 2: kernel constraint split, y = -d_D{2} (L23:113, 117, 120-121)
+      HIPCHK(launch_dual_r2c<double>(D.as<double>(), yD.as<double>(), Usup.as<double>(),
+                                     Ch.as<cpx<double>>(), KG, twc, G, KG, r, st));
+      // d_hat = opt (Z' xi1 + rho xi2) per (bin, wavelength)  (L23:125, 289-295)
+      HIPCHK(launch_hs_corr<double>(Zh.as<cpx<double>>(), Xi.as<cpx<double>>(),
+                                    h.as<cpx<double>>(), F, W, K, n, st));
+      HIPCHK(launch_dsolve<double>(L.as<cpx<double>>(), h.as<cpx<double>>(), Ch.as<cpx<double>>(),
+                                   Dh.as<cpx<double>>(), 1, F, K, p.rho_d, W, st));
+      // d = real(ifft2(d_hat)) (L23:126); support of d - d_D{2} -> u_D{2} of the next d-iteration
+      HIPCHK(launch_c2r_dout<double>(Dh.as<cpx<double>>(), D.as<double>(), yD.as<double>(),
+                                     supp.as<double>(), dnorm.as<double>(), 0, KG, twc, G, r, st));
+      HIPCHK(launch_project<double>(supp.as<double>(), Usup.as<double>(), KG, SS, 1.0, st));
+      // objective (L23:132); its H z is v_D{1} of the next d-iteration (z is fixed here)
+      HIPCHK(launch_hs_synth<double>(Dh.as<cpx<double>>(), Zh.as<cpx<double>>(),
+                                     Xi.as<cpx<double>>(), F, W, K, n, st));
+      obj = finish_objective();
+      tr_od[(size_t)it * p.max_it_d + id] = obj;
+    }
+    obj_filter = obj;                                                            // L23:139
+    const double d_diff = rel_change(D, Dold);                                   // L23:142-146
+    tr_dd[(size_t)it * p.max_it_d] = d_diff;
+
+    // ---- Z-phase (L23:149-200) ----
+    // 1 / (rho + sum_{w,k} |d_hat|^2) per bin (L23:262-268, 317)
+    HIPCHK(launch_sden<double>(Dh.as<cpx<double>>(), sden.as<double>(), F, KG, p.rho_z, 1.0, st));
+    HIPCHK(hipMemcpyAsync(zold.p, z.p, z.bytes, hipMemcpyDeviceToDevice, st));  // z_old (L23:159)
+    // v = H z is current: the last D objective used z_hat = fft2(z) (L23:158)
+    for (int iz = 0; iz < p.max_it_z; ++iz) {                                    // L23:165
+      HIPCHK(launch_hs_data_r2c<double>(v.as<double>(), eZ.as<double>(), bdev.as<double>(),
+                                        smp.as<double>(), Xi.as<cpx<double>>(), (int64_t)W * n,
+                                        twc, G, r, sbx, sby, th_Z1, st));        // L23:175,180,183-184
+      HIPCHK(launch_hs_z_r2c<double>(z.as<double>(), eZ2.as<double>(), Zh.as<cpx<double>>(),
+                                     (int64_t)K * n, twc, G, th_Z2, st));        // L23:176,180,183-184
+      HIPCHK(launch_hs_analysis<double>(Dh.as<cpx<double>>(), Xi.as<cpx<double>>(),
+                                        Zh.as<cpx<double>>(), sden.as<double>(), p.rho_z,
+                                        Zh.as<cpx<double>>(), F, W, K, n, st));  // L23:188, 302-324
+      HIPCHK(launch_hs_c2r_z<double>(Zh.as<cpx<double>>(), z.as<double>(), part.as<double>(),
+                                     (int64_t)K * n, twc, G, st));              // L23:189
+      HIPCHK(launch_sum_pairs<double>(part.as<double>(), K * n, pair.as<double>() + 2, st));
+      // objective (L23:195); H zhat is v_Z{1} of the next z-iteration (L23:171)
+      HIPCHK(launch_hs_synth<double>(Dh.as<cpx<double>>(), Zh.as<cpx<double>>(),
+                                     Xi.as<cpx<double>>(), F, W, K, n, st));
+      obj = finish_objective();
+      tr_oz[(size_t)it * p.max_it_z + iz] = obj;
+    }
+    obj_z = obj;                                                                 // L23:202
+    int flags = 0;
+    if (obj_min <= obj_filter && obj_min <= obj_z) {                             // L23:204-213 (Q16)
+      // roll back to the iterate before this outer iteration and stop
+      HIPCHK(hipMemcpyAsync(z.p, zold.p, z.bytes, hipMemcpyDeviceToDevice, st));
+      HIPCHK(hipMemcpyAsync(Dh.p, Dhold.p, Dh.bytes, hipMemcpyDeviceToDevice, st));
+      HIPCHK(launch_c2r_plain<double>(Dh.as<cpx<double>>(), F, D.as<double>(), P, KG, twc, G,
+                                      1.0 / (double)P, st));
+      obj = objective_fresh();
+      finished = true;
+      flags |= 1;
+    } else {
+      const double z_diff = rel_change(z, zold);                                 // L23:216-220
+      tr_zd[(size_t)it * p.max_it_z] = z_diff;
+      if (z_diff < p.tol && d_diff < p.tol) finished = true;                     // L23:223
+    }
+    HIPCHK(hipStreamSynchronize(st));
+    const double secs =
+        std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    v_obj_d.push_back(obj_filter);
+    v_obj_z.push_back(obj_z);
+    v_tim.push_back(v_tim.back() + secs);
+    v_nd.push_back(p.max_it_d);
+    v_nz.push_back(p.max_it_z);
+    v_flags.push_back(flags);
+    ++outer_done;
+  }
+
+  void step(int n_outer, int32_t* done) {
+    ensure_trace_capacity(outer_done + n_outer);
+    for (int i = 0; i < n_outer && !finished; ++i) outer_iteration();
+    if (done) *done = finished ? 1 : 0;
+  }
+
+  void results(ccsc_outputs* out) {
+    if (!out) return;
+    if (out->d_res) {
+      // d_res = circshift(d, [r r 0 0])(1:2r+1, 1:2r+1, :, :)  (L23:231-232)
+      std::vector<double> Dh_((size_t)KG * P);
+      HIPCHK(hipMemcpy(Dh_.data(), D.p, D.bytes, hipMemcpyDeviceToHost));
+      for (int gI = 0; gI < KG; ++gI)
+        for (int j = 0; j < s; ++j)
+          for (int i = 0; i < s; ++i) {
+            const int x = (i - r + G.X) % G.X, y = (j - r + G.Y) % G.Y;
+            out->d_res[i + (size_t)s * (j + (size_t)s * gI)] = Dh_[(size_t)gI * P + (size_t)y * G.X + x];
+          }
+    }
+    if (out->z_res) HIPCHK(hipMemcpy(out->z_res, z.p, z.bytes, hipMemcpyDeviceToHost));
+    if (out->DZ) {
+      // Dz = real(ifft2(sum_k d_hat .* fft2(z))) + smoothinit  (L23:234-235)
+      DevBuf dz;
+      dz.alloc(v.bytes);
+      HIPCHK(launch_r2c_embed<double>(z.as<double>(), P, G.X, G.Y, 0, 0, Zh.as<cpx<double>>(), F,
+                                      (int64_t)K * n, tw.as<cpx<double>>(), G, st));
+      HIPCHK(launch_hs_synth<double>(Dh.as<cpx<double>>(), Zh.as<cpx<double>>(),
+                                     Xi.as<cpx<double>>(), F, W, K, n, st));
+      HIPCHK(launch_hs_c2r_v<double>(Xi.as<cpx<double>>(), v.as<double>(), bdev.as<double>(),
+                                     smp.as<double>(), dz.as<double>(), part.as<double>(),
+                                     (int64_t)W * n, tw.as<cpx<double>>(), G, r, sbx, sby, st));
+      HIPCHK(hipStreamSynchronize(st));   // st is non-blocking: hipMemcpy does not order after it
+      HIPCHK(hipMemcpy(out->DZ, dz.p, dz.bytes, hipMemcpyDeviceToHost));
+    }
+    if (out->obj_val) *out->obj_val = obj;   // the last objective the learner evaluated
+  }
+
+  void iterlog(ccsc_iterlog* lg) {
+    if (!lg) return;
+    const int cnt = std::min<int>(lg->capacity, (int)v_tim.size());
+    lg->count = cnt;
+    for (int i = 0; i < cnt; ++i) {
+      if (lg->obj_vals_d) lg->obj_vals_d[i] = v_obj_d[i];
+      if (lg->obj_vals_z) lg->obj_vals_z[i] = v_obj_z[i];
+      if (lg->tim_vals) lg->tim_vals[i] = v_tim[i];
+    }
+    const int no = std::min<int>(lg->capacity, outer_done);
+    for (int i = 0; i < no; ++i) {
+      if (lg->n_d) lg->n_d[i] = v_nd[i];
+      if (lg->n_z) lg->n_z[i] = v_nz[i];
+      if (lg->flags) lg->flags[i] = v_flags[i];
+      for (int t = 0; t < p.max_it_d; ++t) {
+        const size_t q = (size_t)i * p.max_it_d + t;
+        if (lg->trace_obj_d) lg->trace_obj_d[q] = q < tr_od.size() ? tr_od[q] : NAN;
+        if (lg->trace_d_diff) lg->trace_d_diff[q] = q < tr_dd.size() ? tr_dd[q] : NAN;
+      }
+      for (int t = 0; t < p.max_it_z; ++t) {
+        const size_t q = (size_t)i * p.max_it_z + t;
+        if (lg->trace_obj_z) lg->trace_obj_z[q] = q < tr_oz.size() ? tr_oz[q] : NAN;
+        if (lg->trace_z_diff) lg->trace_z_diff[q] = q < tr_zd.size() ? tr_zd[q] : NAN;
+      }
+    }
+  }
+};
+
 }  // namespace ccsc
 
 struct ccsc_session {
   std::unique_ptr<ccsc::Session2D> s2;
+  std::unique_ptr<ccsc::SessionHS> hs;
+  ccsc_ctx* ctx() const { return s2 ? s2->ctx : hs->ctx; }
 };
 
 // ===========================================================================
@@ -1084,7 +1479,12 @@ int32_t ccsc_plan_bytes(const ccsc_problem* p, int32_t rank, int32_t nranks, uin
     resolve_problem(q);
     Geom g;
     check_supported(q, &g);
-    *bytes = plan2d(q, g, rank, nranks).total();
+    if (q.variant == CCSC_HS23) {
+      if (nranks != 1) throw Err(CCSC_E_UNSUPPORTED, "the 2-3D learner runs on one rank");
+      *bytes = plan_hs(q, g).total();
+    } else {
+      *bytes = plan2d(q, g, rank, nranks).total();
+    }
   });
 }
 
@@ -1160,6 +1560,8 @@ ccsc_session* ccsc_session_create(ccsc_ctx* ctx, const ccsc_problem* p, const do
   ccsc_session* out = nullptr;
   guarded(err, errlen, [&] {
     if (!ctx || !p) throw Err(CCSC_E_INVALID, "NULL ctx/problem");
+    if (p->variant == CCSC_HS23)
+      throw Err(CCSC_E_INVALID, "the 2-3D learner takes smooth_init: use ccsc_session_create_hs23");
     HIPCHK(hipSetDevice(ctx->device));
     std::unique_ptr<ccsc_session> s(new ccsc_session());
     s->s2.reset(new Session2D(ctx, *p, b, d0, z0));
@@ -1168,40 +1570,63 @@ ccsc_session* ccsc_session_create(ccsc_ctx* ctx, const ccsc_problem* p, const do
   return out;
 }
 
+ccsc_session* ccsc_session_create_hs23(ccsc_ctx* ctx, const ccsc_problem* p, const double* b,
+                                       const double* smooth_init, const double* d0,
+                                       const double* z0, char* err, size_t errlen) {
+  ccsc_session* out = nullptr;
+  guarded(err, errlen, [&] {
+    if (!ctx || !p) throw Err(CCSC_E_INVALID, "NULL ctx/problem");
+    HIPCHK(hipSetDevice(ctx->device));
+    std::unique_ptr<ccsc_session> s(new ccsc_session());
+    s->hs.reset(new SessionHS(ctx, *p, b, smooth_init, d0, z0));
+    out = s.release();
+  });
+  return out;
+}
+
+static void need_session(const ccsc_session* s) {
+  if (!s || (!s->s2 && !s->hs)) throw Err(CCSC_E_STATE, "no session");
+}
+
 int32_t ccsc_session_step(ccsc_session* s, int32_t n_outer, int32_t* done, char* err,
                           size_t errlen) {
   return guarded(err, errlen, [&] {
-    if (!s || !s->s2) throw Err(CCSC_E_STATE, "no session");
-    HIPCHK(hipSetDevice(s->s2->ctx->device));
-    s->s2->step(n_outer, done);
+    need_session(s);
+    HIPCHK(hipSetDevice(s->ctx()->device));
+    if (s->hs) s->hs->step(n_outer, done);
+    else s->s2->step(n_outer, done);
   });
 }
 
 int32_t ccsc_session_objective(ccsc_session* s, double* obj, char* err, size_t errlen) {
   return guarded(err, errlen, [&] {
-    if (!s || !s->s2 || !obj) throw Err(CCSC_E_STATE, "no session");
-    HIPCHK(hipSetDevice(s->s2->ctx->device));
-    *obj = s->s2->objective(s->s2->dhat.as<cpx<double>>(), nullptr);
+    need_session(s);
+    if (!obj) throw Err(CCSC_E_INVALID, "NULL obj");
+    HIPCHK(hipSetDevice(s->ctx()->device));
+    if (s->hs) *obj = s->hs->objective_fresh();
+    else *obj = s->s2->objective(s->s2->dhat.as<cpx<double>>(), nullptr);
   });
 }
 
 int32_t ccsc_session_results(ccsc_session* s, ccsc_outputs* out, char* err, size_t errlen) {
   return guarded(err, errlen, [&] {
-    if (!s || !s->s2) throw Err(CCSC_E_STATE, "no session");
-    HIPCHK(hipSetDevice(s->s2->ctx->device));
-    s->s2->results(out);
+    need_session(s);
+    HIPCHK(hipSetDevice(s->ctx()->device));
+    if (s->hs) s->hs->results(out);
+    else s->s2->results(out);
   });
 }
 
 int32_t ccsc_session_iterlog(ccsc_session* s, ccsc_iterlog* log, char* err, size_t errlen) {
   return guarded(err, errlen, [&] {
-    if (!s || !s->s2) throw Err(CCSC_E_STATE, "no session");
-    s->s2->iterlog(log);
+    need_session(s);
+    if (s->hs) s->hs->iterlog(log);
+    else s->s2->iterlog(log);
   });
 }
 
 int32_t ccsc_session_set_profiling(ccsc_session* s, int32_t on) {
-  if (!s || !s->s2) return CCSC_E_STATE;
+  if (!s || !s->s2) return s && s->hs ? CCSC_OK : CCSC_E_STATE;  // 2-3D: no per-kernel timers
   s->s2->prof = on != 0;
   return CCSC_OK;
 }
@@ -1210,19 +1635,38 @@ int32_t ccsc_session_kernel_stats(ccsc_session* s, int32_t id, int64_t* launches
                                   double* total_ms, double* alg_bytes_per_launch, char* err,
                                   size_t errlen) {
   return guarded(err, errlen, [&] {
-    if (!s || !s->s2) throw Err(CCSC_E_STATE, "no session");
+    need_session(s);
     if (id < 0 || id > 4) throw Err(CCSC_E_INVALID, "kernel id out of range");
-    if (launches) *launches = s->s2->k_launch[id];
-    if (total_ms) *total_ms = s->s2->k_ms[id];
-    if (alg_bytes_per_launch) *alg_bytes_per_launch = s->s2->alg_bytes(id);
+    const bool t = (bool)s->s2;
+    if (launches) *launches = t ? s->s2->k_launch[id] : 0;
+    if (total_ms) *total_ms = t ? s->s2->k_ms[id] : 0.0;
+    if (alg_bytes_per_launch) *alg_bytes_per_launch = t ? s->s2->alg_bytes(id) : 0.0;
     (void)kKernelNames;
   });
 }
 
 void ccsc_session_destroy(ccsc_session* s) {
   if (!s) return;
-  if (s->s2) hipSetDevice(s->s2->ctx->device);
+  if (s->s2 || s->hs) hipSetDevice(s->ctx()->device);
   delete s;
+}
+
+int32_t ccsc_learn_hs23(ccsc_ctx* ctx, const ccsc_problem* p, const double* b,
+                        const double* smooth_init, const double* d0, const double* z0,
+                        ccsc_outputs* out, ccsc_iterlog* log, ccsc_cb cb, void* user, char* err,
+                        size_t errlen) {
+  return guarded(err, errlen, [&] {
+    if (!ctx || !p) throw Err(CCSC_E_INVALID, "NULL ctx/problem");
+    HIPCHK(hipSetDevice(ctx->device));
+    SessionHS S(ctx, *p, b, smooth_init, d0, z0);
+    S.ensure_trace_capacity(S.p.max_it);
+    for (int i = 0; i < S.p.max_it && !S.finished; ++i) {
+      S.outer_iteration();
+      if (cb) cb(user, S.outer_done, S.v_obj_d.back(), S.v_obj_z.back(), S.v_tim.back());
+    }
+    S.results(out);
+    S.iterlog(log);
+  });
 }
 
 int32_t ccsc_learn(ccsc_ctx* ctx, const ccsc_problem* p, const double* b, const double* d0,
@@ -1230,6 +1674,8 @@ int32_t ccsc_learn(ccsc_ctx* ctx, const ccsc_problem* p, const double* b, const 
                    void* user, char* err, size_t errlen) {
   return guarded(err, errlen, [&] {
     if (!ctx || !p) throw Err(CCSC_E_INVALID, "NULL ctx/problem");
+    if (p->variant == CCSC_HS23)
+      throw Err(CCSC_E_INVALID, "the 2-3D learner takes smooth_init: use ccsc_learn_hs23");
     HIPCHK(hipSetDevice(ctx->device));
     Session2D S(ctx, *p, b, d0, z0);
     S.ensure_trace_capacity(S.p.max_it);

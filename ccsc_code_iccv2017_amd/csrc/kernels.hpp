@@ -101,6 +101,46 @@ template <typename T>
 hipError_t launch_crop_sq(const T* Dz, const T* b, int sx, int sy, int st, int r, int X, int Y,
                           const T* z, int64_t zcount, T* part, hipStream_t stream);
 
+// ---- hs23.hip: the 2-3D hyperspectral learner (L23) ----------------------------
+// Spectra slice-major [slice][F]: dhat [K][W], zhat [n][K], Xi1 / Yv [n][W]; h [F][W][K].
+template <typename T>
+hipError_t launch_hs_synth(const cpx<T>* dhat, const cpx<T>* zhat, cpx<T>* Yv, int F, int W,
+                           int K, int n, hipStream_t st);
+template <typename T>
+hipError_t launch_hs_analysis(const cpx<T>* dhat, const cpx<T>* Xi1, const cpx<T>* Xi2,
+                              const T* sden, T rho, cpx<T>* zhat, int F, int W, int K, int n,
+                              hipStream_t st);
+template <typename T>
+hipError_t launch_hs_corr(const cpx<T>* zhat, const cpx<T>* Xi1, cpx<T>* h, int F, int W, int K,
+                          int n, hipStream_t st);
+template <typename T>
+hipError_t launch_hs_c2r_v(const cpx<T>* Ys, T* v, const T* b, const T* sm, T* DZ, T* part,
+                           int64_t nslices, const cpx<T>* tw, const Grid2D& G, int r, int sbx,
+                           int sby, hipStream_t st);
+template <typename T>
+hipError_t launch_hs_data_r2c(const T* v, T* e, const T* b, const T* sm, cpx<T>* Xi,
+                              int64_t nslices, const cpx<T>* tw, const Grid2D& G, int r, int sbx,
+                              int sby, T theta, hipStream_t st);
+template <typename T>
+hipError_t launch_hs_z_r2c(const T* z, T* e, cpx<T>* Xi, int64_t nslices, const cpx<T>* tw,
+                           const Grid2D& G, T theta, hipStream_t st);
+template <typename T>
+hipError_t launch_hs_c2r_z(const cpx<T>* Zh, T* z, T* part, int64_t nslices, const cpx<T>* tw,
+                           const Grid2D& G, hipStream_t st);
+template <typename T>
+hipError_t launch_pad_symmetric(const T* a, T* out, int sbx, int sby, int r, int X, int Y,
+                                int64_t nslices, hipStream_t st);
+template <typename T>
+hipError_t launch_rep_filters(const T* d0, T* out, int SS, int W, int K, hipStream_t st);
+template <typename T>
+hipError_t launch_gather_support(const T* D, const T* y, T* supp, int KG, int r, int X, int Y,
+                                 hipStream_t st);
+constexpr int kNormParts = 1024;  // scratch pairs of launch_norms / launch_max
+template <typename T>
+hipError_t launch_norms(const T* a, const T* b, int64_t count, T* part, T* out2, hipStream_t st);
+template <typename T>
+hipError_t launch_max(const T* a, int64_t count, T* part, T* out, hipStream_t st);
+
 // ---- util.hip ---------------------------------------------------------------
 template <typename T>
 hipError_t launch_randn(T* out, int64_t count, uint64_t seed, uint64_t offset, hipStream_t st);

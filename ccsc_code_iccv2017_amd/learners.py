@@ -8,6 +8,10 @@ functions they replace (what a MEX wrapper would expose):
                                    # 2D/admm_learn_conv2D_large_dParallel.m:1-4
   d_res, z_res, DZ, iterations = admm_learn_conv2D_large_dzParallel(...)
                                    # 2D/admm_learn_conv2D_large_dzParallel.m:1-4
+  d_res, z_res, DZ, obj_val, iterations = admm_learn_conv3D_large(...)      # 3D/...:1-4
+  d_res, z_res, DZ, obj_val, iterations = admm_learn_conv4D_lightfield(...) # 4D/...:1-4
+  d_res, z_res, Dz, obj_val = admm_learn(b, kernel_size, lambda_residual, lambda_prior,
+      max_it, tol, verbose, init, smooth_init)   # 2-3D/DictionaryLearning/admm_learn.m:1-4
 
 Arrays carry the MATLAB shapes (b: [x, y, n]; kernel_size = [psf, psf, K];
 d_res: [psf, psf, K]; z_res: [X, Y, K, n]; DZ: [X, Y, 1, n]) and are exchanged
@@ -103,6 +107,8 @@ def make_problem(variant, b_shape, kernel_size, lambda_residual, lambda_prior, m
     p.views[0] = p.views[1] = 1
     if variant == L.CCSC_L4D and len(kernel_size) == 5:   # b: [x, y, U, V, n]; kernel [s, s, U, V, K]
         p.views[0], p.views[1] = int(kernel_size[2]), int(kernel_size[3])
+    if variant == L.CCSC_HS23:                            # b: [x, y, W, n]; kernel [s, s, W, K]
+        p.views[0] = int(kernel_size[2])
     p.n = int(b_shape[-1])
     p.K = int(kernel_size[-1])
     p.psf = int(kernel_size[0])
@@ -152,17 +158,29 @@ def _f64(a):
 
 
 class Session:
-    """Stateful learner (warm restart, bench): create -> step(k) -> results."""
+    """Stateful learner (warm restart, bench): create -> step(k) -> results.
+    The 2-3D learner (variant CCSC_HS23) also takes ``smooth_init``."""
 
-    def __init__(self, ctx: Context, p: L.Problem, b, d0=None, z0=None):
+    def __init__(self, ctx: Context, p: L.Problem, b, d0=None, z0=None, smooth_init=None):
         self.ctx = ctx
         self.p = resolve(p)
         self._b = _f64(b)
         self._d0 = _f64(d0)
         self._z0 = _f64(z0)
         eb = L.errbuf()
-        self.ptr = L.lib().ccsc_session_create(ctx.ptr, C.byref(self.p), L.dptr(self._b),
-                                               L.dptr(self._d0), L.dptr(self._z0), eb, len(eb))
+        if self.p.variant == L.CCSC_HS23:
+            if smooth_init is None:
+                raise ValueError("the 2-3D learner needs smooth_init (admm_learn.m:4)")
+            self._sm = _f64(smooth_init)
+            if self._sm.shape != self._b.shape:
+                raise ValueError("smooth_init must have the shape of b")
+            self.ptr = L.lib().ccsc_session_create_hs23(
+                ctx.ptr, C.byref(self.p), L.dptr(self._b), L.dptr(self._sm), L.dptr(self._d0),
+                L.dptr(self._z0), eb, len(eb))
+        else:
+            self.ptr = L.lib().ccsc_session_create(ctx.ptr, C.byref(self.p), L.dptr(self._b),
+                                                   L.dptr(self._d0), L.dptr(self._z0), eb,
+                                                   len(eb))
         if not self.ptr:
             raise L.CCSCError(L.CCSC_E_INVALID, eb.value.decode(errors="replace"))
         b0, nb = shard(self.p, ctx.rank, ctx.nranks)
@@ -215,7 +233,12 @@ class Session:
             L.check(L.lib().ccsc_session_results(self.ptr, C.byref(out), eb, len(eb)), eb)
             return d_res, z_res, DZ, (float(obj[0]) if want_obj else None)
         X, Y = self.grid()
-        if p.variant == L.CCSC_L4D:
+        if p.variant == L.CCSC_HS23:
+            W = p.views[0]
+            d_res = np.zeros((p.psf, p.psf, W, p.K), order="F")
+            z_res = np.zeros((X, Y, p.K, self.n_local), order="F") if want_z else None
+            DZ = np.zeros((X, Y, W, self.n_local), order="F") if want_DZ else None
+        elif p.variant == L.CCSC_L4D:
             U, V = p.views[0], p.views[1]
             d_res = np.zeros((p.psf, p.psf, U, V, p.K), order="F")
             z_res = np.zeros((X, Y, 1, 1, p.K, self.n_local), order="F") if want_z else None
@@ -243,9 +266,11 @@ class Session:
         }
         nd = np.zeros(cap, dtype=np.int32)
         nz = np.zeros(cap, dtype=np.int32)
+        fl = np.zeros(cap, dtype=np.int32)
         lg = L.IterLog(cap, 0, L.dptr(a["obj_vals_d"]), L.dptr(a["obj_vals_z"]),
                        L.dptr(a["tim_vals"]), L.dptr(tr["obj_d"]), L.dptr(tr["obj_z"]),
-                       L.dptr(tr["d_diff"]), L.dptr(tr["z_diff"]), L.iptr(nd), L.iptr(nz))
+                       L.dptr(tr["d_diff"]), L.dptr(tr["z_diff"]), L.iptr(nd), L.iptr(nz),
+                       L.iptr(fl))
         eb = L.errbuf()
         L.check(L.lib().ccsc_session_iterlog(self.ptr, C.byref(lg), eb, len(eb)), eb)
         cnt = lg.count
@@ -258,6 +283,7 @@ class Session:
             "z_diff": tr["z_diff"][: nout * p.max_it_z].reshape(nout, p.max_it_z),
             "n_d": nd[:nout].copy(),
             "n_z": nz[:nout].copy(),
+            "flags": fl[:nout].copy(),
         }
         return it
 
@@ -404,6 +430,57 @@ def admm_learn_conv3D_large(b, kernel_size, lambda_residual, lambda_prior, max_i
     iterations = {"obj_vals_d": [], "obj_vals_z": [], "tim_vals": [], "it_vals": [],
                   "trace": log["trace"], "engine_tim_vals": log["tim_vals"]}
     return d_res, z_res, DZ, obj, iterations
+
+
+def admm_learn(b, kernel_size, lambda_residual, lambda_prior, max_it, tol, verbose, init=None,
+               smooth_init=None, ctx=None, device=0, want_z=True, want_DZ=True, return_log=False,
+               **kw):
+    """Drop-in for 2-3D/DictionaryLearning/admm_learn.m:1-237 (hyperspectral learner).
+
+    b, smooth_init: [x, y, W, n] (learn_hyperspectral.m:16-17 passes the 13x13 Gaussian
+    low-pass of b); kernel_size = [psf, psf, W, K].  ``init = {'d': [psf,psf,K],
+    'z': [X,Y,K,n]}`` (the reference's own draw: one filter replicated over W, L23:54-56;
+    its init branch, L23:50-52, cannot run).  Returns (d_res [psf,psf,W,K], z_res [X,Y,K,n],
+    Dz [X,Y,W,n] incl. smoothinit, obj_val) like the reference; ``return_log=True`` appends
+    the engine's log (per-iteration objectives, 'rolled_back' for L23:204-213).
+    """
+    b = np.asarray(b, dtype=np.float64)
+    if b.ndim == 3:
+        b = b[..., None]
+    if b.ndim != 4:
+        raise ValueError("b must be [x, y, W, n]")
+    if len(kernel_size) != 4 or int(kernel_size[2]) != b.shape[2]:
+        raise ValueError("kernel_size must be [psf, psf, W, K] with W = size(b, 3)")
+    if smooth_init is None:
+        raise ValueError("smooth_init is required (admm_learn.m:4)")
+    sm = np.asarray(smooth_init, dtype=np.float64).reshape(b.shape, order="F")
+    own = ctx is None
+    if own:
+        ctx = Context(device)
+    try:
+        p = make_problem(L.CCSC_HS23, b.shape, kernel_size, lambda_residual, lambda_prior,
+                         max_it, tol, verbose, **kw)
+        d0 = z0 = None
+        if init is not None and len(init) > 0:
+            d0 = init.get("d")
+            z0 = init.get("z")
+        s = Session(ctx, p, b, d0, z0, smooth_init=sm)
+        try:
+            done = False
+            while s.outer < s.p.max_it and not done:
+                done = s.step(1)
+            d_res, z_res, DZ, obj = s.results(want_z=want_z, want_DZ=want_DZ, want_obj=True)
+            log = s.iterlog()
+        finally:
+            s.close()
+    finally:
+        if own:
+            ctx.close()
+    if not return_log:
+        return d_res, z_res, DZ, obj
+    log["rolled_back"] = bool(np.any(log["trace"]["flags"] & 1))
+    log["outer"] = len(log["trace"]["flags"])
+    return d_res, z_res, DZ, obj, log
 
 
 def fft2d_test(ctx: Context, slices):

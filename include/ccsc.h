@@ -7,6 +7,7 @@
  *   admm_learn_conv2D_large_dzParallel  2D/admm_learn_conv2D_large_dzParallel.m:1-4
  *   admm_learn_conv3D_large             3D/admm_learn_conv3D_large.m:1-4
  *   admm_learn_conv4D_lightfield        4D/admm_learn_conv4D_lightfield.m:1-4
+ *   admm_learn (2-3D hyperspectral)     2-3D/DictionaryLearning/admm_learn.m:1-4
  *
  * Each MATLAB function above becomes a thin .m wrapper over a MEX gateway that
  * calls ccsc_learn(); the Python mirror in
@@ -40,7 +41,7 @@
 extern "C" {
 #endif
 
-#define CCSC_ABI_VERSION 1
+#define CCSC_ABI_VERSION 2
 
 /* status codes */
 #define CCSC_OK 0
@@ -56,6 +57,7 @@ extern "C" {
 #define CCSC_DZPAR 1 /* 2D dzParallel  dZ:1-206  */
 #define CCSC_L3D 2   /* 3D             L3:1-230  */
 #define CCSC_L4D 3   /* 4D light field L4:1-212  */
+#define CCSC_HS23 4  /* 2-3D hyperspectral admm_learn L23:1-237 (ccsc_learn_hs23)  */
 
 /* verbose: which objectives the reference evaluates (dP:50-60,126,161) */
 #define CCSC_VERBOSE_NONE 0
@@ -66,10 +68,11 @@ extern "C" {
 #define CCSC_FP32 1
 
 typedef struct ccsc_problem {
-  int32_t variant;          /* CCSC_DPAR .. CCSC_L4D                                */
+  int32_t variant;          /* CCSC_DPAR .. CCSC_HS23                               */
   int32_t ndim;             /* spatial dims of b: 2 (2D, 4D) or 3 (3D)              */
   int64_t sb[3];            /* spatial size of b: x, y (, t for 3D)                 */
-  int32_t views[2];         /* 4D: U, V (angular views; kernel_size(3:4)); else 1,1 */
+  int32_t views[2];         /* 4D: U, V (angular views; kernel_size(3:4));
+                               2-3D: W, 1 (wavelengths, kernel_size(3)); else 1,1      */
   int64_t n;                /* number of patches (size(b, end))                     */
   int32_t K;                /* number of filters (kernel_size(end))                 */
   int32_t psf;              /* psf_s = kernel_size(1), odd                          */
@@ -111,6 +114,8 @@ typedef struct ccsc_iterlog {
   double* trace_z_diff;  /* ||z - z_old|| / ||z|| per z-iteration (tol > 0)             */
   int32_t* n_d;          /* d-iterations run per outer iteration                        */
   int32_t* n_z;          /* z-iterations run per outer iteration                        */
+  int32_t* flags;        /* per outer iteration, bit 0: the 2-3D learner rolled back to
+                            the previous iterate and stopped (L23:204-213); nullable      */
 } ccsc_iterlog;
 
 /* Progress callback, on the calling thread after each outer iteration. */
@@ -161,9 +166,27 @@ int32_t ccsc_learn(ccsc_ctx* ctx, const ccsc_problem* p, const double* b, const 
                    const double* z0, ccsc_outputs* out, ccsc_iterlog* log, ccsc_cb cb,
                    void* user, char* err, size_t errlen);
 
+/* 2-3D hyperspectral learner, the drop-in for admm_learn(b, kernel_size, lambda_residual,
+ * lambda, max_it, tol, verbose, init, smooth_init) (2-3D/DictionaryLearning/admm_learn.m:1-4,
+ * called by learn_hyperspectral.m:30).  p->variant = CCSC_HS23, p->views[0] = W.
+ * b, smooth_init: [x, y, W, n] (smooth_init = the caller's low-pass of b,
+ * learn_hyperspectral.m:16-17).  d0: [psf, psf, K], replicated over the W wavelengths
+ * (L23:54-56), or NULL; z0: [X, Y, K, n] or NULL (device RNG from p->seed).
+ * Outputs: d_res [psf,psf,W,K]; z_res [X,Y,K,n]; DZ [X,Y,W,n] = Dz incl. smoothinit,
+ * uncropped (L23:234-235); obj_val = the last objective evaluated (L23:195 / :211).
+ * One rank only (its d-solve couples every image per frequency). */
+int32_t ccsc_learn_hs23(ccsc_ctx* ctx, const ccsc_problem* p, const double* b,
+                        const double* smooth_init, const double* d0, const double* z0,
+                        ccsc_outputs* out, ccsc_iterlog* log, ccsc_cb cb, void* user, char* err,
+                        size_t errlen);
+
 /* ---- stateful session (bench / warm restart) ---------------------------- */
 ccsc_session* ccsc_session_create(ccsc_ctx* ctx, const ccsc_problem* p, const double* b,
                                   const double* d0, const double* z0, char* err, size_t errlen);
+/* The 2-3D learner's session (arguments as ccsc_learn_hs23). */
+ccsc_session* ccsc_session_create_hs23(ccsc_ctx* ctx, const ccsc_problem* p, const double* b,
+                                       const double* smooth_init, const double* d0,
+                                       const double* z0, char* err, size_t errlen);
 /* Run `n_outer` outer iterations (tol tests honoured); returns when the device is
  * idle.  *done = 1 when the tol test ended the learning early. */
 int32_t ccsc_session_step(ccsc_session* s, int32_t n_outer, int32_t* done, char* err,

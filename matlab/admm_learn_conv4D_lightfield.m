@@ -1,0 +1,17 @@
+function [ d_res, z_res, DZ, obj_val, iterations ] = admm_learn_conv4D_lightfield(b, kernel_size, ...
+                    lambda_residual, lambda_prior, max_it, tol, verbose, init)
+% Drop-in for 4D/admm_learn_conv4D_lightfield.m (same signature) on an MI355X.
+% b: [x, y, U, V, n] (single in the reference driver: widened to double here);
+% kernel_size = [s, s, U, V, K].  z_res is returned complex like the reference
+% (L4:164); its imaginary part is round-off there and zero here (Q8).
+    b = double(b);
+    r = floor(kernel_size(1) / 2);
+    sb = size(b);
+    if numel(sb) < 5, sb(5) = 1; end
+    size_z = [sb(1:2) + 2 * r, 1, 1, kernel_size(end), sb(5)];
+    if ~isempty(init) && isfield(init, 'd'), d0 = init.d; else, d0 = randn(kernel_size); end
+    if ~isempty(init) && isfield(init, 'z'), z0 = real(init.z); else, z0 = randn(size_z); end
+    [d_res, z_res, DZ, obj_val, iterations] = ccsc_mex(3, b, kernel_size, lambda_residual, ...
+        lambda_prior, max_it, tol, verbose, d0, z0, ccsc_device());
+    z_res = complex(z_res);
+end

@@ -7,7 +7,13 @@
  * Called by the .m wrappers in this directory, which keep the reference
  * signatures (2D/admm_learn_conv2D_large_dParallel.m:1-4 etc.):
  *   [d_res, z_res, DZ, obj_val, iter] = ccsc_mex(variant, b, kernel_size,
- *        lambda_residual, lambda_prior, max_it, tol, verbose, d0, z0, device)
+ *        lambda_residual, lambda_prior, max_it, tol, verbose, d0, z0, device
+ *        [, smooth_init])                      (smooth_init: 2-3D learner only)
+ * Output shapes per variant (what the library writes, include/ccsc.h):
+ *   dP / dZ  d_res [s,s,K]      z_res [X,Y,K,n]      DZ [X,Y,1,n]
+ *   3D       d_res [s,s,s,K]    z_res [X,Y,T,K,n]    DZ [X,Y,T,n]
+ *   4D       d_res [s,s,U,V,K]  z_res [X,Y,1,1,K,n]  DZ [x,y,U,V,n] (cropped, L4:205-206)
+ *   2-3D     d_res [s,s,W,K]    z_res [X,Y,K,n]      DZ [X,Y,W,n]   (incl. smoothinit)
  */
 #include "mex.h"
 #include "ccsc.h"
@@ -28,9 +34,13 @@ static void progress(void* user, int32_t it, double od, double oz, double t) {
   mexEvalString("drawnow;");
 }
 
+static mxArray* zeros_nd(mwSize nd, const mwSize* d) {
+  return mxCreateNumericArray(nd, d, mxDOUBLE_CLASS, mxREAL);
+}
+
 void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
   char err[1024] = {0};
-  if (nrhs < 11) mexErrMsgIdAndTxt("ccsc:args", "ccsc_mex needs 11 arguments");
+  if (nrhs < 11) mexErrMsgIdAndTxt("ccsc:args", "ccsc_mex needs 11 arguments (12 for 2-3D)");
   const int variant = (int)mxGetScalar(prhs[0]);
   const mxArray* b = prhs[1];
   if (!mxIsDouble(b) || mxIsComplex(b)) mexErrMsgIdAndTxt("ccsc:b", "b must be real double");
@@ -45,8 +55,11 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
   p.ndim = (variant == CCSC_L3D) ? 3 : 2;
   for (int i = 0; i < p.ndim; ++i) p.sb[i] = (int64_t)bd[i];
   p.views[0] = p.views[1] = 1;
-  if (variant == CCSC_L4D) { p.views[0] = (int32_t)ks[2]; p.views[1] = (int32_t)ks[3]; }
-  p.n = (int64_t)(bn > (mwSize)p.ndim ? bd[bn - 1] : 1);
+  if (variant == CCSC_L4D && nks == 5) { p.views[0] = (int32_t)ks[2]; p.views[1] = (int32_t)ks[3]; }
+  if (variant == CCSC_HS23 && nks == 4) p.views[0] = (int32_t)ks[2];
+  /* n = size(b, end): b is [sb..., (U,V | W), n] */
+  const mwSize lead = (mwSize)p.ndim + (variant == CCSC_L4D ? 2 : variant == CCSC_HS23 ? 1 : 0);
+  p.n = (int64_t)(bn > lead ? bd[bn - 1] : 1);
   p.K = (int32_t)ks[nks - 1];
   p.psf = (int32_t)ks[0];
   p.lambda_residual = mxGetScalar(prhs[3]);
@@ -62,6 +75,13 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
   p.precision = CCSC_FP64;
   if (ccsc_resolve(&p, err, sizeof err)) mexErrMsgIdAndTxt("ccsc:invalid", "%s", err);
 
+  const double* smooth = NULL;
+  if (variant == CCSC_HS23) {
+    if (nrhs < 12 || mxGetNumberOfElements(prhs[11]) != mxGetNumberOfElements(b))
+      mexErrMsgIdAndTxt("ccsc:args", "the 2-3D learner needs smooth_init of size(b)");
+    smooth = mxGetDoubles(prhs[11]);
+  }
+
   const int dev = (int)mxGetScalar(prhs[10]);
   if (!g_ctx || g_dev != dev) {
     cleanup();
@@ -75,20 +95,43 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
 
   /* outputs: allocate only what nargout asks for (z_res is ~97 GB at C2) */
   const int64_t r = p.psf / 2;
+  const mwSize s = (mwSize)p.psf, K = (mwSize)p.K, n = (mwSize)p.n;
   const mwSize X = (mwSize)(p.sb[0] + 2 * r), Y = (mwSize)(p.sb[1] + 2 * r);
+  const mwSize T = (mwSize)(p.ndim == 3 ? p.sb[2] + 2 * r : 1);
+  const mwSize U = (mwSize)p.views[0], V = (mwSize)p.views[1];
+  mwSize dd[5], zd[6], xd[5];
+  mwSize ndd, nzd, nxd;
+  switch (variant) {
+    case CCSC_L3D:
+      ndd = 4; dd[0] = s; dd[1] = s; dd[2] = s; dd[3] = K;
+      nzd = 5; zd[0] = X; zd[1] = Y; zd[2] = T; zd[3] = K; zd[4] = n;
+      nxd = 4; xd[0] = X; xd[1] = Y; xd[2] = T; xd[3] = n;
+      break;
+    case CCSC_L4D:
+      ndd = 5; dd[0] = s; dd[1] = s; dd[2] = U; dd[3] = V; dd[4] = K;
+      nzd = 6; zd[0] = X; zd[1] = Y; zd[2] = 1; zd[3] = 1; zd[4] = K; zd[5] = n;
+      nxd = 5; xd[0] = (mwSize)p.sb[0]; xd[1] = (mwSize)p.sb[1]; xd[2] = U; xd[3] = V; xd[4] = n;
+      break;
+    case CCSC_HS23:
+      ndd = 4; dd[0] = s; dd[1] = s; dd[2] = U; dd[3] = K;
+      nzd = 4; zd[0] = X; zd[1] = Y; zd[2] = K; zd[3] = n;
+      nxd = 4; xd[0] = X; xd[1] = Y; xd[2] = U; xd[3] = n;
+      break;
+    default:
+      ndd = 3; dd[0] = s; dd[1] = s; dd[2] = K;
+      nzd = 4; zd[0] = X; zd[1] = Y; zd[2] = K; zd[3] = n;
+      nxd = 4; xd[0] = X; xd[1] = Y; xd[2] = 1; xd[3] = n;
+  }
   ccsc_outputs out;
   memset(&out, 0, sizeof out);
-  mwSize dd[5] = {(mwSize)p.psf, (mwSize)p.psf, (mwSize)p.K, 1, 1};
-  plhs[0] = mxCreateNumericArray(3, dd, mxDOUBLE_CLASS, mxREAL);
+  plhs[0] = zeros_nd(ndd, dd);
   out.d_res = mxGetDoubles(plhs[0]);
   if (nlhs > 1) {
-    mwSize zd[4] = {X, Y, (mwSize)p.K, (mwSize)p.n};
-    plhs[1] = mxCreateNumericArray(4, zd, mxDOUBLE_CLASS, mxREAL);
+    plhs[1] = zeros_nd(nzd, zd);
     out.z_res = mxGetDoubles(plhs[1]);
   }
   if (nlhs > 2) {
-    mwSize zd[4] = {X, Y, 1, (mwSize)p.n};
-    plhs[2] = mxCreateNumericArray(4, zd, mxDOUBLE_CLASS, mxREAL);
+    plhs[2] = zeros_nd(nxd, xd);
     out.DZ = mxGetDoubles(plhs[2]);
   }
   double obj = 0;
@@ -105,9 +148,12 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
   lg.obj_vals_z = mxGetDoubles(oz);
   lg.tim_vals = mxGetDoubles(tv);
 
-  const int rc = ccsc_learn(g_ctx, &p, mxGetDoubles(b), d0, z0, &out, &lg,
-                            p.verbose == CCSC_VERBOSE_NONE ? NULL : progress, NULL, err,
-                            sizeof err);
+  ccsc_cb cb = p.verbose == CCSC_VERBOSE_NONE ? NULL : progress;
+  const int rc = variant == CCSC_HS23
+                     ? ccsc_learn_hs23(g_ctx, &p, mxGetDoubles(b), smooth, d0, z0, &out, &lg, cb,
+                                       NULL, err, sizeof err)
+                     : ccsc_learn(g_ctx, &p, mxGetDoubles(b), d0, z0, &out, &lg, cb, NULL, err,
+                                  sizeof err);
   if (rc) mexErrMsgIdAndTxt("ccsc:learn", "%s (code %d)", err, rc);
   mxSetN(od, lg.count);
   mxSetN(oz, lg.count);

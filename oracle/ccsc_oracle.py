@@ -29,6 +29,7 @@ and MATLAB axis meaning; ``np.reshape(..., order='F')`` restates MATLAB
   dZ  = 2D/admm_learn_conv2D_large_dzParallel.m
   L3  = 3D/admm_learn_conv3D_large.m
   L4  = 4D/admm_learn_conv4D_lightfield.m
+  L23 = 2-3D/DictionaryLearning/admm_learn.m
 
 Deviations (all documented in DESIGN.md):
   * ``init`` is honoured (the reference ignores it, Q11) so runs are
@@ -57,6 +58,12 @@ __all__ = [
     "learn_2d_dzparallel",
     "learn_3d",
     "learn_4d",
+    "learn_hs23",
+    "solve_conv_term_D_hs",
+    "solve_conv_term_Z_hs",
+    "objective_hs",
+    "prox_data_masked",
+    "pad_symmetric_2d",
     "embed_filters",
     "crop_filters",
 ]
@@ -665,3 +672,176 @@ def learn_4d(b, kernel_size, lambda_residual, lambda_prior, max_it, tol, verbose
     obj_val = objective(z, D_hat[0])                              # L4:211
     iterations = {"obj_vals_d": [], "obj_vals_z": [], "tim_vals": [], "it_vals": []}
     return d_res, z, DZ, obj_val, iterations, trace
+
+
+# ----------------------------------------------------------------------------
+# 2-3D hyperspectral   (L23 = 2-3D/DictionaryLearning/admm_learn.m:1-343)
+# ----------------------------------------------------------------------------
+def pad_symmetric_2d(a, r):
+    """padarray(a, [r, r, 0, 0], 'symmetric', 'both')   (L23:19)."""
+    pad = [(r, r), (r, r)] + [(0, 0)] * (a.ndim - 2)
+    return np.pad(a, pad, mode="symmetric")
+
+
+def prox_data_masked(u, theta, M, Mtb):
+    """ProxDataMasked = @(u, theta) (Mtb + 1/theta*u) ./ (M + 1/theta*ones)   (L23:26)."""
+    return (Mtb + (1.0 / theta) * u) / (M + (1.0 / theta) * np.ones(u.shape))
+
+
+def solve_conv_term_D_hs(z_hat, xi_hat1, xi_hat2, rho):
+    """L23:273-300.  Per spatial frequency i: opt = 1/rho*I - 1/rho*Z'*pinv(rho*I + Z*Z')*Z
+    (Z = zhat_mat{i}, n x k), then x = opt*(Z'*xi1(i,w,:) + rho*xi2(i,w,:)) for every
+    wavelength w.  z_hat [X, Y, 1, K, n]; xi_hat1 [X, Y, W, n]; xi_hat2 [X, Y, W, K]."""
+    X, Y, _, K, n = z_hat.shape
+    W = xi_hat1.shape[2]
+    ss = X * Y
+    zm = _F(z_hat, (ss, K, n)).transpose(0, 2, 1)       # zhat_mat{i} = [n, k]   (L23:285)
+    ZH = np.conj(zm.transpose(0, 2, 1))                  # [ss, k, n]
+    opt = (np.eye(K)[None] - ZH @ np.linalg.pinv(rho * np.eye(n)[None] + zm @ ZH) @ zm) / rho
+    x1 = _F(xi_hat1, (ss, W, n))                         # xi_hat_1_cell{ind}, ind = i + ss*(w-1)
+    x2 = _F(xi_hat2, (ss, W, K))
+    rhs = np.einsum("fkn,fwn->fwk", ZH, x1) + rho * x2   # L23:293
+    out = np.einsum("fkj,fwj->fwk", opt, rhs)
+    return _F(out, (X, Y, W, K))                          # L23:298
+
+
+def solve_conv_term_Z_hs(dhat, xi_hat1, xi_hat2, gamma_ratio, W):
+    """L23:302-324, the diagonal form (Q7): b = sum_w conj(dhat) .* xi1 + rho .* xi2,
+    x = 1/rho*b - 1/rho * 1/(rho + s) .* s .* b with s = sum_{w,k}|dhat|^2 and
+    rho = W * gamma_Z(2)/gamma_Z(1).  dhat [X, Y, W, K]; xi_hat1 [X, Y, W, n];
+    xi_hat2 [X, Y, K, n] -> z_hat [X, Y, K, n]."""
+    rho = W * gamma_ratio                                 # L23:311
+    s = np.sum(np.abs(dhat) ** 2, axis=(2, 3))            # sum(dhatTdhat, 2)   (L23:267, 317)
+    b = np.einsum("xywk,xywn->xykn", np.conj(dhat), xi_hat1) + rho * xi_hat2   # L23:314
+    sc = (1.0 / (rho + s))[:, :, None, None]
+    return b / rho - (1.0 / rho) * sc * s[:, :, None, None] * b                # L23:319
+
+
+def objective_hs(z, dhat, b, lambda_residual, lambda_prior, r, smoothinit):
+    """L23:326-343: z repeated over the W wavelengths (z2), Dz = ifft2(sum_k dhat .* fft2(z2))
+    + smoothinit; f = lambda_res/2 ||crop(Dz) - b||^2 + lambda * sum|z2| (= W sum|z|)."""
+    W = dhat.shape[2]
+    zh = np.fft.fft2(z, axes=(0, 1))                      # [X, Y, K, n]
+    Dz = np.real(np.fft.ifft2(np.einsum("xywk,xykn->xywn", dhat, zh), axes=(0, 1))) + smoothinit
+    X, Y = Dz.shape[:2]
+    f_z = lambda_residual * 0.5 * np.sum((Dz[r:X - r, r:Y - r] - b) ** 2)
+    g_z = lambda_prior * W * np.sum(np.abs(z))
+    return float(f_z + g_z)
+
+
+def learn_hs23(b, kernel_size, lambda_residual, lambda_prior, max_it, tol, verbose, init,
+               smooth_init, *, max_it_d=10, max_it_z=10):
+    """Restatement of admm_learn (2-3D/DictionaryLearning/admm_learn.m, "L23").
+
+    b, smooth_init: [x, y, W, n]; kernel_size = [s, s, W, K].  Non-consensus ADMM:
+    v1 = H x (masked data prox) and v2 = x (kernel constraint in the D-phase,
+    sparsity in the Z-phase).  ``init = {'d': [s, s, K], 'z': [X, Y, K, n]}``
+    follows the reference's own draw (L23:54-57: one [s, s, K] array replicated
+    over W, then z = randn(size_z), L23:69); the reference's init branch
+    (L23:50-52) leaves d empty and cannot run.  The objective is evaluated after
+    every inner iteration, as in the reference: it drives the rollback test
+    (L23:204-213, Q16).  ``verbose`` only prints in the reference.
+
+    Returns (d_res [s,s,W,K], z [X,Y,K,n], Dz [X,Y,W,n], obj_val, trace); trace
+    holds obj0, obj_d / obj_z per inner iteration, d_diff, z_diff, rolled_back.
+    """
+    b = np.asarray(b, dtype=np.float64)
+    smooth_init = np.asarray(smooth_init, dtype=np.float64)
+    psf_s = kernel_size[0]
+    k = kernel_size[3]                                            # L23:8
+    n = b.shape[3]
+    W = b.shape[2]
+    r = psf_s // 2                                                # L23:12
+    X, Y = b.shape[0] + 2 * r, b.shape[1] + 2 * r
+    size_x = [X, Y, W, n]                                         # L23:13
+    size_z = [X, Y, k, n]
+    size_k_full = [X, Y, W, k]
+    ax = (0, 1)
+
+    smoothinit = pad_symmetric_2d(smooth_init, r)                 # L23:19
+    M = np.pad(np.ones(b.shape), ((r, r), (r, r), (0, 0), (0, 0)))  # L23:255-258
+    Mtb = np.pad(b, ((r, r), (r, r), (0, 0), (0, 0))) * M - smoothinit * M
+
+    def objective(z_, dh):                                        # L23:22
+        return objective_hs(z_, dh, b, lambda_residual, lambda_prior, r, smoothinit)
+
+    lam = [lambda_residual, lambda_prior]                         # L23:35-38
+    gamma_h = 60.0 * lambda_prior / np.max(b)
+    gD = [gamma_h / 5000.0, gamma_h]
+    gZ = [gamma_h / 500.0, gamma_h]
+
+    d_D = [np.zeros(size_x), np.zeros(size_k_full)]               # L23:41-47
+    d0 = np.asarray(init["d"], dtype=np.float64)                  # [s, s, K]
+    d = embed_filters(d0, [X, Y], 2, r)                           # L23:54-55
+    d = np.repeat(d[:, :, None, :], W, axis=2)                    # L23:56 -> [X, Y, W, K]
+    d_hat = np.fft.fft2(d, axes=ax)                               # L23:57
+    d_Z = [np.zeros(size_x), np.zeros(size_z)]                    # L23:61-67
+    z = np.array(init["z"], dtype=np.float64).reshape(size_z, order="F")   # L23:69
+
+    obj_val = objective(z, d_hat)                                 # L23:72
+    trace = {"obj0": obj_val, "obj_d": [], "obj_z": [], "d_diff": [], "z_diff": [],
+             "rolled_back": False, "outer": 0}
+    obj_val_filter = obj_val_z = obj_val                          # L23:82-83
+    for i in range(max_it):                                       # L23:86
+        rho = gD[1] / gD[0]                                       # L23:93
+        obj_val_min = min(obj_val_filter, obj_val_z)              # L23:94
+        d_old = d
+        d_hat_old = d_hat
+        z_hat = np.fft.fft2(z, axes=ax)[:, :, None]               # L23:100 -> [X, Y, 1, K, n]
+        od = []
+        for i_d in range(max_it_d):                               # L23:102
+            v1 = np.real(np.fft.ifft2(np.einsum("xywk,xykn->xywn", d_hat, z_hat[:, :, 0]),
+                                      axes=ax))                   # L23:108
+            v2 = d                                                # L23:109
+            u1 = prox_data_masked(v1 - d_D[0], lam[0] / gD[0], M, Mtb)   # L23:112
+            u2 = kernel_constraint_proj(v2 - d_D[1], r, 2)        # L23:113 (per (w, k), L23:246)
+            d_D[0] = d_D[0] - (v1 - u1)                           # L23:117
+            d_D[1] = d_D[1] - (v2 - u2)
+            xi1 = np.fft.fft2(u1 + d_D[0], axes=ax)               # L23:120-121
+            xi2 = np.fft.fft2(u2 + d_D[1], axes=ax)
+            d_hat = solve_conv_term_D_hs(z_hat, xi1, xi2, rho)    # L23:125
+            d = np.real(np.fft.ifft2(d_hat, axes=ax))             # L23:126
+            obj_val = objective(z, d_hat)                         # L23:132
+            od.append(obj_val)
+        trace["obj_d"].append(od)
+        obj_val_filter = obj_val                                  # L23:139
+        d_diff = _rel(d - d_old, d)                               # L23:142-146
+        trace["d_diff"].append(d_diff)
+
+        z_hat = np.fft.fft2(z, axes=ax)                           # L23:158
+        z_old = z
+        z_hat_old = z_hat
+        oz = []
+        for i_z in range(max_it_z):                               # L23:165
+            v1 = np.real(np.fft.ifft2(np.einsum("xywk,xykn->xywn", d_hat, z_hat), axes=ax))  # L23:171
+            v2 = z
+            u1 = prox_data_masked(v1 - d_Z[0], lam[0] / gZ[0], M, Mtb)   # L23:175
+            u2 = prox_sparse(v2 - d_Z[1], lam[1] / gZ[1])         # L23:176
+            d_Z[0] = d_Z[0] - (v1 - u1)                           # L23:180
+            d_Z[1] = d_Z[1] - (v2 - u2)
+            xi1 = np.fft.fft2(u1 + d_Z[0], axes=ax)               # L23:183-184
+            xi2 = np.fft.fft2(u2 + d_Z[1], axes=ax)
+            z_hat = solve_conv_term_Z_hs(d_hat, xi1, xi2, gZ[1] / gZ[0], W)   # L23:188
+            z = np.real(np.fft.ifft2(z_hat, axes=ax))             # L23:189
+            obj_val = objective(z, d_hat)                         # L23:195
+            oz.append(obj_val)
+        trace["obj_z"].append(oz)
+        obj_val_z = obj_val                                       # L23:202
+        trace["outer"] = i + 1
+
+        if obj_val_min <= obj_val_filter and obj_val_min <= obj_val_z:   # L23:204-213 (Q16)
+            z = np.real(np.fft.ifft2(z_hat_old, axes=ax))
+            d_hat = d_hat_old
+            d = np.real(np.fft.ifft2(d_hat, axes=ax))
+            obj_val = objective(z, d_hat)
+            trace["rolled_back"] = True
+            break
+        z_diff = _rel(z - z_old, z)                               # L23:216-220
+        trace["z_diff"].append(z_diff)
+        if z_diff < tol and d_diff < tol:                         # L23:223
+            break
+
+    d_res = crop_filters(d, 2, r)                                 # L23:231-232
+    Dz = np.real(np.fft.ifft2(np.einsum("xywk,xykn->xywn", d_hat, np.fft.fft2(z, axes=ax)),
+                              axes=ax)) + smoothinit              # L23:234-235
+    return d_res, z, Dz, obj_val, trace

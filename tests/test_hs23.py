@@ -1,0 +1,204 @@
+"""2-3D hyperspectral learner (L23 = 2-3D/DictionaryLearning/admm_learn.m).
+
+CPU: pin the float64 restatement (oracle.learn_hs23) with known-answer tests of
+its pieces and regress it against the committed fixture tests/golden/hs_small.npz.
+GPU: the HIP engine through the C-ABI (ccsc_learn_hs23 / ccsc_session_create_hs23)
+against the oracle on the same inputs: objectives after every inner iteration to
+1e-9 relative, filters / codes / Dz to 1e-7, the rollback decision (L23:204-213)
+and the outer-iteration count identical.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+from scipy.signal import convolve2d
+
+from oracle import ccsc_oracle as O
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _rel(a, b):
+    a = np.asarray(a)
+    b = np.asarray(b)
+    return np.linalg.norm((a - b).ravel()) / max(np.linalg.norm(b.ravel()), 1e-300)
+
+
+def _case(sb, W, psf, K, n, seed):
+    rng = np.random.default_rng(seed)
+    r = psf // 2
+    X, Y = sb[0] + 2 * r, sb[1] + 2 * r
+    b = rng.random(sb + (W, n))
+    sm = 0.5 * rng.random(sb + (W, n))
+    init = {"d": rng.standard_normal((psf, psf, K)), "z": rng.standard_normal((X, Y, K, n))}
+    return b, sm, init
+
+
+# ---------------------------------------------------------------------------
+# oracle known-answer tests (CPU)
+# ---------------------------------------------------------------------------
+def test_pad_symmetric_is_matlab_symmetric():
+    """padarray(..., 'symmetric') mirrors including the edge sample (L23:19)."""
+    a = np.arange(1.0, 4.0)[:, None] * np.ones((1, 3))
+    p = O.pad_symmetric_2d(a[:, :, None, None], 2)[:, 1, 0, 0]
+    np.testing.assert_array_equal(p, [2, 1, 1, 2, 3, 3, 2])
+
+
+def test_prox_data_masked_is_the_masked_prox():
+    """ProxDataMasked (L23:26) minimises 1/2||M u - Mtb||^2 + 1/(2 theta)||u - a||^2
+    elementwise (M is 0/1): zero gradient inside, identity on the padding."""
+    rng = np.random.default_rng(1)
+    a = rng.standard_normal((6, 5))
+    M = np.zeros((6, 5))
+    M[1:5, 1:4] = 1
+    Mtb = M * rng.standard_normal((6, 5))
+    th = 0.37
+    u = O.prox_data_masked(a, th, M, Mtb)
+    grad = M * (M * u - Mtb) + (u - a) / th
+    assert np.abs(grad).max() < 1e-13
+    np.testing.assert_allclose(u[M == 0], a[M == 0], rtol=1e-15)
+
+
+def test_solve_D_hs_satisfies_normal_equations():
+    """solve_conv_term_D (L23:273-300): (Z'Z + rho I) x_w = Z' xi1_w + rho xi2_w per
+    spatial frequency and wavelength (the Woodbury/pinv form is the exact inverse)."""
+    rng = np.random.default_rng(2)
+    X, Y, W, K, n, rho = 5, 4, 3, 4, 2, 50.0
+    c = lambda *s: rng.standard_normal(s) + 1j * rng.standard_normal(s)
+    zh, x1, x2 = c(X, Y, 1, K, n), c(X, Y, W, n), c(X, Y, W, K)
+    x = O.solve_conv_term_D_hs(zh, x1, x2, rho)
+    for ix in range(X):
+        for iy in range(Y):
+            Z = zh[ix, iy, 0].T                       # n x K
+            G = Z.conj().T @ Z + rho * np.eye(K)
+            for w in range(W):
+                rhs = Z.conj().T @ x1[ix, iy, w] + rho * x2[ix, iy, w]
+                res = G @ x[ix, iy, w] - rhs
+                assert np.linalg.norm(res) <= 1e-12 * np.linalg.norm(rhs)
+
+
+def test_solve_Z_hs_is_the_diagonal_form():
+    """solve_conv_term_Z (L23:302-324, Q7): zhat = (sum_w conj(d) xi1 + rho xi2)/(rho + s),
+    rho = W * gamma ratio, s = sum over wavelengths AND atoms of |dhat|^2."""
+    rng = np.random.default_rng(3)
+    X, Y, W, K, n = 4, 3, 3, 2, 2
+    c = lambda *s: rng.standard_normal(s) + 1j * rng.standard_normal(s)
+    dh, x1, x2 = c(X, Y, W, K), c(X, Y, W, n), c(X, Y, K, n)
+    zh = O.solve_conv_term_Z_hs(dh, x1, x2, 500.0, W)
+    rho = 500.0 * W
+    for ix in range(X):
+        for iy in range(Y):
+            s = np.sum(np.abs(dh[ix, iy]) ** 2)
+            for k in range(K):
+                for p in range(n):
+                    bb = np.sum(np.conj(dh[ix, iy, :, k]) * x1[ix, iy, :, p]) + rho * x2[ix, iy, k, p]
+                    assert abs(zh[ix, iy, k, p] - bb / (rho + s)) <= 1e-12 * abs(bb)
+
+
+def test_objective_hs_equals_direct_convolution():
+    """objectiveFunction (L23:326-343): FFT data term == direct circular convolution per
+    wavelength, smoothinit added, l1 term counted W times."""
+    rng = np.random.default_rng(4)
+    sb, W, psf, K, n = (7, 6), 2, 3, 2, 2
+    r = psf // 2
+    X, Y = sb[0] + 2 * r, sb[1] + 2 * r
+    b = rng.standard_normal(sb + (W, n))
+    d = rng.standard_normal((psf, psf, W, K))
+    z = rng.standard_normal((X, Y, K, n))
+    sm = rng.standard_normal((X, Y, W, n))
+    D = O.embed_filters(d, [X, Y], 2, r)
+    f = O.objective_hs(z, np.fft.fft2(D, axes=(0, 1)), b, 1.0, 0.3, r, sm)
+    ref = 0.0
+    for p in range(n):
+        for w in range(W):
+            acc = sm[:, :, w, p].copy()
+            for k in range(K):
+                zz = np.pad(z[:, :, k, p], ((psf - 1, 0), (psf - 1, 0)), mode="wrap")
+                acc += np.roll(convolve2d(zz, d[:, :, w, k], mode="valid"), (-r, -r), axis=(0, 1))
+            ref += 0.5 * np.sum((acc[r:X - r, r:Y - r] - b[:, :, w, p]) ** 2)
+    ref += 0.3 * W * np.abs(z).sum()
+    assert abs(f - ref) <= 1e-10 * abs(ref)
+
+
+def test_hs_projection_is_per_wavelength_and_atom():
+    """KernelConstraintProj (L23:239-253) normalises every (w, k) 2D slice separately."""
+    rng = np.random.default_rng(5)
+    u = rng.standard_normal((9, 8, 3, 2)) * 3
+    u[:, :, 1, 0] *= 1e-3
+    p = O.kernel_constraint_proj(u, 1, 2)
+    nrm = np.sqrt((O.crop_filters(p, 2, 1) ** 2).sum(axis=(0, 1)))
+    expect = np.ones((3, 2))
+    expect[1, 0] = np.sqrt((O.crop_filters(u, 2, 1)[:, :, 1, 0] ** 2).sum())
+    np.testing.assert_allclose(nrm, expect, rtol=1e-12)
+
+
+def test_hs_rollback_and_descent():
+    """Q16: with a tiny lambda neither phase beats the previous objective at outer
+    iteration 2, so the learner restores that iterate and stops (L23:204-213); with
+    lambda = 1 every outer iteration lowers the objective."""
+    b, sm, init = _case((8, 7), 2, 3, 2, 2, seed=0)
+    d, z, Dz, obj, tr = O.learn_hs23(b, [3, 3, 2, 2], 1.0, 0.05, 30, 0.0, "none", init, sm)
+    assert tr["rolled_back"] and tr["outer"] == 2
+    assert obj == pytest.approx(tr["obj_z"][0][-1], rel=1e-12)   # back to the first iterate
+    b, sm, init = _case((10, 9), 3, 5, 4, 3, seed=1)
+    *_, tr = O.learn_hs23(b, [5, 5, 3, 4], 1.0, 1.0, 4, 0.0, "none", init, sm)
+    ends = [tr["obj0"]] + [o[-1] for o in tr["obj_z"]]
+    assert all(ends[i + 1] < ends[i] for i in range(len(ends) - 1))
+
+
+def test_hs_golden_fixture_regression():
+    g = np.load(os.path.join(GOLD, "hs_small.npz"), allow_pickle=False)
+    meta = json.loads(str(g["meta"]))
+    d, z, Dz, obj, tr = O.learn_hs23(g["b"], meta["kernel_size"], 1.0, meta["lambda"],
+                                     meta["max_it"], 0.0, "none", {"d": g["d0"], "z": g["z0"]},
+                                     g["smooth_init"])
+    np.testing.assert_allclose(d, g["d_res"], rtol=1e-10, atol=1e-12)
+    np.testing.assert_allclose(np.array(tr["obj_d"]), g["trace_obj_d"], rtol=1e-10)
+    np.testing.assert_allclose(np.array(tr["obj_z"]), g["trace_obj_z"], rtol=1e-10)
+    assert abs(obj - float(g["obj"])) <= 1e-10 * abs(float(g["obj"]))
+    assert abs(Dz.sum() - float(g["Dz_sum"])) <= 1e-8 * abs(float(g["Dz_sum"]))
+
+
+# ---------------------------------------------------------------------------
+# GPU parity (HIP engine through the C-ABI)
+# ---------------------------------------------------------------------------
+@pytest.mark.gpu
+@pytest.mark.parametrize("sb,W,psf,K,n,lam,max_it", [
+    ((10, 9), 3, 5, 4, 3, 1.0, 3),       # odd grid extents
+    ((8, 7), 2, 3, 2, 2, 0.05, 30),      # rollback at outer iteration 2 (Q16)
+    ((20, 20), 31, 11, 100, 2, 1.0, 1),  # C3's W = 31, K = 100, 11x11 filters
+    ((100, 100), 31, 11, 8, 2, 1.0, 1),  # C3's 110 x 110 grid
+])
+def test_learn_hs23_matches_oracle(gpu_ctx, sb, W, psf, K, n, lam, max_it):
+    from ccsc_code_iccv2017_amd import learners as E
+    b, sm, init = _case(sb, W, psf, K, n, seed=sb[0] + K)
+    ks = [psf, psf, W, K]
+    d_o, z_o, Dz_o, obj_o, tr_o = O.learn_hs23(b, ks, 1.0, lam, max_it, 0.0, "brief", init, sm)
+    d_e, z_e, Dz_e, obj_e, log = E.admm_learn(b, ks, 1.0, lam, max_it, 0.0, "brief", init, sm,
+                                              ctx=gpu_ctx, return_log=True)
+    assert d_e.shape == d_o.shape and z_e.shape == z_o.shape and Dz_e.shape == Dz_o.shape
+    assert log["outer"] == tr_o["outer"]
+    assert log["rolled_back"] == tr_o["rolled_back"]
+    tr = log["trace"]
+    for i in range(tr_o["outer"]):
+        np.testing.assert_allclose(tr["obj_d"][i], tr_o["obj_d"][i], rtol=1e-9)
+        np.testing.assert_allclose(tr["obj_z"][i], tr_o["obj_z"][i], rtol=1e-9)
+    assert _rel(d_e, d_o) < 1e-7
+    assert _rel(z_e, z_o) < 1e-7
+    assert _rel(Dz_e, Dz_o) < 1e-7
+    assert abs(obj_e - obj_o) <= 1e-9 * abs(obj_o)
+
+
+@pytest.mark.gpu
+def test_hs23_golden_fixture_on_gpu(gpu_ctx):
+    """The engine reproduces the committed oracle fixture (no oracle call)."""
+    from ccsc_code_iccv2017_amd import learners as E
+    g = np.load(os.path.join(GOLD, "hs_small.npz"), allow_pickle=False)
+    meta = json.loads(str(g["meta"]))
+    d, z, Dz, obj, log = E.admm_learn(g["b"], meta["kernel_size"], 1.0, meta["lambda"],
+                                      meta["max_it"], 0.0, "none", {"d": g["d0"], "z": g["z0"]},
+                                      g["smooth_init"], ctx=gpu_ctx, return_log=True)
+    assert _rel(d, g["d_res"]) < 1e-7
+    np.testing.assert_allclose(log["trace"]["obj_z"], g["trace_obj_z"], rtol=1e-9)
+    assert abs(obj - float(g["obj"])) <= 1e-9 * abs(float(g["obj"]))

@@ -40,6 +40,25 @@ def learner_fixture(name, variant, sb, psf, K, n, ni, max_it, seed):
                         DZ_sum=np.array(DZ.sum()), meta=np.array(json.dumps(meta)))
 
 
+def hs_fixture(name, sb, W, psf, K, n, lam, max_it, seed):
+    """2-3D learner (L23): inputs, final filters, per-iteration objectives, Dz checksum."""
+    rng = np.random.default_rng(seed)
+    r = psf // 2
+    X, Y = sb[0] + 2 * r, sb[1] + 2 * r
+    b = rng.random(sb + (W, n))
+    sm = 0.5 * rng.random(sb + (W, n))
+    d0 = rng.standard_normal((psf, psf, K))
+    z0 = rng.standard_normal((X, Y, K, n))
+    d, z, Dz, obj, tr = O.learn_hs23(b, [psf, psf, W, K], 1.0, lam, max_it, 0.0, "none",
+                                     {"d": d0, "z": z0}, sm)
+    meta = {"variant": "hs23", "kernel_size": [psf, psf, W, K], "lambda": lam,
+            "max_it": max_it, "generator": "tools/make_golden.py (oracle/ccsc_oracle.py, float64)"}
+    np.savez_compressed(os.path.join(GOLD, f"{name}.npz"), b=b, smooth_init=sm, d0=d0, z0=z0,
+                        d_res=d, trace_obj_d=np.array(tr["obj_d"]),
+                        trace_obj_z=np.array(tr["obj_z"]), obj=np.array(obj),
+                        Dz_sum=np.array(Dz.sum()), meta=np.array(json.dumps(meta)))
+
+
 def reference_norms():
     from scipy.io import loadmat
     out = {}
@@ -65,6 +84,7 @@ if __name__ == "__main__":
     learner_fixture("dz_small", "dz", (12, 12), 5, 3, 4, 2, 2, 102)
     learner_fixture("dp_odd", "dp", (11, 10), 5, 3, 6, 3, 2, 103)
     learner_fixture("dz_110", "dz", (100, 100), 11, 2, 2, 1, 1, 104)
+    hs_fixture("hs_small", (10, 9), 3, 5, 4, 3, 1.0, 2, 105)
     norms = reference_norms()
     if norms:
         json.dump(norms, open(os.path.join(GOLD, "reference_filter_norms.json"), "w"), indent=0)
