@@ -30,6 +30,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip table)
+ZKERNEL = "ccsc::k_zsplit"  # the dominant kernel (one z-iteration over the local patches)
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_zsplit.json")   # tools/pmc_summary.py --json
 
 
 def log(*a):
@@ -70,6 +72,22 @@ def cpu_baseline(args):
                   f"block of ni=100 synthetic 100x100 patches; oracle/ccsc_port.py float64, "
                   f"scipy.fft workers={cores}, host CPU '{cpu_model()}', {dt:.1f} s",
     }
+
+
+def pmc_traffic(n_local):
+    """HBM bytes per k_zsplit launch from the committed rocprofv3 PMC passes
+    (FETCH_SIZE doubled for 16-B streaming loads on gfx950 and WRITE_SIZE, both
+    kB per dispatch; MI355X_MICROARCH.md "HBM"), scaled to this run's patch count
+    when the profile was taken at another n.  None when no summary is committed."""
+    try:
+        d = json.load(open(PMC_SUMMARY))
+    except (OSError, ValueError):
+        return None, None
+    k = next((v for name, v in d.items() if name.startswith(ZKERNEL + "<")), None)
+    if not k or "FETCH_SIZE" not in k or "WRITE_SIZE" not in k:
+        return None, None
+    per = (2.0 * k["FETCH_SIZE"] + k["WRITE_SIZE"]) * 1024.0 * n_local / d.get("n_local", n_local)
+    return per, os.path.relpath(PMC_SUMMARY, ROOT)
 
 
 def main():
@@ -157,6 +175,7 @@ def main():
 
     avg_ms = zms / max(launches, 1)
     achieved = zbytes / (avg_ms * 1e-3) / 1e9 if launches else 0.0
+    traffic, traffic_src = pmc_traffic(n_local)
     result = {
         "metric": "ADMM outer iters/sec x patches (whole node)",
         "value": args.n * args.steps / dt,
@@ -180,12 +199,13 @@ def main():
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "k_zstep (fused prox/dual + R2C + Sherman-Morrison + C2R, one WG/patch)",
+            "kernel": "k_zsplit (C2R of the w term + prox/dual + R2C + per-bin reduction, one WG/patch)",
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
-            "traffic": None,
+            "traffic": traffic,
+            "traffic_source": traffic_src,
             "alg_bytes_per_launch": zbytes,
             "avg_launch_ms": avg_ms,
         },

@@ -95,8 +95,8 @@ typedef struct ccsc_problem {
 
 typedef struct ccsc_outputs {
   double* d_res; /* [psf,psf,(psf | U,V),K] cropped filters of block 1 (dP:195-196) */
-  double* z_res; /* this rank's codes: [X,Y,(T),K,n_local]; 4D: interleaved complex
-                    [X,Y,1,1,K,n_local] (L4:164, Q8 keeps it complex)                  */
+  double* z_res; /* this rank's codes: [X,Y,(T),K,n_local]; 4D: real part of the complex
+                    [X,Y,1,1,K,n_local] (L4:164; its imaginary part is round-off, Q8)  */
   double* DZ;    /* this rank's reconstruction (dP:193 uncropped; L4:205-206 cropped) */
   double* obj_val; /* scalar final objective (L3:229, L4:211)                           */
 } ccsc_outputs;

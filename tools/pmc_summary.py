@@ -25,6 +25,17 @@ def summarize(path, match=("ccsc::",)):
 
 
 if __name__ == "__main__":
-    for p in sys.argv[1:]:
+    args = sys.argv[1:]
+    if args and args[0] == "--json":
+        # --json OUT N_LOCAL csv...: one merged {kernel: {counter: mean per dispatch}} file
+        import json
+        out, n_local = args[1], int(args[2])
+        merged = {"n_local": n_local, "units": "FETCH_SIZE/WRITE_SIZE in kB per dispatch (raw)"}
+        for p in args[3:]:
+            for k, d in summarize(p).items():
+                merged.setdefault(k, {}).update(d)
+        json.dump(merged, open(out, "w"), indent=1)
+        sys.exit(0)
+    for p in args:
         for k, d in summarize(p).items():
             print(p.split("/")[-1], k, {a: f"{b:.4g}" for a, b in d.items()})

@@ -12,6 +12,7 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d $out/trace -o trace
 timeout -k 10 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -f csv -d $out/fetch -o fetch -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline > $out/fetch.log 2>&1 || exit $?
 timeout -k 10 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -f csv -d $out/write -o write -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline > $out/write.log 2>&1 || exit $?
 python3 tools/pmc_summary.py $out/fetch/fetch_counter_collection.csv $out/write/write_counter_collection.csv > $out/pmc_summary.txt
+python3 tools/pmc_summary.py --json $out/pmc_zsplit.json 10000 $out/fetch/fetch_counter_collection.csv $out/write/write_counter_collection.csv
 for f in $(find $out -name "*_kernel_trace.csv" -o -name "*_counter_collection.csv"); do
   grep -E "ccsc::|Kernel_Name" $f | gzip > $f.ccsc.gz; rm -f $f
 done
