@@ -19,6 +19,128 @@ constexpr int kGramPC = 16;  // patches staged in LDS per chunk
 
 __device__ __forceinline__ int pk_off(int j, int K) { return j * K - (j * (j - 1)) / 2; }
 
+// ---------------------------------------------------------------------------
+// Blocked right-looking Cholesky G = L L^H of the packed lower Hermitian G in LDS
+// (column-major, pk_off), in place, K <= 128, by one workgroup of kGramNT threads.
+// Panels of kCholNB columns are factored by wave 0 in registers (rows over the
+// lanes, pivot rows by shuffles: no workgroup barrier inside a panel); then every
+// wave applies the rank-kCholNB update to the trailing lower triangle with
+// kCholT x kCholT register tiles, one LDS read-modify-write per element per
+// panel.  Two barriers per panel instead of two per column: the column-by-column
+// form spent its time in LDS latency chains (measured 2.9 of 4.2 ms per block
+// launch at K = 100).
+// ---------------------------------------------------------------------------
+constexpr int kCholNB = 8;
+constexpr int kCholT = 4;
+
+template <typename T>
+__device__ __forceinline__ void chol_blocked(cpx<T>* sG, int K) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int j0 = 0; j0 < K; j0 += kCholNB) {
+    const int jb = min(kCholNB, K - j0);
+    if (wave == 0) {
+      cpx<T> P[2][kCholNB];  // rows r = j0 + lane + 64 t of the panel columns j0 .. j0+jb-1
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int r = j0 + lane + 64 * t;
+#pragma unroll
+        for (int c = 0; c < kCholNB; ++c) {
+          const int j = j0 + c;
+          P[t][c] = (c < jb && r < K && r >= j) ? sG[pk_off(j, K) + r - j] : cpx<T>{(T)0, (T)0};
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < kCholNB; ++c) {
+        if (c < jb) {
+          const int j = j0 + c;
+          const T djj = sqrt(__shfl(P[0][c].x, c, 64));  // row j sits in lane c
+          const T inv = (T)1 / djj;
+#pragma unroll
+          for (int t = 0; t < 2; ++t) {
+            const int r = j0 + lane + 64 * t;
+            if (r > j) P[t][c] = cscale(P[t][c], inv);
+            else if (r == j) P[t][c] = {djj, (T)0};
+          }
+          // G[r][j0+c2] -= G[r][j] conj(G[j0+c2][j]) inside the panel
+#pragma unroll
+          for (int c2 = c + 1; c2 < kCholNB; ++c2) {
+            if (c2 < jb) {
+              const cpx<T> g = {__shfl(P[0][c].x, c2, 64), __shfl(P[0][c].y, c2, 64)};
+#pragma unroll
+              for (int t = 0; t < 2; ++t) {
+                const int r = j0 + lane + 64 * t;
+                if (r >= j0 + c2) {
+                  P[t][c2].x -= P[t][c].x * g.x + P[t][c].y * g.y;
+                  P[t][c2].y -= P[t][c].y * g.x - P[t][c].x * g.y;
+                }
+              }
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int r = j0 + lane + 64 * t;
+#pragma unroll
+        for (int c = 0; c < kCholNB; ++c) {
+          const int j = j0 + c;
+          if (c < jb && r < K && r >= j) sG[pk_off(j, K) + r - j] = P[t][c];
+        }
+      }
+    }
+    __syncthreads();
+    // trailing update G[i][l] -= sum_c G[i][j0+c] conj(G[l][j0+c]),  b0 <= l <= i < K
+    const int b0 = j0 + jb;
+    const int mt = K - b0;
+    if (mt > 0) {
+      const int nt = (mt + kCholT - 1) / kCholT;
+      const int ntiles = nt * (nt + 1) / 2;
+      for (int q = tid; q < ntiles; q += kGramNT) {
+        int I = (int)((sqrt(8.0 * q + 1.0) - 1.0) * 0.5);
+        while ((I + 1) * (I + 2) / 2 <= q) ++I;
+        while (I * (I + 1) / 2 > q) --I;
+        const int J = q - I * (I + 1) / 2;
+        const int i0 = b0 + I * kCholT, l0 = b0 + J * kCholT;
+        cpx<T> acc[kCholT][kCholT];
+#pragma unroll
+        for (int a = 0; a < kCholT; ++a)
+#pragma unroll
+          for (int b = 0; b < kCholT; ++b) acc[a][b] = {(T)0, (T)0};
+        for (int c = 0; c < jb; ++c) {
+          const int j = j0 + c;
+          const cpx<T>* col = sG + pk_off(j, K) - j;   // col[r] = G[r][j]
+          cpx<T> ai[kCholT], bl[kCholT];
+#pragma unroll
+          for (int a = 0; a < kCholT; ++a) {
+            ai[a] = (i0 + a < K) ? col[i0 + a] : cpx<T>{(T)0, (T)0};
+            bl[a] = (l0 + a < K) ? col[l0 + a] : cpx<T>{(T)0, (T)0};
+          }
+#pragma unroll
+          for (int a = 0; a < kCholT; ++a)
+#pragma unroll
+            for (int b = 0; b < kCholT; ++b) {
+              acc[a][b].x += ai[a].x * bl[b].x + ai[a].y * bl[b].y;
+              acc[a][b].y += ai[a].y * bl[b].x - ai[a].x * bl[b].y;
+            }
+        }
+#pragma unroll
+        for (int b = 0; b < kCholT; ++b) {
+          const int l = l0 + b;
+          if (l < K) {
+            cpx<T>* cl = sG + pk_off(l, K) - l;
+#pragma unroll
+            for (int a = 0; a < kCholT; ++a) {
+              const int i = i0 + a;
+              if (i < K && i >= l) cl[i] = csub(cl[i], acc[a][b]);
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // one workgroup per frequency (XCD-aware: consecutive f share an XCD's L2)
 constexpr int kGramHPT = 8;  // (view, filter) right-hand-side entries per thread
 
@@ -59,6 +181,9 @@ __global__ __launch_bounds__(kGramNT) void k_gram_chol(const cpx<T>* __restrict_
   for (int i = 0; i < kGramHPT; ++i) hacc[i] = {(T)0, (T)0};
   const int KV = K * NV;
 
+#ifdef CCSC_ABL_NOGRAM
+  ni = 0;  // ablation build: skip the Gram accumulation (timing only)
+#endif
   for (int p0 = 0; p0 < ni; p0 += kGramPC) {
     const int pc = min(kGramPC, ni - p0);
     __syncthreads();
@@ -119,33 +244,9 @@ __global__ __launch_bounds__(kGramNT) void k_gram_chol(const cpx<T>* __restrict_
   }
   __syncthreads();
 
-  // right-looking Cholesky in LDS: G = L L^H
-  const int a0 = tid & 63, c0 = tid >> 6;  // 64 x 4 thread grid over the trailing block
-  for (int j = 0; j < K; ++j) {
-    const int oj = pk_off(j, K);
-    const T djj = sqrt(sG[oj].x);
-    const T inv = (T)1 / djj;
-    for (int i = j + 1 + tid; i < K; i += kGramNT) sG[oj + i - j] = cscale(sG[oj + i - j], inv);
-    __syncthreads();
-    if (tid == 0) sG[oj] = {djj, (T)0};
-    const int m = K - j - 1;
-    for (int c = c0; c < m; c += 4) {
-      const int l = j + 1 + c;
-      const cpx<T> glj = sG[oj + l - j];
-      const int ol = pk_off(l, K);
-      const int start = c + ((a0 - (c & 63)) & 63);
-      for (int a = start; a < m; a += 64) {
-        const int i = j + 1 + a;
-        const cpx<T> gij = sG[oj + i - j];
-        // G[i][l] -= G[i][j] * conj(G[l][j])
-        cpx<T> t = sG[ol + i - l];
-        t.x -= gij.x * glj.x + gij.y * glj.y;
-        t.y -= gij.y * glj.x - gij.x * glj.y;
-        sG[ol + i - l] = t;
-      }
-    }
-    __syncthreads();
-  }
+#ifndef CCSC_ABL_NOCHOL
+  chol_blocked(sG, K);
+#endif
   cpx<T>* Lf = L + (int64_t)f * Kp;
   for (int q = tid; q < Kp; q += kGramNT) Lf[q] = sG[q];
 }
@@ -156,6 +257,7 @@ hipError_t launch_gram_chol(const cpx<T>* Zh, const cpx<T>* Bh, cpx<T>* L, cpx<T
   const int Kt = (K + kGramTS - 1) / kGramTS;
   if (Kt * (Kt + 1) / 2 > kGramNT) return hipErrorInvalidValue;
   if (K * NV > kGramHPT * kGramNT) return hipErrorInvalidValue;
+  if (K > 128) return hipErrorInvalidValue;  // chol_blocked: two panel rows per lane
   const int Kp = K * (K + 1) / 2;
   size_t sm = (size_t)Kp * sizeof(cpx<T>);
   const size_t sm2 = (size_t)(kGramPC * K + kGramPC * NV) * sizeof(cpx<T>);

@@ -1,6 +1,9 @@
-# bench-only A/B (ablation builds fail parity by design): tools/ab_bench.sh v1 v2 ...
+# bench-only A/B (ablation builds fail parity by design): tools/ab_bench.sh dir v1 v2 ...
+# dir holds libccsc_<v>.so (push it un-ignored); n=1000 C2 slice, per-kernel times on stderr
 set -o pipefail
+d=$1; shift
+mkdir -p gpurun_out/ab
 for v in "$@"; do
-  cp variants/libccsc_$v.so ccsc_code_iccv2017_amd/libccsc.so
-  timeout -k 10 300 python bench.py --n 1000 --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/ab_b_$v.log 2>&1 || exit 1
+  cp $d/libccsc_$v.so ccsc_code_iccv2017_amd/libccsc.so
+  timeout -k 10 300 python bench.py --n 1000 --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/ab/$v.json 2> gpurun_out/ab/$v.err || exit 1
 done
