@@ -459,9 +459,10 @@ struct Session2D {
 
   DevBuf tw, bdev, Bhat, z, yz, cbuf, D, yD, Usup, ssum, supp, Ch, Dh, L, h, Zh, dhat, dtmp, sden,
       dnorm, znorm, part, pair, E;
-  // 2D z-phase state (zsplit.hip): zmode 0 = z materialised in `z`; zmode 1 =
-  // split, `z` holds u, W the last w and `dw` the filter spectrum w was solved
-  // with (dhat, or dhatw after the next z-prep replaced dhat).
+  // 2D z-phase state (zsplit.hip): zmode 0 = (z, y) materialised in `z`, `yz`;
+  // zmode 1 = `z` holds the pre-threshold state a = z + y, W the last w and `dw`
+  // the filter spectrum w was solved with (dhat, or dhatw after the next z-prep
+  // replaced dhat); `yz` is then stale until materialize_z().
   DevBuf W, dhatw;
   int zmode = 0;
   const cpx<double>* dw = nullptr;
@@ -746,7 +747,7 @@ struct Session2D {
                                       tol_on ? znorm.as<double>() : nullptr, 0, 1.0, r, np * K,
                                       Tn, twc, G, st));
     } else if (!tol_on) {
-      // one pass per patch over the split state (zsplit.hip)
+      // one pass per patch over the pre-threshold state a (zsplit.hip): `z` holds a
       HIPCHK(launch_zsplit<double>(z.as<double>(), z.as<double>(), yz.as<double>(),
                                    W.as<cpx<double>>(), Bhat.as<cpx<double>>(), dw,
                                    dhat.as<cpx<double>>(), sden.as<double>(), np, twc, G, K,
@@ -754,24 +755,24 @@ struct Session2D {
       zmode = 1;
       dw = dhat.as<cpx<double>>();
     } else {
-      // tol test (dP:156-157): u into cbuf so z_old stays in z, then z = u - y +
-      // ifft2(conj(d) w) with the per-slice change norms
+      // tol test (dP:156-157): a into cbuf so z_old stays in z, then (z, y) from a
+      // and ifft2(conj(d) w) with the per-slice change norms
       HIPCHK(launch_zsplit<double>(z.as<double>(), cbuf.as<double>(), yz.as<double>(),
                                    W.as<cpx<double>>(), Bhat.as<cpx<double>>(), dw,
                                    dhat.as<cpx<double>>(), sden.as<double>(), np, twc, G, K,
                                    theta, zmode, st));
       HIPCHK(launch_zmat<double>(cbuf.as<double>(), yz.as<double>(), W.as<cpx<double>>(),
                                  dhat.as<cpx<double>>(), z.as<double>(), z.as<double>(),
-                                 znorm.as<double>(), np, twc, G, K, st));
+                                 znorm.as<double>(), np, twc, G, K, theta, st));
       zmode = 0;
     }
   }
-  // split z-state -> z materialised in place (objective, outputs)
+  // state a -> (z, y) materialised in place (objective, outputs)
   void materialize_z() {
     if (zmode == 0) return;
     HIPCHK(launch_zmat<double>(z.as<double>(), yz.as<double>(), W.as<cpx<double>>(), dw,
                                z.as<double>(), nullptr, nullptr, np, tw.as<cpx<double>>(), G, K,
-                               st));
+                               theta, st));
     zmode = 0;
   }
 
@@ -848,12 +849,11 @@ struct Session2D {
 
     // ---- D precompute (dP:95-99) ----
     for (int64_t jl = 0; jl < nbl; ++jl) {
-      if (zmode)  // fft2(z) of the split state: fft2(u - y) + XY conj(dw) w
+      if (zmode)  // fft2(z) of the state a: fft2(u - y) + XY conj(dw) w, u = soft(a)
         HIPCHK(launch_zhat_split<double>(z.as<double>() + (size_t)jl * ni * K * P,
-                                         yz.as<double>() + (size_t)jl * ni * K * P,
                                          W.as<cpx<double>>() + (size_t)jl * ni * F, dw,
                                          Zh.as<cpx<double>>(), ni, tw.as<cpx<double>>(), G, K,
-                                         st));
+                                         theta, st));
       else
         fwd_embed(z.as<double>() + (size_t)jl * ni * K * P, G.X, G.Y, Tn, 0,
                   Zh.as<cpx<double>>(), (int64_t)ni * K);

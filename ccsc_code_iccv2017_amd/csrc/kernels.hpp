@@ -47,22 +47,23 @@ hipError_t launch_view_corr(const cpx<T>* dhat, const cpx<T>* Bhat, cpx<T>* E, i
 template <typename T>
 hipError_t launch_sum_pairs(const T* part, int count, T* out, hipStream_t st);
 
-// ---- zsplit.hip: the 2D learners' z-iteration on the split state ----------
-// (u, y) per slice + w per patch, z = u - y + ifft2(conj(dcorr) w); see zsplit.hip.
+// ---- zsplit.hip: the 2D learners' z-iteration on the pre-threshold state ----
+// a = z + y per slice + w per patch: u = soft(a), y = a - u, z = u - y +
+// ifft2(conj(dcorr) w); see zsplit.hip.
 size_t zsplit_smem_bytes(const Grid2D& G);
 template <typename T>
-hipError_t launch_zsplit(const T* U, T* Uo, T* Yz, cpx<T>* W, const cpx<T>* Bhat,
+hipError_t launch_zsplit(const T* A, T* Ao, const T* Yz, cpx<T>* W, const cpx<T>* Bhat,
                          const cpx<T>* dcorr, const cpx<T>* dhat, const T* sden, int64_t npatch,
                          const cpx<T>* tw, const Grid2D& G, int K, T theta, int mode,
                          hipStream_t st);
 template <typename T>
-hipError_t launch_zmat(const T* Us, const T* Yz, const cpx<T>* W, const cpx<T>* dcorr, T* Zd,
+hipError_t launch_zmat(const T* As, T* Yz, const cpx<T>* W, const cpx<T>* dcorr, T* Zd,
                        const T* zold, T* znorm, int64_t npatch, const cpx<T>* tw, const Grid2D& G,
-                       int K, hipStream_t st);
+                       int K, T theta, hipStream_t st);
 template <typename T>
-hipError_t launch_zhat_split(const T* U, const T* Yz, const cpx<T>* W, const cpx<T>* dcorr,
-                             cpx<T>* dst, int64_t npatch, const cpx<T>* tw, const Grid2D& G,
-                             int K, hipStream_t st);
+hipError_t launch_zhat_split(const T* A, const cpx<T>* W, const cpx<T>* dcorr, cpx<T>* dst,
+                             int64_t npatch, const cpx<T>* tw, const Grid2D& G, int K, T theta,
+                             hipStream_t st);
 
 // ---- dstep.hip ------------------------------------------------------------
 // Per frequency f of one block: G = A^H A + rho I (A = ni x K code spectra),

@@ -10,38 +10,29 @@
 // Closed form: z_k = c_k + ifft2(conj(d_k) w),
 //   w = (B - sum_k d_k C_k) / (rho + s),   c_k = u_k - y_k.
 //
-// The per-bin reduction over k makes a z-iteration need every filter slice of
-// a patch before any new z_k exists, which costs a fused kernel a second pass
-// over the patch (6 slice-sized HBM transfers per (patch, filter) instead of
-// the 4 of the state itself: read z, y; write z, y).  The engine therefore
-// keeps the z-phase state *split*: (u_k, y_k) per slice plus w per patch (1/K
-// of a slice), with
-//     z_k = u_k - y_k + ifft2(conj(dw_k) w)                        (*)
-// (dw = the filter spectrum w was solved with).  One z-iteration is then ONE
-// pass per patch, each slice read once and written once:
-//     z_k   <- (*)                       C2R of conj(dw_k) w, LDS-resident
-//     u, y  <- prox / dual of z_k        stored back over (u_k, y_k)
-//     C_k    = fft2(u - y)               R2C, LDS-resident
-//     acc   += d_k C_k                   registers + spare LDS
+// State.  The prox and the dual update are functions of the pre-threshold
+// value a = z + y alone (dP:150-151):
+//     u = soft(a, theta),   y_new = y + z - u = a - u   (= clip(a, -theta, theta)),
+// and the next iteration's pre-threshold value is
+//     a' = z' + y_new = (u - y_new + corr) + y_new = u + corr,   corr = ifft2(conj(dw_k) w)
+// (dw = the filter spectrum w was solved with).  So the z-phase state is ONE
+// array a per (patch, filter) slice plus w per patch (1/K of a slice): a
+// z-iteration streams 2 slice transfers (read a, write a') instead of the 4 of
+// (z, y), in one pass per patch:
+//     a  <- soft(a) + corr               C2R of conj(dw_k) w, LDS-resident
+//     u = soft(a), y = a - u, C_k = fft2(u - y)     R2C, LDS-resident
+//     acc += d_k C_k                     registers + spare LDS
 //   w <- (B - acc) / ((rho + s) X Y)     stored for the next iteration.
-// In exact arithmetic this is the reference's iteration; rounding matches the
-// two-pass form operation for operation ((u - y) + ifft2(...) is how z_k was
-// formed there too).  k_zmat materialises z (objective, outputs, tol tests);
-// k_zhat_split gives the D-precompute its fft2(z) from the split state.
+// In exact arithmetic this is the reference's iteration.  k_zmat materialises
+// z = u - y + corr and y (objective, outputs, tol tests); k_zhat_split gives
+// the D-precompute fft2(z) from the state.  Mode 0 (z, y materialised: session
+// start, after an objective) forms a = z + y on the fly.
 #include "fft_fixed.hpp"
 #include "slice.hpp"
 
 #include <type_traits>
 
 namespace ccsc {
-
-// element pairs per thread whose loads are issued before the C2R (the rest
-// after it): the prefetch hides HBM latency under the transform, bounded by
-// the 128-VGPR budget of a 1024-thread workgroup.
-#ifndef CCSC_ZS_PREFETCH
-#define CCSC_ZS_PREFETCH 4
-#endif
-constexpr int kZsPrefetch = CCSC_ZS_PREFETCH;
 
 // 16-B global access at a 32-bit byte offset from a uniform base: lowers to
 // the saddr form (SGPR base + one VGPR offset) instead of a 64-bit VGPR
@@ -55,21 +46,21 @@ __device__ __forceinline__ void st16(void* base, uint32_t boff, V v) {
   *reinterpret_cast<V*>(reinterpret_cast<char*>(base) + boff) = v;
 }
 
+// ProxSparse = max(0, 1 - theta/|a|) a  (dP:32); a = 0 -> 0
 template <typename T>
-__device__ __forceinline__ T soft_dual(T zv, T yv, T theta, T& yn) {
-  const T a = zv + yv;
+__device__ __forceinline__ T soft(T a, T theta) {
   const T aa = fabs(a);
-  const T u = ((aa > theta) ? (T)1 - theta / aa : (T)0) * a;  // max(0, 1-theta/|a|) a  (dP:32)
-  yn = a - u;                                                  // y + z - u  (dP:151)
-  return u;
+  return ((aa > theta) ? (T)1 - theta / aa : (T)0) * a;
 }
 
-// One workgroup (NT threads) per patch.  mode 0: U holds z (materialised
-// state); mode 1: U holds u and W the previous w (solved with dcorr).
-// Outputs: Uo <- u (Uo may alias U), Yz <- y, W <- w.  NBR + NBL accumulator
-// bins per thread (registers + spare LDS), NPR element pairs per thread.
+// One workgroup (NT threads) per patch.  mode 0: A holds z and Yz holds y
+// (materialised state); mode 1: A holds the previous pre-threshold state and
+// W the previous w (solved with dcorr).  Outputs: Ao <- a (may alias A),
+// W <- w.  NBR + NBL accumulator bins per thread (registers + spare LDS), NPR
+// element pairs per thread; the next slice's state is loaded while this
+// slice's R2C, accumulation and the next C2R run.
 template <typename T, int NBR, int NBL, class FG, int NT>
-__global__ __launch_bounds__(NT) void k_zsplit(const T* U, T* Uo, T* __restrict__ Yz,
+__global__ __launch_bounds__(NT) void k_zsplit(const T* A, T* Ao, const T* __restrict__ Yz,
                                                cpx<T>* __restrict__ W,
                                                const cpx<T>* __restrict__ Bhat,
                                                const cpx<T>* __restrict__ dcorr,
@@ -88,37 +79,30 @@ __global__ __launch_bounds__(NT) void k_zsplit(const T* U, T* Uo, T* __restrict_
   const int X = GO::X(Gd), Yd = GO::Y(Gd), RS = GO::RS(Gd), F = GO::F(Gd);
   const int P = X * Yd;
   const int P2 = P / 2;
+  const bool vec = (X & 1) == 0;  // element pairs never straddle a row: 16-B accesses
   BinAcc<T, NBR, NBL, NT> acc;
   acc.init(S.acc);
   cpx<T>* Wp = W + (int64_t)p * F;
+
+  V2 av[NPR];
+  auto load_state = [&](int k) {
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    const V2* A2 = reinterpret_cast<const V2*>(A + ((int64_t)p * K + k) * P);
+#pragma unroll
+    for (int i = 0; i < NPR; ++i) {
+      const int e2 = tid + i * NT;
+      if (e2 < P2) av[i] = ld16<V2>(A2, (uint32_t)e2 * 16u);
+    }
+  };
+  if (vec) load_state(0);
 
   for (int k = 0; k < K; ++k) {
     const int64_t off = ((int64_t)p * K + k) * P;
     int tid = threadIdx.x;
     asm volatile("" : "+v"(tid));  // per-thread index math stays inside the K loop (LICM)
-    const bool vec = (X & 1) == 0;  // element pairs never straddle a row: 16-B accesses
-    const V2* U2 = reinterpret_cast<const V2*>(U + off);
-    V2* Uo2 = reinterpret_cast<V2*>(Uo + off);
-    V2* Y2 = reinterpret_cast<V2*>(Yz + off);
-    V2 uv[NPR], yv[NPR];
-    if (vec) {
-      // first kZsPrefetch pairs: issued before the C2R so their latency hides under it
-#pragma unroll
-      for (int i = 0; i < kZsPrefetch && i < NPR; ++i) {
-        const int e2 = tid + i * NT;
-        if (e2 < P2) {
-#ifndef CCSC_ABL_NOMEM
-          uv[i] = ld16<V2>(U2, (uint32_t)e2 * 16u);
-          yv[i] = ld16<V2>(Y2, (uint32_t)e2 * 16u);
-#else
-          uv[i].x = uv[i].y = (T)e2;
-          yv[i].x = yv[i].y = (T)k;
-#endif
-        }
-      }
-    }
     lds_sync();  // previous slice's spectrum reads are done
-    if (mode) {  // LDS <- conj(dw_k) w, C2R: the ifft2 term of (*)
+    if (mode) {  // LDS <- conj(dw_k) w, C2R: the corr term
       const cpx<T>* dk = dcorr + (int64_t)k * F;
 #pragma unroll
       for (int i = 0; i < NB; ++i) {
@@ -128,25 +112,12 @@ __global__ __launch_bounds__(NT) void k_zsplit(const T* U, T* Uo, T* __restrict_
           lds_cpx_store(S.slice + y * RS + 2 * (f - y * GO::Xh(Gd)), 1, cmulc(dk[f], Wp[f]));
         }
       }
-#ifndef CCSC_ABL_NOFFT
       GO::c2r(S.slice, Gd, S.tw, tid);
-#endif
     }
     asm volatile("" : "+v"(tid));  // elementwise index math after the C2R, not live across it
     if (vec) {
-#pragma unroll
-      for (int i = kZsPrefetch; i < NPR; ++i) {
-        const int e2 = tid + i * NT;
-        if (e2 < P2) {
-#ifndef CCSC_ABL_NOMEM
-          uv[i] = ld16<V2>(U2, (uint32_t)e2 * 16u);
-          yv[i] = ld16<V2>(Y2, (uint32_t)e2 * 16u);
-#else
-          uv[i].x = uv[i].y = (T)e2;
-          yv[i].x = yv[i].y = (T)k;
-#endif
-        }
-      }
+      V2* Ao2 = reinterpret_cast<V2*>(Ao + off);
+      const V2* Y2 = reinterpret_cast<const V2*>(Yz + off);
 #pragma unroll
       for (int i = 0; i < NPR; ++i) {
         const int e2 = tid + i * NT;
@@ -154,46 +125,39 @@ __global__ __launch_bounds__(NT) void k_zsplit(const T* U, T* Uo, T* __restrict_
           const int e = 2 * e2;
           const int y = e / X;
           T* q = S.slice + y * RS + (e - y * X);
-          V2 zv = uv[i];
+          V2 a = av[i];
           if (mode) {
             const V2 c = *reinterpret_cast<const V2*>(q);
-            zv.x = (uv[i].x - yv[i].x) + c.x;
-            zv.y = (uv[i].y - yv[i].y) + c.y;
+            a.x = soft(a.x, theta) + c.x;
+            a.y = soft(a.y, theta) + c.y;
+          } else {
+            const V2 yv = ld16<V2>(Y2, (uint32_t)e2 * 16u);
+            a.x += yv.x;
+            a.y += yv.y;
           }
-          V2 un, yn, cn;
-          un.x = soft_dual(zv.x, yv[i].x, theta, yn.x);
-          un.y = soft_dual(zv.y, yv[i].y, theta, yn.y);
-          cn.x = un.x - yn.x;
-          cn.y = un.y - yn.y;
-#ifndef CCSC_ABL_NOMEM
-          st16<V2>(Uo2, (uint32_t)e2 * 16u, un);
-          st16<V2>(Y2, (uint32_t)e2 * 16u, yn);
-#else
-          if (un.x == (T)-1.2345) st16<V2>(Uo2, (uint32_t)e2 * 16u, un);
-#endif
+          st16<V2>(Ao2, (uint32_t)e2 * 16u, a);
+          const T ux = soft(a.x, theta), uy = soft(a.y, theta);
+          V2 cn;
+          cn.x = ux - (a.x - ux);   // u - y_new
+          cn.y = uy - (a.y - uy);
           *reinterpret_cast<V2*>(q) = cn;
         }
       }
+      if (k + 1 < K) load_state(k + 1);
     } else {
       // odd X (test grids only): scalar elements
       for (int e = tid; e < P; e += NT) {
         const int y = e / X, x = e - y * X;
-        const T uu = U[off + e], yy = Yz[off + e];
-        const T zv = mode ? (uu - yy) + S.slice[y * RS + x] : uu;
-        T yn;
-        const T un = soft_dual(zv, yy, theta, yn);
-        Uo[off + e] = un;
-        Yz[off + e] = yn;
-        S.slice[y * RS + x] = un - yn;
+        const T av0 = A[off + e];
+        const T a = mode ? soft(av0, theta) + S.slice[y * RS + x] : av0 + Yz[off + e];
+        Ao[off + e] = a;
+        const T u = soft(a, theta);
+        S.slice[y * RS + x] = u - (a - u);
       }
     }
     if (GO::Yp(Gd) != GO::Y(Gd))
       for (int x = tid; x < RS; x += NT) S.slice[Yd * RS + x] = (T)0;
-#ifndef CCSC_ABL_NOFFT
     GO::r2c(S.slice, Gd, S.tw, tid);
-#else
-    lds_sync();
-#endif
     const cpx<T>* dk = dhat + (int64_t)k * F;
     acc.each(F, [&](int f, cpx<T>& a) {
       const int y = f / GO::Xh(Gd);
@@ -208,16 +172,18 @@ __global__ __launch_bounds__(NT) void k_zsplit(const T* U, T* Uo, T* __restrict_
   acc.each(F, [&](int f, cpx<T>& a) { Wp[f] = cscale(csub(Bp[f], a), sden[f]); });
 }
 
-// Materialise z from the split state, one workgroup per (patch, filter) slice:
-//   Zd = Us - Yz + ifft2(conj(dcorr_k) w_p)          (*)
-// Zd may alias Us.  With zold != NULL also ||Zd - zold||^2, ||Zd||^2 per slice
-// (the tol test, dP:156-157; zold may alias Zd, read before written).
+// Materialise (z, y) from the state, one workgroup per (patch, filter) slice:
+//   u = soft(a), y = a - u, z = (u - y) + ifft2(conj(dcorr_k) w_p)
+// Zd may alias As (each element read, then written, by one thread).  With
+// zold != NULL also ||Zd - zold||^2, ||Zd||^2 per slice (the tol test,
+// dP:156-157; zold may alias Zd, read before written).
 template <typename T, class FG>
-__global__ __launch_bounds__(kNT) void k_zmat(const T* Us, const T* __restrict__ Yz,
+__global__ __launch_bounds__(kNT) void k_zmat(const T* As, T* __restrict__ Yz,
                                               const cpx<T>* __restrict__ W,
                                               const cpx<T>* __restrict__ dcorr, T* Zd,
                                               const T* zold, T* __restrict__ znorm,
-                                              const cpx<T>* __restrict__ twg, Grid2D Gd, int K) {
+                                              const cpx<T>* __restrict__ twg, Grid2D Gd, int K,
+                                              T theta) {
   using GO = GridOps<FG>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   Smem<T> S = carve<T>(smem, Gd);
@@ -239,12 +205,16 @@ __global__ __launch_bounds__(kNT) void k_zmat(const T* Us, const T* __restrict__
   T nd = 0, nz = 0;
   for (int e = tid; e < P; e += kNT) {
     const int y = e / X, x = e - y * X;
-    const T zn = (Us[off + e] - Yz[off + e]) + S.slice[y * RS + x];
+    const T a = As[off + e];
+    const T u = soft(a, theta);
+    const T yv = a - u;
+    const T zn = (u - yv) + S.slice[y * RS + x];
     if (zold) {
       const T zo = zold[off + e];
       nd += (zn - zo) * (zn - zo);
       nz += zn * zn;
     }
+    Yz[off + e] = yv;
     Zd[off + e] = zn;
   }
   if (zold) {
@@ -257,17 +227,16 @@ __global__ __launch_bounds__(kNT) void k_zmat(const T* Us, const T* __restrict__
   }
 }
 
-// fft2(z) from the split state for the D-precompute (dP:97 uses zhat), one
-// workgroup per slice: fft2(u - y) + X*Y conj(dcorr_k) w_p  (fft2 of (*)).
-// Slices s = 0..count-1 of patches starting at U/Yz/W (K slices per patch).
+// fft2(z) from the state for the D-precompute (dP:97 uses zhat), one
+// workgroup per slice: fft2(u - y) + X*Y conj(dcorr_k) w_p  with u = soft(a),
+// y = a - u.  Slices s = 0..count-1 of patches starting at A/W (K per patch).
 template <typename T, class FG>
-__global__ __launch_bounds__(kNT) void k_zhat_split(const T* __restrict__ U,
-                                                    const T* __restrict__ Yz,
+__global__ __launch_bounds__(kNT) void k_zhat_split(const T* __restrict__ A,
                                                     const cpx<T>* __restrict__ W,
                                                     const cpx<T>* __restrict__ dcorr,
                                                     cpx<T>* __restrict__ dst,
                                                     const cpx<T>* __restrict__ twg, Grid2D Gd,
-                                                    int K) {
+                                                    int K, T theta) {
   using GO = GridOps<FG>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   Smem<T> S = carve<T>(smem, Gd);
@@ -281,7 +250,9 @@ __global__ __launch_bounds__(kNT) void k_zhat_split(const T* __restrict__ U,
   const int64_t off = slice * P;
   for (int e = tid; e < P; e += kNT) {
     const int y = e / X, x = e - y * X;
-    S.slice[y * RS + x] = U[off + e] - Yz[off + e];
+    const T a = A[off + e];
+    const T u = soft(a, theta);
+    S.slice[y * RS + x] = u - (a - u);
   }
   if (GO::Yp(Gd) != Yd)
     for (int x = tid; x < RS; x += kNT) S.slice[Yd * RS + x] = (T)0;
@@ -303,9 +274,9 @@ __global__ __launch_bounds__(kNT) void k_zhat_split(const T* __restrict__ U,
 // runtime plan otherwise.
 // ---------------------------------------------------------------------------
 // Workgroup of the fixed-grid z-iteration: 12 waves (3 per SIMD) leave 168
-// VGPRs per lane for the transform, the accumulator bins and the prefetch
-// (16 waves cap a lane at 128 and spill); every FFT pass of the 110 grid has
-// <= 616 butterflies, so one butterfly per thread still covers a pass.
+// VGPRs per lane for the transform, the accumulator bins and the one-slice
+// state prefetch (16 waves cap a lane at 128 and spill); the wave-local line
+// transforms of the 110 grid need 11 (x) and 12 (y) waves.
 #ifndef CCSC_ZS_NT
 #define CCSC_ZS_NT 768
 #endif
@@ -324,7 +295,7 @@ size_t zsplit_smem_bytes(const Grid2D& G) {
 }
 
 template <typename T>
-hipError_t launch_zsplit(const T* U, T* Uo, T* Yz, cpx<T>* W, const cpx<T>* Bhat,
+hipError_t launch_zsplit(const T* U, T* Uo, const T* Yz, cpx<T>* W, const cpx<T>* Bhat,
                          const cpx<T>* dcorr, const cpx<T>* dhat, const T* sden, int64_t npatch,
                          const cpx<T>* tw, const Grid2D& G, int K, T theta, int mode,
                          hipStream_t st) {
@@ -346,48 +317,49 @@ hipError_t launch_zsplit(const T* U, T* Uo, T* Yz, cpx<T>* W, const cpx<T>* Bhat
 }
 
 template <typename T>
-hipError_t launch_zmat(const T* Us, const T* Yz, const cpx<T>* W, const cpx<T>* dcorr, T* Zd,
+hipError_t launch_zmat(const T* As, T* Yz, const cpx<T>* W, const cpx<T>* dcorr, T* Zd,
                        const T* zold, T* znorm, int64_t npatch, const cpx<T>* tw, const Grid2D& G,
-                       int K, hipStream_t st) {
+                       int K, T theta, hipStream_t st) {
   if (npatch <= 0) return hipSuccess;
   const dim3 grid((unsigned)(npatch * K));
   const size_t sm = slice_smem_bytes(G, sizeof(T));
   if (grid_is<Grid110>(G))
-    hipLaunchKernelGGL((k_zmat<T, Grid110>), grid, dim3(kNT), sm, st, Us, Yz, W, dcorr, Zd, zold,
-                       znorm, tw, G, K);
+    hipLaunchKernelGGL((k_zmat<T, Grid110>), grid, dim3(kNT), sm, st, As, Yz, W, dcorr, Zd, zold,
+                       znorm, tw, G, K, theta);
   else
-    hipLaunchKernelGGL((k_zmat<T, DynGrid>), grid, dim3(kNT), sm, st, Us, Yz, W, dcorr, Zd, zold,
-                       znorm, tw, G, K);
+    hipLaunchKernelGGL((k_zmat<T, DynGrid>), grid, dim3(kNT), sm, st, As, Yz, W, dcorr, Zd, zold,
+                       znorm, tw, G, K, theta);
   return hipGetLastError();
 }
 
 template <typename T>
-hipError_t launch_zhat_split(const T* U, const T* Yz, const cpx<T>* W, const cpx<T>* dcorr,
-                             cpx<T>* dst, int64_t npatch, const cpx<T>* tw, const Grid2D& G,
-                             int K, hipStream_t st) {
+hipError_t launch_zhat_split(const T* A, const cpx<T>* W, const cpx<T>* dcorr, cpx<T>* dst,
+                             int64_t npatch, const cpx<T>* tw, const Grid2D& G, int K, T theta,
+                             hipStream_t st) {
   if (npatch <= 0) return hipSuccess;
   const dim3 grid((unsigned)(npatch * K));
   const size_t sm = slice_smem_bytes(G, sizeof(T));
   if (grid_is<Grid110>(G))
-    hipLaunchKernelGGL((k_zhat_split<T, Grid110>), grid, dim3(kNT), sm, st, U, Yz, W, dcorr, dst,
-                       tw, G, K);
+    hipLaunchKernelGGL((k_zhat_split<T, Grid110>), grid, dim3(kNT), sm, st, A, W, dcorr, dst, tw,
+                       G, K, theta);
   else
-    hipLaunchKernelGGL((k_zhat_split<T, DynGrid>), grid, dim3(kNT), sm, st, U, Yz, W, dcorr, dst,
-                       tw, G, K);
+    hipLaunchKernelGGL((k_zhat_split<T, DynGrid>), grid, dim3(kNT), sm, st, A, W, dcorr, dst, tw,
+                       G, K, theta);
   return hipGetLastError();
 }
 
-template hipError_t launch_zsplit<double>(const double*, double*, double*, cpx<double>*,
+template hipError_t launch_zsplit<double>(const double*, double*, const double*, cpx<double>*,
                                           const cpx<double>*, const cpx<double>*,
                                           const cpx<double>*, const double*, int64_t,
                                           const cpx<double>*, const Grid2D&, int, double, int,
                                           hipStream_t);
-template hipError_t launch_zmat<double>(const double*, const double*, const cpx<double>*,
+template hipError_t launch_zmat<double>(const double*, double*, const cpx<double>*,
                                         const cpx<double>*, double*, const double*, double*,
-                                        int64_t, const cpx<double>*, const Grid2D&, int,
+                                        int64_t, const cpx<double>*, const Grid2D&, int, double,
                                         hipStream_t);
-template hipError_t launch_zhat_split<double>(const double*, const double*, const cpx<double>*,
+template hipError_t launch_zhat_split<double>(const double*, const cpx<double>*,
                                               const cpx<double>*, cpx<double>*, int64_t,
-                                              const cpx<double>*, const Grid2D&, int, hipStream_t);
+                                              const cpx<double>*, const Grid2D&, int, double,
+                                              hipStream_t);
 
 }  // namespace ccsc
