@@ -70,20 +70,21 @@ struct BinAcc {
 #pragma unroll
     for (int i = 0; i < NBL; ++i) l[i * NT] = {(T)0, (T)0};
   }
-  // apply fn(bin f, acc&) to every bin f = threadIdx.x + i*NT < F
-  template <typename Fn>
+  // apply fn(bin f, acc&) to every bin f = threadIdx.x + i*NT < F; the first
+  // NFULL bins are known in range (compile-time grids): no guard, no branch
+  template <int NFULL = 0, typename Fn>
   __device__ __forceinline__ void each(int F, Fn&& fn) {
     int tid = threadIdx.x;
     asm volatile("" : "+v"(tid));  // bin index math stays at the use (LICM)
 #pragma unroll
     for (int i = 0; i < NBR; ++i) {
       const int f = tid + i * NT;
-      if (f < F) fn(f, r[i]);
+      if (i < NFULL || f < F) fn(f, r[i]);
     }
 #pragma unroll
     for (int i = 0; i < NBL; ++i) {
       const int f = tid + (NBR + i) * NT;
-      if (f < F) {
+      if (NBR + i < NFULL || f < F) {
         cpx<T> a = l[i * NT];
         fn(f, a);
         l[i * NT] = a;

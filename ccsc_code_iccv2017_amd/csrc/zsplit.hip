@@ -46,11 +46,20 @@ __device__ __forceinline__ void st16(void* base, uint32_t boff, V v) {
   *reinterpret_cast<V*>(reinterpret_cast<char*>(base) + boff) = v;
 }
 
-// ProxSparse = max(0, 1 - theta/|a|) a  (dP:32); a = 0 -> 0
+// ProxSparse = max(0, 1 - theta/|a|) a  (dP:32) = a - theta sign(a) for |a| > theta,
+// else 0: the division-free form (equal up to one rounding; the fp64 divide
+// expands to ~12 VALU ops and ran twice per element per iteration, a quarter of
+// the z-iteration's VALU instructions).
 template <typename T>
 __device__ __forceinline__ T soft(T a, T theta) {
-  const T aa = fabs(a);
-  return ((aa > theta) ? (T)1 - theta / aa : (T)0) * a;
+  return (fabs(a) > theta) ? a - copysign(theta, a) : (T)0;
+}
+
+// half-spectrum bins of a compile-time grid (0 for the runtime-planned one)
+template <class FG>
+__device__ constexpr int fixed_bins() {
+  if constexpr (FG::P == 0) return 0;
+  else return FG::F;
 }
 
 // One workgroup (NT threads) per patch.  mode 0: A holds z and Yz holds y
@@ -72,6 +81,11 @@ __global__ __launch_bounds__(NT) void k_zsplit(const T* A, T* Ao, const T* __res
   using V2 = typename vec2_t<T>::type;
   constexpr int NB = NBR + NBL;
   constexpr int NPR = FG::P == 0 ? NB : (FG::P / 2 + NT - 1) / NT;
+  // element pairs / bins per thread that are in range for every thread (fixed
+  // grids): straight-line code without exec-mask branches, which would make
+  // the waitcnt pass fence every global access
+  constexpr int PFULL = FG::P == 0 ? 0 : (FG::P / 2) / NT;
+  constexpr int BFULL = fixed_bins<FG>() / NT;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   Smem<T> S = carve<T>(smem, Gd);
   load_twiddles<T, NT>(S.tw, twg, GO::ntw(Gd));
@@ -92,7 +106,7 @@ __global__ __launch_bounds__(NT) void k_zsplit(const T* A, T* Ao, const T* __res
 #pragma unroll
     for (int i = 0; i < NPR; ++i) {
       const int e2 = tid + i * NT;
-      if (e2 < P2) av[i] = ld16<V2>(A2, (uint32_t)e2 * 16u);
+      if (i < PFULL || e2 < P2) av[i] = ld16<V2>(A2, (uint32_t)e2 * 16u);
     }
   };
   if (vec) load_state(0);
@@ -104,12 +118,21 @@ __global__ __launch_bounds__(NT) void k_zsplit(const T* A, T* Ao, const T* __res
     lds_sync();  // previous slice's spectrum reads are done
     if (mode) {  // LDS <- conj(dw_k) w, C2R: the corr term
       const cpx<T>* dk = dcorr + (int64_t)k * F;
+      cpx<T> dv[NB], wv[NB];
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {  // all loads in flight before the first use
+        const int f = tid + i * NT;
+        if (i < BFULL || f < F) {
+          dv[i] = dk[f];
+          wv[i] = Wp[f];
+        }
+      }
 #pragma unroll
       for (int i = 0; i < NB; ++i) {
         const int f = tid + i * NT;
-        if (f < F) {
+        if (i < BFULL || f < F) {
           const int y = f / GO::Xh(Gd);
-          lds_cpx_store(S.slice + y * RS + 2 * (f - y * GO::Xh(Gd)), 1, cmulc(dk[f], Wp[f]));
+          lds_cpx_store(S.slice + y * RS + 2 * (f - y * GO::Xh(Gd)), 1, cmulc(dv[i], wv[i]));
         }
       }
       GO::c2r(S.slice, Gd, S.tw, tid);
@@ -118,10 +141,13 @@ __global__ __launch_bounds__(NT) void k_zsplit(const T* A, T* Ao, const T* __res
     if (vec) {
       V2* Ao2 = reinterpret_cast<V2*>(Ao + off);
       const V2* Y2 = reinterpret_cast<const V2*>(Yz + off);
+      // all state values are consumed before the first store: on gfx9 vmcnt
+      // counts stores too, so a use of a prefetched value after a store waits
+      // for that store's completion (the interleaved form stalled once per pair)
 #pragma unroll
       for (int i = 0; i < NPR; ++i) {
         const int e2 = tid + i * NT;
-        if (e2 < P2) {
+        if (i < PFULL || e2 < P2) {
           const int e = 2 * e2;
           const int y = e / X;
           T* q = S.slice + y * RS + (e - y * X);
@@ -135,7 +161,7 @@ __global__ __launch_bounds__(NT) void k_zsplit(const T* A, T* Ao, const T* __res
             a.x += yv.x;
             a.y += yv.y;
           }
-          st16<V2>(Ao2, (uint32_t)e2 * 16u, a);
+          av[i] = a;
           const T ux = soft(a.x, theta), uy = soft(a.y, theta);
           V2 cn;
           cn.x = ux - (a.x - ux);   // u - y_new
@@ -143,7 +169,11 @@ __global__ __launch_bounds__(NT) void k_zsplit(const T* A, T* Ao, const T* __res
           *reinterpret_cast<V2*>(q) = cn;
         }
       }
-      if (k + 1 < K) load_state(k + 1);
+#pragma unroll
+      for (int i = 0; i < NPR; ++i) {
+        const int e2 = tid + i * NT;
+        if (i < PFULL || e2 < P2) st16<V2>(Ao2, (uint32_t)e2 * 16u, av[i]);
+      }
     } else {
       // odd X (test grids only): scalar elements
       for (int e = tid; e < P; e += NT) {
@@ -158,8 +188,12 @@ __global__ __launch_bounds__(NT) void k_zsplit(const T* A, T* Ao, const T* __res
     if (GO::Yp(Gd) != GO::Y(Gd))
       for (int x = tid; x < RS; x += NT) S.slice[Yd * RS + x] = (T)0;
     GO::r2c(S.slice, Gd, S.tw, tid);
+    // next slice's state: issued after the R2C, when this slice's stores (whose
+    // data registers the loads overwrite) have drained; it lands under the
+    // accumulation and the next C2R
+    if (vec && k + 1 < K) load_state(k + 1);
     const cpx<T>* dk = dhat + (int64_t)k * F;
-    acc.each(F, [&](int f, cpx<T>& a) {
+    acc.template each<BFULL>(F, [&](int f, cpx<T>& a) {
       const int y = f / GO::Xh(Gd);
       const cpx<T> c = lds_cpx(S.slice + y * RS + 2 * (f - y * GO::Xh(Gd)), 1);
       a = cadd(a, cmul(dk[f], c));
@@ -169,7 +203,7 @@ __global__ __launch_bounds__(NT) void k_zsplit(const T* A, T* Ao, const T* __res
   // writes only its own bins of W, so no barrier is needed after the last
   // C2R's reads of w.
   const cpx<T>* Bp = Bhat + (int64_t)p * F;
-  acc.each(F, [&](int f, cpx<T>& a) { Wp[f] = cscale(csub(Bp[f], a), sden[f]); });
+  acc.template each<BFULL>(F, [&](int f, cpx<T>& a) { Wp[f] = cscale(csub(Bp[f], a), sden[f]); });
 }
 
 // Materialise (z, y) from the state, one workgroup per (patch, filter) slice:
