@@ -279,6 +279,11 @@ __device__ __forceinline__ cpx<T> shfl_c(cpx<T> v, int src) {
 }
 
 // NV right-hand sides per (block, f) share one factor (4D views, L4:281-308).
+// The factor's columns are read in blocks of kDsJB per wave (one load batch per
+// block, address-independent of the solve) so their latency is paid once per
+// block instead of once per column.
+constexpr int kDsJB = 8;
+
 template <typename T, int RPL>
 __global__ __launch_bounds__(256) void k_dsolve(const cpx<T>* __restrict__ L,
                                                 const cpx<T>* __restrict__ h,
@@ -291,6 +296,7 @@ __global__ __launch_bounds__(256) void k_dsolve(const cpx<T>* __restrict__ L,
   if (f >= F) return;
   const int Kp = K * (K + 1) / 2;
   const cpx<T>* Lf = L + ((int64_t)blk * F + f) * Kp;
+  const cpx<T> zero = {(T)0, (T)0};
   for (int uv = 0; uv < NV; ++uv) {
   const cpx<T>* hf = h + (((int64_t)blk * F + f) * NV + uv) * K;
   const cpx<T>* Cb = Ch + (int64_t)blk * K * NV * F + (int64_t)uv * F;   // [blk][k][uv][F]
@@ -303,44 +309,71 @@ __global__ __launch_bounds__(256) void k_dsolve(const cpx<T>* __restrict__ L,
       const cpx<T> hh = hf[i];
       x[t] = {hh.x + rho * c.x, hh.y + rho * c.y};
     } else {
-      x[t] = {(T)0, (T)0};
+      x[t] = zero;
     }
   }
-  // forward: L y = rhs
-  int off = 0;
+  // forward: L y = rhs (column axpy)
+  for (int j0 = 0; j0 < K; j0 += kDsJB) {
+    cpx<T> lc[kDsJB][RPL];
+    T dg[kDsJB];
 #pragma unroll
-  for (int t = 0; t < RPL; ++t) {
-    for (int jl = 0; jl < 64; ++jl) {
-      const int j = t * 64 + jl;
-      if (j >= K) break;
-      const T inv = (T)1 / Lf[off].x;
-      cpx<T> xj = shfl_c(x[t], jl);
-      xj = cscale(xj, inv);
-      if (lane == jl) x[t] = xj;
+    for (int jj = 0; jj < kDsJB; ++jj) {
+      const int j = min(j0 + jj, K - 1);
+      const cpx<T>* col = Lf + (j * K - (j * (j - 1)) / 2) - j;   // col[i] = L[i][j]
+      dg[jj] = col[j].x;
 #pragma unroll
-      for (int u = 0; u < RPL; ++u) {
-        const int i = lane + 64 * u;
-        if (i > j && i < K) x[u] = csub(x[u], cmul(Lf[off + i - j], xj));
+      for (int u = 0; u < RPL; ++u) lc[jj][u] = col[min(lane + 64 * u, K - 1)];
+    }
+#pragma unroll
+    for (int jj = 0; jj < kDsJB; ++jj) {
+      const int j = j0 + jj;
+      if (j < K) {
+        const int src = j & 63, tj = j >> 6;
+        const cpx<T> xs = (tj == 0) ? x[0] : x[RPL - 1];
+        cpx<T> xj = shfl_c(xs, src);
+        xj = cscale(xj, (T)1 / dg[jj]);
+        if (lane == src) {
+          if (tj == 0) x[0] = xj;
+          else x[RPL - 1] = xj;
+        }
+#pragma unroll
+        for (int u = 0; u < RPL; ++u) {
+          const int i = lane + 64 * u;
+          if (i > j && i < K) x[u] = csub(x[u], cmul(lc[jj][u], xj));
+        }
       }
-      off += K - j;
     }
   }
-  // backward: L^H x = y
+  // backward: L^H x = y (column dot products, wave-reduced)
+  for (int j1 = K - 1; j1 >= 0; j1 -= kDsJB) {
+    cpx<T> lc[kDsJB][RPL];
+    T dg[kDsJB];
 #pragma unroll
-  for (int t = RPL - 1; t >= 0; --t) {
-    for (int jl = 63; jl >= 0; --jl) {
-      const int j = t * 64 + jl;
-      if (j >= K) continue;
-      const int oj = j * K - (j * (j - 1)) / 2;
-      cpx<T> part = {(T)0, (T)0};
+    for (int jj = 0; jj < kDsJB; ++jj) {
+      const int j = max(j1 - jj, 0);
+      const cpx<T>* col = Lf + (j * K - (j * (j - 1)) / 2) - j;
+      dg[jj] = col[j].x;
 #pragma unroll
-      for (int u = 0; u < RPL; ++u) {
-        const int i = lane + 64 * u;
-        if (i > j && i < K) part = cadd(part, cmulc(Lf[oj + i - j], x[u]));
+      for (int u = 0; u < RPL; ++u) lc[jj][u] = col[min(lane + 64 * u, K - 1)];
+    }
+#pragma unroll
+    for (int jj = 0; jj < kDsJB; ++jj) {
+      const int j = j1 - jj;
+      if (j >= 0) {
+        cpx<T> part = zero;
+#pragma unroll
+        for (int u = 0; u < RPL; ++u) {
+          const int i = lane + 64 * u;
+          if (i > j && i < K) part = cadd(part, cmulc(lc[jj][u], x[u]));
+        }
+        part.x = wave_sum(part.x);
+        part.y = wave_sum(part.y);
+        const int src = j & 63, tj = j >> 6;
+        if (lane == src) {
+          if (tj == 0) x[0] = cscale(csub(x[0], part), (T)1 / dg[jj]);
+          else x[RPL - 1] = cscale(csub(x[RPL - 1], part), (T)1 / dg[jj]);
+        }
       }
-      part.x = wave_sum(part.x);
-      part.y = wave_sum(part.y);
-      if (lane == jl) x[t] = cscale(csub(x[t], part), (T)1 / Lf[oj].x);
     }
   }
   cpx<T>* Db = Dh + (int64_t)blk * K * NV * F + (int64_t)uv * F;
