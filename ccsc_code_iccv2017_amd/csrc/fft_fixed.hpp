@@ -144,185 +144,29 @@ __device__ __forceinline__ void fpass(T* lds, const cpx<T>* __restrict__ tw, int
   lds_sync();
 }
 
-// ---------------------------------------------------------------------------
-// Wave-local line transforms.  A line of length N = N1*N2 belongs to N2
-// consecutive lanes of ONE wave (64/N2 lines per wave):
-//   stage 1: lane t (0 <= t < N2) takes x = t + N2*m (m < N1), DFT-N1 over m,
-//            twiddle W_N^(t*k1), result back to the slots x = t + N2*k1;
-//   stage 2: lane k1 (< N1) reads t + N2*k1 (t < N2), DFT-N2 over t, writes
-//            X[k1 + N1*k2]  (X[k1 + N1 k2] = sum_t W_N^(t k1) W_N2^(t k2) sum_m x W_N1^(m k1)).
-// The exchange between the stages stays inside the line's own LDS slots and
-// inside one wave (its LDS ops execute in order), so it needs no workgroup
-// barrier: a 2D transform takes 3 barriers instead of 9, and the waves drift
-// apart within a direction so LDS and VALU phases of different waves overlap.
-// The stage-1 twiddles W_N^(t*k1) are exactly the second Stockham pass's table
-// (R = N1, Ns = N2): tw[(k1 - 1)*N2 + t].
-// Measured on the C2 z-iteration (MI355X, n = 1000): 12.50 ms per launch vs
-// 12.00 ms for the barrier-synchronous Stockham passes below (the passes are
-// LDS/VALU-throughput bound, not barrier bound), so it is off by default
-// (-DCCSC_WAVE_LINES=1 selects it).
-// ---------------------------------------------------------------------------
-#ifndef CCSC_WAVE_LINES
-#define CCSC_WAVE_LINES 0
-#endif
-
-__device__ __forceinline__ void wave_lds_fence() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-}
-
-// LD1(line, e) / ST1(line, e, v): stage-1 input / intermediate slots (ST1 must
-// address the slots LD2 reads); LD2 / ST2: stage-2 input / output.  Every slot
-// a line touches belongs to that line (one wave), so reads-before-writes in
-// program order is all the ordering the in-place stages need.
-template <typename T, int N1, int N2, int SIGN, class LD1, class ST1, class LD2, class ST2>
-__device__ __forceinline__ void wl_lines(int nlines, const cpx<T>* __restrict__ tw, int tid,
-                                         LD1&& ld1, ST1&& st1, LD2&& ld2, ST2&& st2) {
-  constexpr int LPW = 64 / N2;
-  asm volatile("" : "+v"(tid));
-  const int lane = tid & 63, wave = tid >> 6;
-  const int li = lane / N2, t = lane - li * N2;
-  const int line = wave * LPW + li;
-  const bool act = li < LPW && line < nlines;
-  if (act) {
-    cpx<T> v[N1];
-#pragma unroll
-    for (int m = 0; m < N1; ++m) v[m] = ld1(line, t + N2 * m);
-    dft_sink<T, N1, SIGN>(v, [&](int k1, cpx<T> val) {
-      if (k1 > 0 && t > 0) {
-        cpx<T> w = tw[(k1 - 1) * N2 + t];
-        if (SIGN > 0) w.y = -w.y;
-        val = cmul(val, w);
-      }
-      st1(line, t + N2 * k1, val);
-    });
-  }
-  wave_lds_fence();
-  if (act && t < N1) {
-    cpx<T> v[N2];
-#pragma unroll
-    for (int q = 0; q < N2; ++q) v[q] = ld2(line, q + N2 * t);
-    dft_sink<T, N2, SIGN>(v, [&](int k2, cpx<T> val) { st2(line, t + N1 * k2, val); });
-  }
-  wave_lds_fence();
-}
-
-// Two-for-one separation of the x-transformed row pairs, in place and wave-local:
-// Z_j = A_2j + i A_2j+1 (split format, rows 2j / 2j+1) -> the half spectra A_2j[c],
-// A_2j+1[c] (c < Xh) interleaved in the same two rows (the lanes of line j read
-// every Z_j[c], Z_j[X-c] they need before any of them writes).
-template <typename T, class FG>
-__device__ __forceinline__ void wl_split_half(T* lds, int tid) {
-  constexpr int N2 = FG::rx0, LPW = 64 / N2, RS = FG::RS;
-  constexpr int CPL = (FG::Xh + N2 - 1) / N2;  // columns per lane
-  asm volatile("" : "+v"(tid));
-  const int lane = tid & 63, wave = tid >> 6;
-  const int li = lane / N2, t = lane - li * N2;
-  const int j = wave * LPW + li;
-  if (li < LPW && j < FG::Yp / 2) {
-    T* r0 = lds + 2 * j * RS;
-    T* r1 = r0 + RS;
-    cpx<T> ae[CPL], ao[CPL];
-#pragma unroll
-    for (int i = 0; i < CPL; ++i) {
-      const int c = t + N2 * i;
-      if (c < FG::Xh) {
-        const int x2 = (c == 0) ? 0 : FG::X - c;
-        const cpx<T> z1 = {r0[c], r1[c]};
-        const cpx<T> z2 = {r0[x2], r1[x2]};
-        ae[i] = {(T)0.5 * (z1.x + z2.x), (T)0.5 * (z1.y - z2.y)};
-        ao[i] = {(T)0.5 * (z1.y + z2.y), (T)-0.5 * (z1.x - z2.x)};
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < CPL; ++i) {
-      const int c = t + N2 * i;
-      if (c < FG::Xh) {
-        lds_cpx_store(r0 + 2 * c, 1, ae[i]);
-        lds_cpx_store(r1 + 2 * c, 1, ao[i]);
-      }
-    }
-  }
-  wave_lds_fence();
-}
-
-template <typename T, class FG, int NT>
-__device__ __forceinline__ void wslice_r2c(T* lds, const cpx<T>* tw, int tid) {
-  static_assert(FG::Y % 2 == 0, "wave-local R2C assumes an even grid height");
-  static_assert((NT / 64) * (64 / FG::rx0) >= FG::Yp / 2, "too few waves for the x lines");
-  static_assert((NT / 64) * (64 / FG::ry0) >= FG::Xh, "too few waves for the y lines");
-  constexpr int RS = FG::RS;
-  // split format: line j = rows 2j (re), 2j+1 (im)
-  auto ld_sp = [&](int j, int e) { const T* p = lds + 2 * j * RS + e; return cpx<T>{p[0], p[RS]}; };
-  auto st_sp = [&](int j, int e, cpx<T> v) { T* p = lds + 2 * j * RS + e; p[0] = v.x; p[RS] = v.y; };
-  // interleaved half spectrum: column c, row e
-  auto ld_il = [&](int c, int e) { return lds_cpx(lds + e * RS + 2 * c, 1); };
-  auto st_il = [&](int c, int e, cpx<T> v) { lds_cpx_store(lds + e * RS + 2 * c, 1, v); };
-  lds_sync();
-  wl_lines<T, FG::rx1, FG::rx0, -1>(FG::Yp / 2, tw + FG::TWX1, tid, ld_sp, st_sp, ld_sp, st_sp);
-  wl_split_half<T, FG>(lds, tid);
-  lds_sync();
-  wl_lines<T, FG::ry1, FG::ry0, -1>(FG::Xh, tw + FG::TWY1, tid, ld_il, st_il, ld_il, st_il);
-  lds_sync();
-}
-
-template <typename T, class FG, int NT>
-__device__ __forceinline__ void wslice_c2r(T* lds, const cpx<T>* tw, int tid) {
-  static_assert(FG::Y % 2 == 0, "wave-local C2R assumes an even grid height");
-  static_assert((NT / 64) * (64 / FG::rx0) >= FG::Yp / 2, "too few waves for the x lines");
-  static_assert((NT / 64) * (64 / FG::ry0) >= FG::Xh, "too few waves for the y lines");
-  constexpr int RS = FG::RS;
-  auto ld_sp = [&](int j, int e) { const T* p = lds + 2 * j * RS + e; return cpx<T>{p[0], p[RS]}; };
-  auto st_sp = [&](int j, int e, cpx<T> v) { T* p = lds + 2 * j * RS + e; p[0] = v.x; p[RS] = v.y; };
-  auto ld_il = [&](int c, int e) { return lds_cpx(lds + e * RS + 2 * c, 1); };
-  auto st_il = [&](int c, int e, cpx<T> v) { lds_cpx_store(lds + e * RS + 2 * c, 1, v); };
-  // Hermitian pair Z_j[x] = A_2j[x] + i A_2j+1[x] from the interleaved half spectrum
-  // (kModeHermPair); reads and writes stay inside rows 2j, 2j+1 (one wave's lanes)
-  auto ld_herm = [&](int j, int e) {
-    const bool hi = e >= FG::Xh;
-    const int c = hi ? FG::X - e : e;
-    const T* r0 = lds + 2 * j * RS + 2 * c;
-    cpx<T> a = lds_cpx(r0, 1);
-    cpx<T> b = lds_cpx(r0 + RS, 1);
-    if (hi) {
-      a.y = -a.y;
-      b.y = -b.y;
-    }
-    return cpx<T>{a.x - b.y, a.y + b.x};
-  };
-  lds_sync();
-  wl_lines<T, FG::ry1, FG::ry0, +1>(FG::Xh, tw + FG::TWY1, tid, ld_il, st_il, ld_il, st_il);
-  lds_sync();
-  wl_lines<T, FG::rx1, FG::rx0, +1>(FG::Yp / 2, tw + FG::TWX1, tid, ld_herm, st_sp, ld_sp, st_sp);
-  lds_sync();
-}
-
 // Forward 2D R2C (MATLAB fft2) of the real slice in LDS rows [y*RS, y*RS+X);
 // result: interleaved half spectrum, bin (x', y) at lds[y*RS + 2x'].
+// (A wave-local variant -- each 110-point line owned by 11 lanes of one wave,
+// its two radix stages exchanging through the line's own LDS slots, 3 barriers
+// per 2D transform instead of 9 -- measured 5% slower on the C2 z-iteration:
+// these passes are LDS/VALU-throughput bound, not barrier bound.)
 template <typename T, class FG, int NT>
 __device__ __forceinline__ void fslice_r2c(T* lds, const cpx<T>* tw, int tid) {
-#if CCSC_WAVE_LINES
-  wslice_r2c<T, FG, NT>(lds, tw, tid);
-#else
   lds_sync();
   fpass<T, FG, NT, true, FG::rx0, 1, -1, kModePlain>(lds, tw + FG::TWX0, tid);
   fpass<T, FG, NT, true, FG::rx1, FG::rx0, -1, kModePlain>(lds, tw + FG::TWX1, tid);
   fpass<T, FG, NT, false, FG::ry0, 1, -1, kModeSplitToHalf>(lds, tw + FG::TWY0, tid);
   fpass<T, FG, NT, false, FG::ry1, FG::ry0, -1, kModePlain>(lds, tw + FG::TWY1, tid);
-#endif
 }
 
 // Inverse 2D C2R (unnormalised) of the interleaved half spectrum in LDS.
 template <typename T, class FG, int NT>
 __device__ __forceinline__ void fslice_c2r(T* lds, const cpx<T>* tw, int tid) {
-#if CCSC_WAVE_LINES
-  wslice_c2r<T, FG, NT>(lds, tw, tid);
-#else
   lds_sync();
   fpass<T, FG, NT, false, FG::ry0, 1, +1, kModePlain>(lds, tw + FG::TWY0, tid);
   fpass<T, FG, NT, false, FG::ry1, FG::ry0, +1, kModePlain>(lds, tw + FG::TWY1, tid);
   fpass<T, FG, NT, true, FG::rx0, 1, +1, kModeHermPair>(lds, tw + FG::TWX0, tid);
   fpass<T, FG, NT, true, FG::rx1, FG::rx0, +1, kModePlain>(lds, tw + FG::TWX1, tid);
-#endif
 }
 
 // Runtime-planned grids (every other size): the same slice kernels, with
