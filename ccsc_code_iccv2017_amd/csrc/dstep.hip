@@ -30,8 +30,25 @@ __device__ __forceinline__ int pk_off(int j, int K) { return j * K - (j * (j - 1
 // form spent its time in LDS latency chains (measured 2.9 of 4.2 ms per block
 // launch at K = 100).
 // ---------------------------------------------------------------------------
-constexpr int kCholNB = 8;
-constexpr int kCholT = 4;
+#ifndef CCSC_CHOL_NB
+#define CCSC_CHOL_NB 8
+#endif
+#ifndef CCSC_CHOL_T
+#define CCSC_CHOL_T 2
+#endif
+constexpr int kCholNB = CCSC_CHOL_NB;
+constexpr int kCholT = CCSC_CHOL_T;
+
+// broadcast of lane `l` (wave-uniform) through v_readlane: a scalar-register
+// hop of a few cycles, where a shuffle is an LDS-crossbar round trip
+__device__ __forceinline__ double readlane(double v, int l) {
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
+                          __builtin_amdgcn_readlane(__double2loint(v), l));
+}
+template <typename T>
+__device__ __forceinline__ cpx<T> readlane_c(cpx<T> v, int l) {
+  return {readlane(v.x, l), readlane(v.y, l)};
+}
 
 template <typename T>
 __device__ __forceinline__ void chol_blocked(cpx<T>* sG, int K) {
@@ -53,7 +70,7 @@ __device__ __forceinline__ void chol_blocked(cpx<T>* sG, int K) {
       for (int c = 0; c < kCholNB; ++c) {
         if (c < jb) {
           const int j = j0 + c;
-          const T djj = sqrt(__shfl(P[0][c].x, c, 64));  // row j sits in lane c
+          const T djj = sqrt(readlane(P[0][c].x, c));  // row j sits in lane c
           const T inv = (T)1 / djj;
 #pragma unroll
           for (int t = 0; t < 2; ++t) {
@@ -65,7 +82,7 @@ __device__ __forceinline__ void chol_blocked(cpx<T>* sG, int K) {
 #pragma unroll
           for (int c2 = c + 1; c2 < kCholNB; ++c2) {
             if (c2 < jb) {
-              const cpx<T> g = {__shfl(P[0][c].x, c2, 64), __shfl(P[0][c].y, c2, 64)};
+              const cpx<T> g = readlane_c(P[0][c], c2);
 #pragma unroll
               for (int t = 0; t < 2; ++t) {
                 const int r = j0 + lane + 64 * t;
@@ -330,7 +347,7 @@ __global__ __launch_bounds__(256) void k_dsolve(const cpx<T>* __restrict__ L,
       if (j < K) {
         const int src = j & 63, tj = j >> 6;
         const cpx<T> xs = (tj == 0) ? x[0] : x[RPL - 1];
-        cpx<T> xj = shfl_c(xs, src);
+        cpx<T> xj = readlane_c(xs, src);
         xj = cscale(xj, (T)1 / dg[jj]);
         if (lane == src) {
           if (tj == 0) x[0] = xj;

@@ -135,7 +135,11 @@ __global__ __launch_bounds__(NT) void k_zsplit(const T* A, T* Ao, const T* __res
           lds_cpx_store(S.slice + y * RS + 2 * (f - y * GO::Xh(Gd)), 1, cmulc(dv[i], wv[i]));
         }
       }
+#ifndef CCSC_ABL_NOC2R
       GO::c2r(S.slice, Gd, S.tw, tid);
+#else
+      lds_sync();
+#endif
     }
     asm volatile("" : "+v"(tid));  // elementwise index math after the C2R, not live across it
     if (vec) {
@@ -187,7 +191,11 @@ __global__ __launch_bounds__(NT) void k_zsplit(const T* A, T* Ao, const T* __res
     }
     if (GO::Yp(Gd) != GO::Y(Gd))
       for (int x = tid; x < RS; x += NT) S.slice[Yd * RS + x] = (T)0;
+#ifndef CCSC_ABL_NOR2C
     GO::r2c(S.slice, Gd, S.tw, tid);
+#else
+    lds_sync();
+#endif
     // next slice's state: issued after the R2C, when this slice's stores (whose
     // data registers the loads overwrite) have drained; it lands under the
     // accumulation and the next C2R
