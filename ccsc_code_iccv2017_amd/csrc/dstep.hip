@@ -295,13 +295,15 @@ __device__ __forceinline__ cpx<T> shfl_c(cpx<T> v, int src) {
   return {__shfl(v.x, src, 64), __shfl(v.y, src, 64)};
 }
 
-// NV right-hand sides per (block, f) share one factor (4D views, L4:281-308).
-// The factor's columns are read in blocks of kDsJB per wave (one load batch per
-// block, address-independent of the solve) so their latency is paid once per
-// block instead of once per column.
+// NV right-hand sides per (block, f) share one factor (4D views, L4:281-308;
+// the W wavelengths of the 2-3D learner, L23:293).  They are solved NVB at a
+// time in one sweep over the factor, so L is streamed ceil(NV/NVB) times
+// instead of NV times.  The factor's columns are read in blocks of kDsJB per
+// wave (one load batch per block, address-independent of the solve) so their
+// latency is paid once per block instead of once per column.
 constexpr int kDsJB = 8;
 
-template <typename T, int RPL>
+template <typename T, int RPL, int NVB>
 __global__ __launch_bounds__(256) void k_dsolve(const cpx<T>* __restrict__ L,
                                                 const cpx<T>* __restrict__ h,
                                                 const cpx<T>* __restrict__ Ch,
@@ -314,19 +316,25 @@ __global__ __launch_bounds__(256) void k_dsolve(const cpx<T>* __restrict__ L,
   const int Kp = K * (K + 1) / 2;
   const cpx<T>* Lf = L + ((int64_t)blk * F + f) * Kp;
   const cpx<T> zero = {(T)0, (T)0};
-  for (int uv = 0; uv < NV; ++uv) {
-  const cpx<T>* hf = h + (((int64_t)blk * F + f) * NV + uv) * K;
-  const cpx<T>* Cb = Ch + (int64_t)blk * K * NV * F + (int64_t)uv * F;   // [blk][k][uv][F]
-  cpx<T> x[RPL];
+  for (int uv0 = 0; uv0 < NV; uv0 += NVB) {
+  // views past NV solve a zero right-hand side (uniform, no divergence) and are not stored
+  const int nvc = min(NVB, NV - uv0);
+  cpx<T> x[NVB][RPL];
 #pragma unroll
-  for (int t = 0; t < RPL; ++t) {
-    const int i = lane + 64 * t;
-    if (i < K) {
-      const cpx<T> c = Cb[(int64_t)i * NV * F + f];
-      const cpx<T> hh = hf[i];
-      x[t] = {hh.x + rho * c.x, hh.y + rho * c.y};
-    } else {
-      x[t] = zero;
+  for (int v = 0; v < NVB; ++v) {
+    const int uv = uv0 + v;
+    const cpx<T>* hf = h + (((int64_t)blk * F + f) * NV + uv) * K;
+    const cpx<T>* Cb = Ch + (int64_t)blk * K * NV * F + (int64_t)uv * F;   // [blk][k][uv][F]
+#pragma unroll
+    for (int t = 0; t < RPL; ++t) {
+      const int i = lane + 64 * t;
+      if (v < nvc && i < K) {
+        const cpx<T> c = Cb[(int64_t)i * NV * F + f];
+        const cpx<T> hh = hf[i];
+        x[v][t] = {hh.x + rho * c.x, hh.y + rho * c.y};
+      } else {
+        x[v][t] = zero;
+      }
     }
   }
   // forward: L y = rhs (column axpy)
@@ -346,17 +354,20 @@ __global__ __launch_bounds__(256) void k_dsolve(const cpx<T>* __restrict__ L,
       const int j = j0 + jj;
       if (j < K) {
         const int src = j & 63, tj = j >> 6;
-        const cpx<T> xs = (tj == 0) ? x[0] : x[RPL - 1];
-        cpx<T> xj = readlane_c(xs, src);
-        xj = cscale(xj, (T)1 / dg[jj]);
-        if (lane == src) {
-          if (tj == 0) x[0] = xj;
-          else x[RPL - 1] = xj;
-        }
+        const T inv = (T)1 / dg[jj];
 #pragma unroll
-        for (int u = 0; u < RPL; ++u) {
-          const int i = lane + 64 * u;
-          if (i > j && i < K) x[u] = csub(x[u], cmul(lc[jj][u], xj));
+        for (int v = 0; v < NVB; ++v) {
+          const cpx<T> xs = (tj == 0) ? x[v][0] : x[v][RPL - 1];
+          const cpx<T> xj = cscale(readlane_c(xs, src), inv);
+          if (lane == src) {
+            if (tj == 0) x[v][0] = xj;
+            else x[v][RPL - 1] = xj;
+          }
+#pragma unroll
+          for (int u = 0; u < RPL; ++u) {
+            const int i = lane + 64 * u;
+            if (i > j && i < K) x[v][u] = csub(x[v][u], cmul(lc[jj][u], xj));
+          }
         }
       }
     }
@@ -377,29 +388,45 @@ __global__ __launch_bounds__(256) void k_dsolve(const cpx<T>* __restrict__ L,
     for (int jj = 0; jj < kDsJB; ++jj) {
       const int j = j1 - jj;
       if (j >= 0) {
-        cpx<T> part = zero;
-#pragma unroll
-        for (int u = 0; u < RPL; ++u) {
-          const int i = lane + 64 * u;
-          if (i > j && i < K) part = cadd(part, cmulc(lc[jj][u], x[u]));
-        }
-        part.x = wave_sum(part.x);
-        part.y = wave_sum(part.y);
         const int src = j & 63, tj = j >> 6;
-        if (lane == src) {
-          if (tj == 0) x[0] = cscale(csub(x[0], part), (T)1 / dg[jj]);
-          else x[RPL - 1] = cscale(csub(x[RPL - 1], part), (T)1 / dg[jj]);
+        const T inv = (T)1 / dg[jj];
+#pragma unroll
+        for (int v = 0; v < NVB; ++v) {
+          cpx<T> part = zero;
+#pragma unroll
+          for (int u = 0; u < RPL; ++u) {
+            const int i = lane + 64 * u;
+            if (i > j && i < K) part = cadd(part, cmulc(lc[jj][u], x[v][u]));
+          }
+          part.x = wave_sum(part.x);
+          part.y = wave_sum(part.y);
+          if (lane == src) {
+            if (tj == 0) x[v][0] = cscale(csub(x[v][0], part), inv);
+            else x[v][RPL - 1] = cscale(csub(x[v][RPL - 1], part), inv);
+          }
         }
       }
     }
   }
-  cpx<T>* Db = Dh + (int64_t)blk * K * NV * F + (int64_t)uv * F;
 #pragma unroll
-  for (int t = 0; t < RPL; ++t) {
-    const int i = lane + 64 * t;
-    if (i < K) Db[(int64_t)i * NV * F + f] = x[t];
+  for (int v = 0; v < NVB; ++v) {
+    if (v < nvc) {
+      cpx<T>* Db = Dh + (int64_t)blk * K * NV * F + (int64_t)(uv0 + v) * F;
+#pragma unroll
+      for (int t = 0; t < RPL; ++t) {
+        const int i = lane + 64 * t;
+        if (i < K) Db[(int64_t)i * NV * F + f] = x[v][t];
+      }
+    }
   }
-  }  // views
+  }  // view groups
+}
+
+template <typename T, int RPL, int NVB>
+static void dsolve_go(dim3 grid, hipStream_t st, const cpx<T>* L, const cpx<T>* h,
+                      const cpx<T>* Ch, cpx<T>* Dh, int F, int K, T rho, int fgroups, int NV) {
+  hipLaunchKernelGGL((k_dsolve<T, RPL, NVB>), grid, dim3(256), 0, st, L, h, Ch, Dh, F, K, rho,
+                     fgroups, NV);
 }
 
 template <typename T>
@@ -408,14 +435,16 @@ hipError_t launch_dsolve(const cpx<T>* L, const cpx<T>* h, const cpx<T>* Ch, cpx
   if (nblocks <= 0) return hipSuccess;
   const int fgroups = (F + 3) / 4;
   const dim3 grid((unsigned)(nblocks * fgroups));
-  if (K <= 64)
-    hipLaunchKernelGGL((k_dsolve<T, 1>), grid, dim3(256), 0, st, L, h, Ch, Dh, F, K, rho,
-                       fgroups, NV);
-  else if (K <= 128)
-    hipLaunchKernelGGL((k_dsolve<T, 2>), grid, dim3(256), 0, st, L, h, Ch, Dh, F, K, rho,
-                       fgroups, NV);
-  else
+  if (K <= 64) {
+    if (NV == 1) dsolve_go<T, 1, 1>(grid, st, L, h, Ch, Dh, F, K, rho, fgroups, NV);
+    else if (NV <= 4) dsolve_go<T, 1, 4>(grid, st, L, h, Ch, Dh, F, K, rho, fgroups, NV);
+    else dsolve_go<T, 1, 8>(grid, st, L, h, Ch, Dh, F, K, rho, fgroups, NV);
+  } else if (K <= 128) {
+    if (NV == 1) dsolve_go<T, 2, 1>(grid, st, L, h, Ch, Dh, F, K, rho, fgroups, NV);
+    else dsolve_go<T, 2, 4>(grid, st, L, h, Ch, Dh, F, K, rho, fgroups, NV);
+  } else {
     return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 

@@ -81,8 +81,12 @@ static bool is_native_radix(int R) {
 
 // Fewest passes; native (unrolled) radices first, then at most one generic
 // prime radix <= kMaxGenericRadix (e.g. 74 = 2 * 37).  Register budget: a native
-// pass holds n/R butterflies per line (<= kMaxButterflies), a generic pass n
-// outputs per line (<= kMaxGenericOut * kNT).
+// pass holds n/R butterflies per line (<= kMaxButterflies), a generic pass one
+// task (kGenericQP conjugate output pairs of one DFT) per thread.
+static int64_t generic_tasks(int n, int nlines, int p) {
+  return (int64_t)nlines * (n / p) * (((p - 1) / 2 + kGenericQP - 1) / kGenericQP);
+}
+
 static bool plan1d(int n, int nlines, Plan1D& out) {
   Plan1D best{};
   best.npass = 99;
@@ -118,7 +122,7 @@ static bool plan1d(int n, int nlines, Plan1D& out) {
       for (int d = 2; d * d <= p; ++d)
         if (p % d == 0) prime = false;
       if (!prime || n % p) continue;
-      if ((int64_t)n * nlines > (int64_t)kMaxGenericOut * kNT) continue;
+      if (generic_tasks(n, nlines, p) > kNT) continue;
       Plan1D rest{};
       if (!plan1d(n / p, nlines, rest) && n / p != 1) continue;
       if (rest.npass + 1 > kMaxPass) continue;

@@ -199,7 +199,7 @@ struct Plan1D {
 // to kMaxGenericRadix, e.g. 37 for the 74-point grids of the 3D/4D configs)
 // runs through fft_pass_generic.
 constexpr int kMaxGenericRadix = 64;
-constexpr int kMaxGenericOut = 4;  // outputs per thread of a generic pass
+constexpr int kGenericQP = 3;      // conjugate output pairs per generic-pass task
 
 // Per-slice description of the 2D grid (all in units of T unless noted).
 struct Grid2D {
@@ -333,60 +333,103 @@ __device__ __forceinline__ void fft_pass(T* lds, int mode, const LineGeom& gin,
   lds_sync();
 }
 
-// Generic radix-R Stockham pass (R not unrolled): every output element is an
-// R-term sum read straight from LDS,
-//   out[(j-k)R + k + q Ns] = sum_r x[j + r nb] tw(r, k) w^(r q),   w = e^(SIGN 2 pi i/R),
-// so a thread only keeps its (<= kMaxGenericOut) outputs across the barrier.
+// Generic odd-prime radix-R Stockham pass (R not unrolled, e.g. 37 for the
+// 74-point grids):
+//   out[(j-k)R + k + q Ns] = sum_r x[j + r nb] tw(r, k) w^(r q),   w = e^(SIGN 2 pi i/R).
+// The R-point DFT is evaluated in conjugate output pairs.  With twiddled inputs
+// x_r, s_r = x_r + x_{R-r}, d_r = x_r - x_{R-r} (r = 1..h, h = (R-1)/2) and
+// theta = 2 pi r q / R:  A = x_0 + sum_r s_r cos(theta), B = -sum_r d_r sin(theta),
+// X_q = A + iB and X_{R-q} = A - iB forward (swapped for the inverse).  One task
+// reads its DFT's R inputs once and produces kGenericQP pairs (task 0 also the
+// DC term): ~(2R + 3h)/(2 kGenericQP) LDS reads per output instead of the
+// 3(R-1) of an output-per-thread R-term sum.  The host plan keeps the task
+// count within one per thread (generic_tasks() in engine.cpp).
 template <typename T, int SIGN>
 __device__ __forceinline__ void fft_pass_generic(T* lds, int R, int mode, const LineGeom& gin,
                                               const LineGeom& gout, const Grid2D& G, int n,
                                               int Ns, const cpx<T>* __restrict__ tw) {
+  constexpr int QP = kGenericQP;
   const int nb = n / R;
   const int nl = gin.nlines;
-  const int total = nl * n;
+  const int h = (R - 1) / 2;
+  const int ng = (h + QP - 1) / QP;   // tasks per DFT
+  const int total = nl * nb * ng;
   const bool along = gin.estride == 1;
-  const cpx<T>* roots = tw + (R - 1) * Ns;
-  cpx<T> acc[kMaxGenericOut];
-  int dst[kMaxGenericOut];
-#pragma unroll
-  for (int i = 0; i < kMaxGenericOut; ++i) {
-    const int o = (int)threadIdx.x + i * kNT;
-    dst[i] = -1;
-    if (o < total) {
-      int line, t;
-      if (along) {
-        line = o / n;
-        t = o - line * n;
-      } else {
-        t = o / nl;
-        line = o - t * nl;
-      }
-      const int k = t % Ns;
-      const int q = (t / Ns) % R;
-      const int j = (t / (Ns * R)) * Ns + k;
-      cpx<T> a = load_elem<T>(lds, gin, G, mode, line, j);
-      int m = 0;
-      for (int r = 1; r < R; ++r) {
-        cpx<T> x = load_elem<T>(lds, gin, G, mode, line, j + r * nb);
-        if (Ns > 1) {
-          cpx<T> w = tw[(r - 1) * Ns + k];
-          if (SIGN > 0) w.y = -w.y;
-          x = cmul(x, w);
-        }
-        m += q;
-        if (m >= R) m -= R;
-        cpx<T> rt = roots[m];
-        if (SIGN > 0) rt.y = -rt.y;
-        a = cadd(a, cmul(x, rt));
-      }
-      acc[i] = a;
-      dst[i] = line * gout.lstride + t * gout.estride;
+  const cpx<T>* roots = tw + (R - 1) * Ns;   // (cos, -sin)(2 pi m / R)
+  const int o = (int)threadIdx.x;
+  int dst = -1, q0 = 0;
+  cpx<T> dc = {(T)0, (T)0}, A[QP], B[QP];
+  if (o < total) {
+    int line, j, g;
+    if (along) {   // lanes contiguous in j (contiguous LDS addresses)
+      j = o % nb;
+      const int rest = o / nb;
+      g = rest % ng;
+      line = rest / ng;
+    } else {       // lanes contiguous in line (strided lines: one address per line)
+      line = o % nl;
+      const int rest = o / nl;
+      j = rest % nb;
+      g = rest / nb;
     }
+    const int k = j % Ns;
+    q0 = 1 + g * QP;
+    int m[QP];
+#pragma unroll
+    for (int i = 0; i < QP; ++i) {
+      A[i] = {(T)0, (T)0};
+      B[i] = {(T)0, (T)0};
+      m[i] = 0;
+    }
+    const cpx<T> x0 = load_elem<T>(lds, gin, G, mode, line, j);
+    cpx<T> sdc = {(T)0, (T)0};
+    for (int r = 1; r <= h; ++r) {
+      cpx<T> xa = load_elem<T>(lds, gin, G, mode, line, j + r * nb);
+      cpx<T> xb = load_elem<T>(lds, gin, G, mode, line, j + (R - r) * nb);
+      if (Ns > 1) {
+        cpx<T> wa = tw[(r - 1) * Ns + k], wb = tw[(R - r - 1) * Ns + k];
+        if (SIGN > 0) {
+          wa.y = -wa.y;
+          wb.y = -wb.y;
+        }
+        xa = cmul(xa, wa);
+        xb = cmul(xb, wb);
+      }
+      const cpx<T> sr = cadd(xa, xb), dr = csub(xa, xb);
+      sdc = cadd(sdc, sr);
+#pragma unroll
+      for (int i = 0; i < QP; ++i) {
+        m[i] += q0 + i;
+        if (m[i] >= R) m[i] -= R;
+        const cpx<T> rt = roots[m[i]];   // (cos theta, -sin theta)
+        A[i].x += sr.x * rt.x;
+        A[i].y += sr.y * rt.x;
+        B[i].x += dr.x * rt.y;
+        B[i].y += dr.y * rt.y;
+      }
+    }
+    dc = cadd(x0, sdc);
+#pragma unroll
+    for (int i = 0; i < QP; ++i) A[i] = cadd(A[i], x0);
+    dst = line * gout.lstride + ((j - k) * R + k) * gout.estride;
   }
   lds_sync();
+  if (dst >= 0) {
+    // forward (SIGN < 0): X_q = A + i B, X_{R-q} = A - i B; inverse: the opposite
+    const int ostride = Ns * gout.estride;
+    if (q0 == 1) lds_cpx_store(lds + dst, gout.imoff, dc);
 #pragma unroll
-  for (int i = 0; i < kMaxGenericOut; ++i)
-    if (dst[i] >= 0) lds_cpx_store(lds + dst[i], gout.imoff, acc[i]);
+    for (int i = 0; i < QP; ++i) {
+      const int q = q0 + i;
+      if (q <= h) {
+        const cpx<T> iB = {-B[i].y, B[i].x};
+        const cpx<T> xq = SIGN < 0 ? cadd(A[i], iB) : csub(A[i], iB);
+        const cpx<T> xr = SIGN < 0 ? csub(A[i], iB) : cadd(A[i], iB);
+        lds_cpx_store(lds + dst + q * ostride, gout.imoff, xq);
+        lds_cpx_store(lds + dst + (R - q) * ostride, gout.imoff, xr);
+      }
+    }
+  }
   lds_sync();
 }
 

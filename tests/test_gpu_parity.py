@@ -21,7 +21,7 @@ def _rel(a, b):
 
 
 @pytest.mark.parametrize("X,Y", [(16, 16), (110, 110), (15, 14), (14, 15), (24, 20), (74, 74),
-                                 (26, 37), (60, 60)])
+                                 (26, 37), (60, 60), (62, 41), (38, 34), (58, 46), (110, 106)])
 def test_fft2d_r2c_c2r(gpu_ctx, X, Y):
     from ccsc_code_iccv2017_amd.learners import fft2d_test
     rng = np.random.default_rng(X * 1000 + Y)
