@@ -287,8 +287,9 @@ hipError_t launch_gram_chol(const cpx<T>* Zh, const cpx<T>* Bh, cpx<T>* L, cpx<T
 
 // ---------------------------------------------------------------------------
 // d-solve: one wave per (block, f); rows of the K-vector are spread over the
-// 64 lanes (RPL rows per lane).  Forward solve column-oriented (axpy with the
-// contiguous packed column), backward solve as wave-reduced dot products.
+// 64 lanes (RPL rows per lane).  Both triangular solves are column axpys with
+// the pivot broadcast by v_readlane: forward with the contiguous packed column
+// (coalesced), backward with each lane's own column (L^H's row).
 // ---------------------------------------------------------------------------
 template <typename T>
 __device__ __forceinline__ cpx<T> shfl_c(cpx<T> v, int src) {
@@ -316,6 +317,14 @@ __global__ __launch_bounds__(256) void k_dsolve(const cpx<T>* __restrict__ L,
   const int Kp = K * (K + 1) / 2;
   const cpx<T>* Lf = L + ((int64_t)blk * F + f) * Kp;
   const cpx<T> zero = {(T)0, (T)0};
+  // lane row l = lane + 64u (clamped into the matrix): packed column l starts at
+  // coff[u] + l (entry L[p][l] at coff[u] + p, p >= l)
+  int il[RPL], coff[RPL];
+#pragma unroll
+  for (int u = 0; u < RPL; ++u) {
+    il[u] = min(lane + 64 * u, K - 1);
+    coff[u] = il[u] * K - (il[u] * (il[u] - 1)) / 2 - il[u];
+  }
   for (int uv0 = 0; uv0 < NV; uv0 += NVB) {
   // views past NV solve a zero right-hand side (uniform, no divergence) and are not stored
   const int nvc = min(NVB, NV - uv0);
@@ -372,7 +381,12 @@ __global__ __launch_bounds__(256) void k_dsolve(const cpx<T>* __restrict__ L,
       }
     }
   }
-  // backward: L^H x = y (column dot products, wave-reduced)
+  // backward, one right-hand side: column dot products (coalesced reads of
+  // column p), wave-reduced.  With several right-hand sides per sweep the
+  // reductions dominate and the column-axpy form below is faster; with one the
+  // latter's per-lane column walk (64 lines per load) costs more than the
+  // reductions (C2: 22 vs 42 ms per launch).
+  if constexpr (NVB == 1) {
   for (int j1 = K - 1; j1 >= 0; j1 -= kDsJB) {
     cpx<T> lc[kDsJB][RPL];
     T dg[kDsJB];
@@ -388,25 +402,58 @@ __global__ __launch_bounds__(256) void k_dsolve(const cpx<T>* __restrict__ L,
     for (int jj = 0; jj < kDsJB; ++jj) {
       const int j = j1 - jj;
       if (j >= 0) {
+        cpx<T> part = zero;
+#pragma unroll
+        for (int u = 0; u < RPL; ++u) {
+          const int i = lane + 64 * u;
+          if (i > j && i < K) part = cadd(part, cmulc(lc[jj][u], x[0][u]));
+        }
+        part.x = wave_sum(part.x);
+        part.y = wave_sum(part.y);
         const int src = j & 63, tj = j >> 6;
-        const T inv = (T)1 / dg[jj];
-#pragma unroll
-        for (int v = 0; v < NVB; ++v) {
-          cpx<T> part = zero;
-#pragma unroll
-          for (int u = 0; u < RPL; ++u) {
-            const int i = lane + 64 * u;
-            if (i > j && i < K) part = cadd(part, cmulc(lc[jj][u], x[v][u]));
-          }
-          part.x = wave_sum(part.x);
-          part.y = wave_sum(part.y);
-          if (lane == src) {
-            if (tj == 0) x[v][0] = cscale(csub(x[v][0], part), inv);
-            else x[v][RPL - 1] = cscale(csub(x[v][RPL - 1], part), inv);
-          }
+        if (lane == src) {
+          if (tj == 0) x[0][0] = cscale(csub(x[0][0], part), (T)1 / dg[jj]);
+          else x[0][RPL - 1] = cscale(csub(x[0][RPL - 1], part), (T)1 / dg[jj]);
         }
       }
     }
+  }
+  } else {
+  // backward: L^H x = y, also as column axpys: once x_p is final, every row
+  // l < p loses conj(L[p][l]) x_p.  L[p][l] sits in column l, so lane l walks
+  // its own packed column upwards (8 consecutive entries per block = one
+  // 128-B line per lane); no cross-lane reductions.
+  for (int j1 = K - 1; j1 >= 0; j1 -= kDsJB) {
+    cpx<T> lr[kDsJB][RPL];
+    T dg[kDsJB];
+#pragma unroll
+    for (int jj = 0; jj < kDsJB; ++jj) {
+      const int p = max(j1 - jj, 0);
+      dg[jj] = Lf[p * K - (p * (p - 1)) / 2].x;                  // L[p][p]
+#pragma unroll
+      for (int u = 0; u < RPL; ++u) lr[jj][u] = Lf[coff[u] + max(p, il[u])];   // L[p][l]
+    }
+#pragma unroll
+    for (int jj = 0; jj < kDsJB; ++jj) {
+      const int p = j1 - jj;
+      if (p >= 0) {
+        const int src = p & 63, tp = p >> 6;
+        const T inv = (T)1 / dg[jj];
+#pragma unroll
+        for (int v = 0; v < NVB; ++v) {
+          const cpx<T> xs = (tp == 0) ? x[v][0] : x[v][RPL - 1];
+          const cpx<T> xp = cscale(readlane_c(xs, src), inv);
+          if (lane == src) {
+            if (tp == 0) x[v][0] = xp;
+            else x[v][RPL - 1] = xp;
+          }
+#pragma unroll
+          for (int u = 0; u < RPL; ++u)
+            if (lane + 64 * u < p) x[v][u] = csub(x[v][u], cmulc(lr[jj][u], xp));
+        }
+      }
+    }
+  }
   }
 #pragma unroll
   for (int v = 0; v < NVB; ++v) {
