@@ -50,6 +50,24 @@ __device__ __forceinline__ cpx<T> readlane_c(cpx<T> v, int l) {
   return {readlane(v.x, l), readlane(v.y, l)};
 }
 
+// Full-wave fp64 sum through DPP (VALU lane moves, no LDS): quad swaps, then
+// half-row and row mirrors leave each 16-lane row's sum in all its lanes; the
+// four row sums are combined through v_readlane.  Result in every lane.  The
+// xor-shuffle form (wave_sum) costs 12 ds_bpermute round trips per double.
+template <int CTRL>
+__device__ __forceinline__ double dpp_mov(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double wave_sum_dpp(double v) {
+  v += dpp_mov<0xB1>(v);    // quad_perm [1,0,3,2]
+  v += dpp_mov<0x4E>(v);    // quad_perm [2,3,0,1]
+  v += dpp_mov<0x141>(v);   // row_half_mirror
+  v += dpp_mov<0x140>(v);   // row_mirror
+  return (readlane(v, 0) + readlane(v, 16)) + (readlane(v, 32) + readlane(v, 48));
+}
+
 template <typename T>
 __device__ __forceinline__ void chol_blocked(cpx<T>* sG, int K) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -303,6 +321,10 @@ __device__ __forceinline__ cpx<T> shfl_c(cpx<T> v, int src) {
 // wave (one load batch per block, address-independent of the solve) so their
 // latency is paid once per block instead of once per column.
 constexpr int kDsJB = 8;
+#ifndef CCSC_DS_BWRED
+#define CCSC_DS_BWRED 0
+#endif
+constexpr bool kDsBwRed = CCSC_DS_BWRED;   // A/B: reduction backward for every NVB
 
 template <typename T, int RPL, int NVB>
 __global__ __launch_bounds__(256) void k_dsolve(const cpx<T>* __restrict__ L,
@@ -385,8 +407,8 @@ __global__ __launch_bounds__(256) void k_dsolve(const cpx<T>* __restrict__ L,
   // column p), wave-reduced.  With several right-hand sides per sweep the
   // reductions dominate and the column-axpy form below is faster; with one the
   // latter's per-lane column walk (64 lines per load) costs more than the
-  // reductions (C2: 22 vs 42 ms per launch).
-  if constexpr (NVB == 1) {
+  // reductions (C2: 22 vs 42 ms per launch, with shuffle reductions).
+  if constexpr (NVB == 1 || kDsBwRed) {
   for (int j1 = K - 1; j1 >= 0; j1 -= kDsJB) {
     cpx<T> lc[kDsJB][RPL];
     T dg[kDsJB];
@@ -402,18 +424,22 @@ __global__ __launch_bounds__(256) void k_dsolve(const cpx<T>* __restrict__ L,
     for (int jj = 0; jj < kDsJB; ++jj) {
       const int j = j1 - jj;
       if (j >= 0) {
-        cpx<T> part = zero;
-#pragma unroll
-        for (int u = 0; u < RPL; ++u) {
-          const int i = lane + 64 * u;
-          if (i > j && i < K) part = cadd(part, cmulc(lc[jj][u], x[0][u]));
-        }
-        part.x = wave_sum(part.x);
-        part.y = wave_sum(part.y);
         const int src = j & 63, tj = j >> 6;
-        if (lane == src) {
-          if (tj == 0) x[0][0] = cscale(csub(x[0][0], part), (T)1 / dg[jj]);
-          else x[0][RPL - 1] = cscale(csub(x[0][RPL - 1], part), (T)1 / dg[jj]);
+        const T inv = (T)1 / dg[jj];
+#pragma unroll
+        for (int v = 0; v < NVB; ++v) {
+          cpx<T> part = zero;
+#pragma unroll
+          for (int u = 0; u < RPL; ++u) {
+            const int i = lane + 64 * u;
+            if (i > j && i < K) part = cadd(part, cmulc(lc[jj][u], x[v][u]));
+          }
+          part.x = wave_sum_dpp(part.x);
+          part.y = wave_sum_dpp(part.y);
+          if (lane == src) {
+            if (tj == 0) x[v][0] = cscale(csub(x[v][0], part), inv);
+            else x[v][RPL - 1] = cscale(csub(x[v][RPL - 1], part), inv);
+          }
         }
       }
     }
