@@ -521,6 +521,268 @@ hipError_t launch_dsolve(const cpx<T>* L, const cpx<T>* h, const cpx<T>* Ch, cpx
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Woodbury form for blocks of ni << K patches (3D/4D: ni = sqrt(n) = 8, K = 49):
+// (A^H A + rho I)^{-1} = (I - A^H M^{-1} A) / rho, M = rho I + A A^H (ni x ni) --
+// the reference's own pinv(rho I + A A^H) form (dP:230-236, L3/L4 precompute),
+// with M factored instead of inverted.  Per f: ni K + ni^2 complex instead of
+// the K(K+1)/2 of the K x K factor, no K^3 factorisation, and a solve of
+// 2 ni K + ni^2 complex MACs per right-hand side instead of K^2.
+// One wave per f, lanes over k (RPL rows per lane); row p of M / L_M lives in
+// lane p.
+// ---------------------------------------------------------------------------
+template <typename T, int RPL>
+__global__ __launch_bounds__(256) void k_gram_wb(const cpx<T>* __restrict__ Zh,
+                                                 const cpx<T>* __restrict__ Bh,
+                                                 cpx<T>* __restrict__ L, cpx<T>* __restrict__ h,
+                                                 int F, int K, int ni, T rho, int NV, int Kp) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int f = blockIdx.x * 4 + wave;
+  if (f >= F) return;
+  const cpx<T> zero = {(T)0, (T)0};
+  cpx<T> a[kWbMaxNi][RPL];
+#pragma unroll
+  for (int p = 0; p < kWbMaxNi; ++p)
+#pragma unroll
+    for (int u = 0; u < RPL; ++u) {
+      const int i = lane + 64 * u;
+      a[p][u] = (p < ni && i < K) ? Zh[((int64_t)p * K + i) * F + f] : zero;
+    }
+  cpx<T>* slot = L + (int64_t)f * Kp;
+#pragma unroll
+  for (int p = 0; p < kWbMaxNi; ++p)
+#pragma unroll
+    for (int u = 0; u < RPL; ++u) {
+      const int i = lane + 64 * u;
+      if (p < ni && i < K) slot[p * K + i] = a[p][u];
+    }
+  // M[p][q] = rho delta_pq + sum_k A[p][k] conj(A[q][k]), q <= p (wave sums,
+  // staged through LDS so that lane p picks up row p with static indices)
+  __shared__ cpx<T> sM[4][kWbMaxNi * kWbMaxNi];
+#pragma unroll
+  for (int p = 0; p < kWbMaxNi; ++p)
+#pragma unroll
+    for (int q = 0; q <= p; ++q) {
+      if (p < ni) {
+        cpx<T> part = zero;
+#pragma unroll
+        for (int u = 0; u < RPL; ++u) part = cadd(part, cmulc(a[q][u], a[p][u]));
+        cpx<T> v = {wave_sum_dpp(part.x), wave_sum_dpp(part.y)};
+        if (p == q) v = {v.x + rho, (T)0};
+        if (lane == 0) sM[wave][p * kWbMaxNi + q] = v;
+      }
+    }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  cpx<T> m[kWbMaxNi];
+#pragma unroll
+  for (int q = 0; q < kWbMaxNi; ++q)
+    m[q] = (lane < ni && q <= lane) ? sM[wave][min(lane, kWbMaxNi - 1) * kWbMaxNi + q] : zero;
+  // right-looking Cholesky M = L_M L_M^H across the lanes
+#pragma unroll
+  for (int j = 0; j < kWbMaxNi; ++j) {
+    if (j < ni) {
+      const T d = sqrt(readlane(m[j].x, j));
+      const T inv = (T)1 / d;
+      if (lane == j) m[j] = {d, (T)0};
+      if (lane > j && lane < ni) m[j] = cscale(m[j], inv);           // L[lane][j]
+#pragma unroll
+      for (int q = 0; q < kWbMaxNi; ++q) {
+        if (q > j && q < ni) {
+          const cpx<T> lq = readlane_c(m[j], q);                      // L[q][j]
+          if (lane >= q && lane < ni) m[q] = csub(m[q], cmul(m[j], cpx<T>{lq.x, -lq.y}));
+        }
+      }
+    }
+  }
+  if (lane < ni) {
+#pragma unroll
+    for (int q = 0; q < kWbMaxNi; ++q)
+      if (q < ni) slot[ni * K + lane * ni + q] = (q <= lane) ? m[q] : zero;
+  }
+  // h[f][uv][k] = sum_p conj(A[p][k]) B[p][uv][f]
+  for (int uv = 0; uv < NV; ++uv) {
+    cpx<T> acc[RPL];
+#pragma unroll
+    for (int u = 0; u < RPL; ++u) acc[u] = zero;
+#pragma unroll
+    for (int p = 0; p < kWbMaxNi; ++p) {
+      if (p < ni) {
+        const cpx<T> b = Bh[((int64_t)p * NV + uv) * F + f];
+#pragma unroll
+        for (int u = 0; u < RPL; ++u) acc[u] = cadd(acc[u], cmulc(a[p][u], b));
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < RPL; ++u) {
+      const int i = lane + 64 * u;
+      if (i < K) h[((int64_t)f * NV + uv) * K + i] = acc[u];
+    }
+  }
+}
+
+template <typename T, int RPL, int NVB>
+__global__ __launch_bounds__(256) void k_dsolve_wb(const cpx<T>* __restrict__ L,
+                                                   const cpx<T>* __restrict__ h,
+                                                   const cpx<T>* __restrict__ Ch,
+                                                   cpx<T>* __restrict__ Dh, int F, int K, T rho,
+                                                   int fgroups, int NV, int ni, int Kp) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int blk = blockIdx.x / fgroups;
+  const int f = (blockIdx.x - blk * fgroups) * 4 + wave;
+  if (f >= F) return;
+  const cpx<T> zero = {(T)0, (T)0};
+  const cpx<T>* slot = L + ((int64_t)blk * F + f) * Kp;
+  cpx<T> a[kWbMaxNi][RPL];
+#pragma unroll
+  for (int p = 0; p < kWbMaxNi; ++p)
+#pragma unroll
+    for (int u = 0; u < RPL; ++u) {
+      const int i = lane + 64 * u;
+      a[p][u] = (p < ni && i < K) ? slot[p * K + i] : zero;
+    }
+  // lane p: row p and column p of L_M, 1 / L_M[p][p]
+  const cpx<T>* lm = slot + ni * K;
+  cpx<T> lrow[kWbMaxNi], lcol[kWbMaxNi];
+  const bool lp = lane < ni;
+#pragma unroll
+  for (int q = 0; q < kWbMaxNi; ++q) {
+    lrow[q] = (lp && q < ni) ? lm[lane * ni + q] : zero;
+    lcol[q] = (lp && q < ni) ? lm[q * ni + lane] : zero;
+  }
+  const T dinv = lp ? (T)1 / lm[lane * ni + lane].x : (T)0;
+  const T irho = (T)1 / rho;
+  for (int uv0 = 0; uv0 < NV; uv0 += NVB) {
+    const int nvc = min(NVB, NV - uv0);
+    cpx<T> r[NVB][RPL], t[NVB];
+#pragma unroll
+    for (int v = 0; v < NVB; ++v) {
+      const int uv = uv0 + v;
+      const cpx<T>* hf = h + (((int64_t)blk * F + f) * NV + uv) * K;
+      const cpx<T>* Cb = Ch + (int64_t)blk * K * NV * F + (int64_t)uv * F;   // [blk][k][uv][F]
+#pragma unroll
+      for (int u = 0; u < RPL; ++u) {
+        const int i = lane + 64 * u;
+        if (v < nvc && i < K) {
+          const cpx<T> c = Cb[(int64_t)i * NV * F + f];
+          const cpx<T> hh = hf[i];
+          r[v][u] = {hh.x + rho * c.x, hh.y + rho * c.y};
+        } else {
+          r[v][u] = zero;
+        }
+      }
+      t[v] = zero;
+    }
+    // t = A r (lane p keeps t_p)
+#pragma unroll
+    for (int p = 0; p < kWbMaxNi; ++p) {
+      if (p < ni) {
+#pragma unroll
+        for (int v = 0; v < NVB; ++v) {
+          cpx<T> part = zero;
+#pragma unroll
+          for (int u = 0; u < RPL; ++u) part = cadd(part, cmul(a[p][u], r[v][u]));
+          const cpx<T> s = {wave_sum_dpp(part.x), wave_sum_dpp(part.y)};
+          if (lane == p) t[v] = s;
+        }
+      }
+    }
+    // M s = t: forward L_M y = t, backward L_M^H s = y (pivots via v_readlane)
+#pragma unroll
+    for (int j = 0; j < kWbMaxNi; ++j) {
+      if (j < ni) {
+        const T dj = readlane(dinv, j);
+#pragma unroll
+        for (int v = 0; v < NVB; ++v) {
+          const cpx<T> yj = cscale(readlane_c(t[v], j), dj);
+          if (lane == j) t[v] = yj;
+          if (lane > j && lane < ni) t[v] = csub(t[v], cmul(lrow[j], yj));
+        }
+      }
+    }
+#pragma unroll
+    for (int j = kWbMaxNi - 1; j >= 0; --j) {
+      if (j < ni) {
+        const T dj = readlane(dinv, j);
+#pragma unroll
+        for (int v = 0; v < NVB; ++v) {
+          const cpx<T> sj = cscale(readlane_c(t[v], j), dj);
+          if (lane == j) t[v] = sj;
+          if (lane < j) t[v] = csub(t[v], cmulc(lcol[j], sj));         // conj(L_M[j][lane])
+        }
+      }
+    }
+    // x = (r - A^H s) / rho
+#pragma unroll
+    for (int p = 0; p < kWbMaxNi; ++p) {
+      if (p < ni) {
+#pragma unroll
+        for (int v = 0; v < NVB; ++v) {
+          const cpx<T> sp = readlane_c(t[v], p);
+#pragma unroll
+          for (int u = 0; u < RPL; ++u) r[v][u] = csub(r[v][u], cmulc(a[p][u], sp));
+        }
+      }
+    }
+#pragma unroll
+    for (int v = 0; v < NVB; ++v) {
+      if (v < nvc) {
+        cpx<T>* Db = Dh + (int64_t)blk * K * NV * F + (int64_t)(uv0 + v) * F;
+#pragma unroll
+        for (int u = 0; u < RPL; ++u) {
+          const int i = lane + 64 * u;
+          if (i < K) Db[(int64_t)i * NV * F + f] = cscale(r[v][u], irho);
+        }
+      }
+    }
+  }
+}
+
+template <typename T>
+hipError_t launch_gram_wb(const cpx<T>* Zh, const cpx<T>* Bh, cpx<T>* L, cpx<T>* h, int F, int K,
+                          int ni, T rho, int NV, hipStream_t st) {
+  if (!woodbury_fits(K, ni)) return hipErrorInvalidValue;
+  const int Kp = K * (K + 1) / 2;
+  const dim3 grid((unsigned)((F + 3) / 4));
+  if (K <= 64)
+    hipLaunchKernelGGL((k_gram_wb<T, 1>), grid, dim3(256), 0, st, Zh, Bh, L, h, F, K, ni, rho, NV,
+                       Kp);
+  else
+    hipLaunchKernelGGL((k_gram_wb<T, 2>), grid, dim3(256), 0, st, Zh, Bh, L, h, F, K, ni, rho, NV,
+                       Kp);
+  return hipGetLastError();
+}
+
+template <typename T, int RPL, int NVB>
+static void dsolve_wb_go(dim3 grid, hipStream_t st, const cpx<T>* L, const cpx<T>* h,
+                         const cpx<T>* Ch, cpx<T>* Dh, int F, int K, T rho, int fgroups, int NV,
+                         int ni) {
+  hipLaunchKernelGGL((k_dsolve_wb<T, RPL, NVB>), grid, dim3(256), 0, st, L, h, Ch, Dh, F, K, rho,
+                     fgroups, NV, ni, K * (K + 1) / 2);
+}
+
+template <typename T>
+hipError_t launch_dsolve_wb(const cpx<T>* L, const cpx<T>* h, const cpx<T>* Ch, cpx<T>* Dh,
+                            int nblocks, int F, int K, int ni, T rho, int NV, hipStream_t st) {
+  if (nblocks <= 0) return hipSuccess;
+  if (!woodbury_fits(K, ni)) return hipErrorInvalidValue;
+  const int fgroups = (F + 3) / 4;
+  const dim3 grid((unsigned)(nblocks * fgroups));
+  if (K <= 64) {
+    if (NV == 1) dsolve_wb_go<T, 1, 1>(grid, st, L, h, Ch, Dh, F, K, rho, fgroups, NV, ni);
+    else dsolve_wb_go<T, 1, 4>(grid, st, L, h, Ch, Dh, F, K, rho, fgroups, NV, ni);
+  } else {
+    if (NV == 1) dsolve_wb_go<T, 2, 1>(grid, st, L, h, Ch, Dh, F, K, rho, fgroups, NV, ni);
+    else dsolve_wb_go<T, 2, 4>(grid, st, L, h, Ch, Dh, F, K, rho, fgroups, NV, ni);
+  }
+  return hipGetLastError();
+}
+
+template hipError_t launch_gram_wb<double>(const cpx<double>*, const cpx<double>*, cpx<double>*,
+                                           cpx<double>*, int, int, int, double, int, hipStream_t);
+template hipError_t launch_dsolve_wb<double>(const cpx<double>*, const cpx<double>*,
+                                             const cpx<double>*, cpx<double>*, int, int, int, int,
+                                             double, int, hipStream_t);
 template hipError_t launch_gram_chol<double>(const cpx<double>*, const cpx<double>*,
                                              cpx<double>*, cpx<double>*, int, int, int, double,
                                              int, hipStream_t);

@@ -456,6 +456,7 @@ struct Session2D {
   int Tn;       // 3D: t extent of the padded grid (1 otherwise)
   int NV, KG;   // views, filter slices per block (K * NV)
   bool is4, is3;
+  bool woodbury;   // D-factor in Woodbury form (woodbury_fits: blocks of ni << K patches)
   int64_t N, nbl, b0, np;
   bool owner0;
   double theta;
@@ -563,6 +564,7 @@ struct Session2D {
     F = (int)g.F();
     SS = s * s * (Tn > 1 ? s : 1);
     Kp = K * (K + 1) / 2;
+    woodbury = woodbury_fits(K, ni);
     NV = p.views[0] * p.views[1];
     KG = K * NV;
     is4 = p.variant == CCSC_L4D;
@@ -862,11 +864,15 @@ struct Session2D {
         fwd_embed(z.as<double>() + (size_t)jl * ni * K * P, G.X, G.Y, Tn, 0,
                   Zh.as<cpx<double>>(), (int64_t)ni * K);
       timed(1, [&] {
-        HIPCHK(launch_gram_chol<double>(Zh.as<cpx<double>>(),
-                                        Bhat.as<cpx<double>>() + (size_t)jl * ni * NV * F,
-                                        L.as<cpx<double>>() + (size_t)jl * F * Kp,
-                                        h.as<cpx<double>>() + (size_t)jl * F * NV * K, F, K,
-                                        ni, p.rho_d, NV, st));
+        const cpx<double>* Bj = Bhat.as<cpx<double>>() + (size_t)jl * ni * NV * F;
+        cpx<double>* Lj = L.as<cpx<double>>() + (size_t)jl * F * Kp;
+        cpx<double>* hj = h.as<cpx<double>>() + (size_t)jl * F * NV * K;
+        if (woodbury)
+          HIPCHK(launch_gram_wb<double>(Zh.as<cpx<double>>(), Bj, Lj, hj, F, K, ni, p.rho_d, NV,
+                                        st));
+        else
+          HIPCHK(launch_gram_chol<double>(Zh.as<cpx<double>>(), Bj, Lj, hj, F, K, ni, p.rho_d,
+                                          NV, st));
       });
     }
     // ---- D iterations (dP:103-134) ----
@@ -876,9 +882,14 @@ struct Session2D {
     for (int id = 0; id < p.max_it_d; ++id) {
       timed(3, [&] { dual_fwd(); });
       timed(2, [&] {
-        HIPCHK(launch_dsolve<double>(L.as<cpx<double>>(), h.as<cpx<double>>(),
-                                     Ch.as<cpx<double>>(), Dh.as<cpx<double>>(), (int)nbl, F, K,
-                                     p.rho_d, NV, st));
+        if (woodbury)
+          HIPCHK(launch_dsolve_wb<double>(L.as<cpx<double>>(), h.as<cpx<double>>(),
+                                          Ch.as<cpx<double>>(), Dh.as<cpx<double>>(), (int)nbl, F,
+                                          K, ni, p.rho_d, NV, st));
+        else
+          HIPCHK(launch_dsolve<double>(L.as<cpx<double>>(), h.as<cpx<double>>(),
+                                       Ch.as<cpx<double>>(), Dh.as<cpx<double>>(), (int)nbl, F, K,
+                                       p.rho_d, NV, st));
       });
       timed(4, [&] { inv_dout(); });
       HIPCHK(launch_supp_reduce<double>(supp.as<double>(), ssum.as<double>(), (int)nbl, KG * SS,

@@ -77,6 +77,20 @@ hipError_t launch_gram_chol(const cpx<T>* Zh, const cpx<T>* Bh, cpx<T>* L, cpx<T
 template <typename T>
 hipError_t launch_dsolve(const cpx<T>* L, const cpx<T>* h, const cpx<T>* Ch, cpx<T>* Dh,
                          int nblocks, int F, int K, T rho, int NV, hipStream_t st);
+// Woodbury form for blocks of few patches (woodbury_fits): per f the slot of
+// Kp = K(K+1)/2 complex holds A (ni x K, row-major) and the Cholesky factor of
+// M = rho I + A A^H (ni x ni dense, row-major, zeros above the diagonal);
+// (A^H A + rho I)^{-1} = (I - A^H M^{-1} A) / rho.  Same h, C, Dh layouts.
+constexpr int kWbMaxNi = 8;
+inline bool woodbury_fits(int K, int ni) {
+  return ni <= kWbMaxNi && 4 * ni <= K && K <= 128 && ni * K + ni * ni <= K * (K + 1) / 2;
+}
+template <typename T>
+hipError_t launch_gram_wb(const cpx<T>* Zh, const cpx<T>* Bh, cpx<T>* L, cpx<T>* h, int F, int K,
+                          int ni, T rho, int NV, hipStream_t st);
+template <typename T>
+hipError_t launch_dsolve_wb(const cpx<T>* L, const cpx<T>* h, const cpx<T>* Ch, cpx<T>* Dh,
+                            int nblocks, int F, int K, int ni, T rho, int NV, hipStream_t st);
 
 // ---- kernels3d.hip: the 3D learner's factored transforms -------------------
 // Spectra [slice][t][F2]; P2 = X*Y plane voxels.  Modes: see kernels3d.hip.

@@ -47,7 +47,10 @@ def _case(variant, sb, psf, K, n, ni, seed):
 
 @pytest.mark.parametrize("variant", ["dp", "dz"])
 @pytest.mark.parametrize("sb,psf,K,n,ni", [((12, 12), 5, 3, 4, 2), ((100, 100), 11, 4, 4, 2),
-                                           ((11, 10), 5, 3, 6, 3)])
+                                           ((11, 10), 5, 3, 6, 3),
+                                           # Woodbury D-factor (ni << K): K <= 64, K > 64, ni = 8
+                                           ((12, 12), 5, 8, 4, 2), ((12, 12), 5, 70, 4, 2),
+                                           ((12, 12), 5, 32, 16, 8)])
 def test_learn_2d_matches_oracle(gpu_ctx, variant, sb, psf, K, n, ni):
     from ccsc_code_iccv2017_amd import learners as E
     b, d0, z0 = _case(variant, sb, psf, K, n, ni, seed=7)
@@ -76,7 +79,8 @@ def test_learn_2d_matches_oracle(gpu_ctx, variant, sb, psf, K, n, ni):
 
 
 @pytest.mark.parametrize("sb,UV,psf,K,n", [((10, 9), 2, 5, 3, 4), ((9, 9), 3, 5, 2, 9),
-                                           ((64, 64), 5, 11, 4, 4)])
+                                           ((64, 64), 5, 11, 4, 4),
+                                           ((10, 9), 2, 5, 8, 4)])     # Woodbury, 4 views
 def test_learn_4d_matches_oracle(gpu_ctx, sb, UV, psf, K, n):
     """4D light-field learner (L4:1-212): spatial-only convolution over U x V views,
     per-view D-solves sharing one factor, diagonal z-solve (Q7), per-slice projection (Q10)."""
@@ -105,7 +109,7 @@ def test_learn_4d_matches_oracle(gpu_ctx, sb, UV, psf, K, n):
 
 @pytest.mark.parametrize("sb,psf,K,n,tol", [((8, 9, 7), 3, 3, 4, 0.0), ((10, 10, 6), 5, 4, 9, 0.0),
                                             ((10, 10, 6), 5, 4, 9, 2e-2),
-                                            ((20, 20, 12), 11, 8, 4, 0.0),
+                                            ((20, 20, 12), 11, 8, 4, 0.0),   # Woodbury
                                             ((64, 64, 32), 11, 2, 1, 0.0)])   # C4 grid 74x74x42
 def test_learn_3d_matches_oracle(gpu_ctx, sb, psf, K, n, tol):
     """3D learner (L3:1-230): plane R2C/C2R + t-direction FFT, Sherman-Morrison z-solve,
