@@ -20,9 +20,10 @@ CCSC_E_UNSUPPORTED = -5
 CCSC_E_STATE = -6
 
 CCSC_DPAR, CCSC_DZPAR, CCSC_L3D, CCSC_L4D, CCSC_HS23 = 0, 1, 2, 3, 4
-ABI_VERSION = 2
+ABI_VERSION = 3
 VERBOSE = {"none": 0, "brief": 1, "all": 2}
 CCSC_FP64, CCSC_FP32 = 0, 1
+DFACTOR = {"auto": 0, "cholesky": 1, "woodbury": 2}
 
 
 class Problem(C.Structure):
@@ -48,6 +49,7 @@ class Problem(C.Structure):
         ("precision", C.c_int32),
         ("trace_objective", C.c_int32),
         ("seed", C.c_uint64),
+        ("dfactor", C.c_int32),
     ]
 
 

@@ -741,7 +741,7 @@ __global__ __launch_bounds__(256) void k_dsolve_wb(const cpx<T>* __restrict__ L,
 template <typename T>
 hipError_t launch_gram_wb(const cpx<T>* Zh, const cpx<T>* Bh, cpx<T>* L, cpx<T>* h, int F, int K,
                           int ni, T rho, int NV, hipStream_t st) {
-  if (!woodbury_fits(K, ni)) return hipErrorInvalidValue;
+  if (!woodbury_ok(K, ni)) return hipErrorInvalidValue;
   const int Kp = K * (K + 1) / 2;
   const dim3 grid((unsigned)((F + 3) / 4));
   if (K <= 64)
@@ -765,7 +765,7 @@ template <typename T>
 hipError_t launch_dsolve_wb(const cpx<T>* L, const cpx<T>* h, const cpx<T>* Ch, cpx<T>* Dh,
                             int nblocks, int F, int K, int ni, T rho, int NV, hipStream_t st) {
   if (nblocks <= 0) return hipSuccess;
-  if (!woodbury_fits(K, ni)) return hipErrorInvalidValue;
+  if (!woodbury_ok(K, ni)) return hipErrorInvalidValue;
   const int fgroups = (F + 3) / 4;
   const dim3 grid((unsigned)(nblocks * fgroups));
   if (K <= 64) {

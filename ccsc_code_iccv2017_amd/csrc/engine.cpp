@@ -306,6 +306,8 @@ static void resolve_problem(ccsc_problem& p) {
   if (p.verbose < CCSC_VERBOSE_NONE || p.verbose > CCSC_VERBOSE_ALL)
     throw Err(CCSC_E_INVALID, "bad verbose");
   if (p.precision != CCSC_FP64 && p.precision != CCSC_FP32) throw Err(CCSC_E_INVALID, "bad precision");
+  if (p.dfactor < CCSC_DFACTOR_AUTO || p.dfactor > CCSC_DFACTOR_WOODBURY)
+    throw Err(CCSC_E_INVALID, "bad dfactor");
   const int r = p.psf / 2;
   for (int i = 0; i < p.ndim; ++i)
     if (p.sb[i] + 2 * r < p.psf) throw Err(CCSC_E_INVALID, "grid smaller than the filter");
@@ -329,6 +331,9 @@ static void check_supported(const ccsc_problem& p, Geom* Gout) {
     throw Err(CCSC_E_UNSUPPORTED, "K * views > 2048 exceeds the gram kernel's RHS budget");
   if (p.precision != CCSC_FP64) throw Err(CCSC_E_UNSUPPORTED, "only CCSC_FP64 is built");
   if (p.K > 110) throw Err(CCSC_E_UNSUPPORTED, "K > 110 exceeds the gram kernel's tile budget");
+  if (p.dfactor == CCSC_DFACTOR_WOODBURY && (p.variant == CCSC_HS23 || !woodbury_ok(p.K, p.ni)))
+    throw Err(CCSC_E_UNSUPPORTED, "the Woodbury D-factor needs ni <= 8 and ni K + ni^2 <= K (K + 1) / 2 "
+                                  "(consensus learners only)");
   const int r = p.psf / 2;
   Geom g;
   std::string why;
@@ -456,7 +461,7 @@ struct Session2D {
   int Tn;       // 3D: t extent of the padded grid (1 otherwise)
   int NV, KG;   // views, filter slices per block (K * NV)
   bool is4, is3;
-  bool woodbury;   // D-factor in Woodbury form (woodbury_fits: blocks of ni << K patches)
+  bool woodbury;   // D-factor in Woodbury form (p.dfactor; AUTO: woodbury_fits, ni << K)
   int64_t N, nbl, b0, np;
   bool owner0;
   double theta;
@@ -564,7 +569,8 @@ struct Session2D {
     F = (int)g.F();
     SS = s * s * (Tn > 1 ? s : 1);
     Kp = K * (K + 1) / 2;
-    woodbury = woodbury_fits(K, ni);
+    woodbury = p.dfactor == CCSC_DFACTOR_WOODBURY ||
+               (p.dfactor == CCSC_DFACTOR_AUTO && woodbury_fits(K, ni));
     NV = p.views[0] * p.views[1];
     KG = K * NV;
     is4 = p.variant == CCSC_L4D;

@@ -81,10 +81,16 @@ hipError_t launch_dsolve(const cpx<T>* L, const cpx<T>* h, const cpx<T>* Ch, cpx
 // Kp = K(K+1)/2 complex holds A (ni x K, row-major) and the Cholesky factor of
 // M = rho I + A A^H (ni x ni dense, row-major, zeros above the diagonal);
 // (A^H A + rho I)^{-1} = (I - A^H M^{-1} A) / rho.  Same h, C, Dh layouts.
+// woodbury_ok: the kernels can hold the form (lanes over k, ni <= 8 rows of A,
+// A and L_M within the K(K+1)/2 slot); woodbury_fits: the AUTO choice, blocks
+// of few patches (ni <= K/4) where the form saves bytes and flops.  The form is
+// the reference's pinv(rho I + A A^H) (dP:230-236); its solve loses digits when
+// ||A||^2 >> rho, which CCSC_DFACTOR_CHOLESKY avoids.
 constexpr int kWbMaxNi = 8;
-inline bool woodbury_fits(int K, int ni) {
-  return ni <= kWbMaxNi && 4 * ni <= K && K <= 128 && ni * K + ni * ni <= K * (K + 1) / 2;
+inline bool woodbury_ok(int K, int ni) {
+  return ni <= kWbMaxNi && K <= 128 && ni * K + ni * ni <= K * (K + 1) / 2;
 }
+inline bool woodbury_fits(int K, int ni) { return woodbury_ok(K, ni) && 4 * ni <= K; }
 template <typename T>
 hipError_t launch_gram_wb(const cpx<T>* Zh, const cpx<T>* Bh, cpx<T>* L, cpx<T>* h, int F, int K,
                           int ni, T rho, int NV, hipStream_t st);

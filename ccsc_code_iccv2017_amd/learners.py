@@ -97,7 +97,8 @@ _VARIANT_FOR = {
 
 def make_problem(variant, b_shape, kernel_size, lambda_residual, lambda_prior, max_it, tol,
                  verbose, *, ni=None, max_it_d=None, max_it_z=None, rho_d=None, rho_z=None,
-                 theta_div=None, trace_objective=False, seed=0, precision="fp64"):
+                 theta_div=None, trace_objective=False, seed=0, precision="fp64",
+                 dfactor="auto"):
     p = L.Problem()
     p.variant = variant
     p.ndim = 3 if variant == L.CCSC_L3D else 2
@@ -128,6 +129,9 @@ def make_problem(variant, b_shape, kernel_size, lambda_residual, lambda_prior, m
     p.precision = L.CCSC_FP64 if precision == "fp64" else L.CCSC_FP32
     p.trace_objective = 1 if trace_objective else 0
     p.seed = int(seed)
+    if dfactor not in L.DFACTOR:
+        raise ValueError(f"dfactor must be one of {sorted(L.DFACTOR)}")
+    p.dfactor = L.DFACTOR[dfactor]
     return p
 
 

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define CCSC_ABI_VERSION 2
+#define CCSC_ABI_VERSION 3
 
 /* status codes */
 #define CCSC_OK 0
@@ -67,6 +67,16 @@ extern "C" {
 #define CCSC_FP64 0
 #define CCSC_FP32 1
 
+/* form of the per-frequency D-step factor (precompute_H_hat_D, dP:221-237).
+ * AUTO: Woodbury when blocks hold few patches (ni <= 8 and 4 ni <= K), else the
+ * K x K Cholesky of A^H A + rho I.  The Woodbury solve (I - A^H M^-1 A) / rho,
+ * M = rho I + A A^H, is the reference's own pinv form; it loses digits when
+ * ||A||^2 >> rho, so CHOLESKY forces the better-conditioned K x K factor.
+ * WOODBURY forces the ni x ni form (ni <= 8, ni K + ni^2 <= K (K + 1) / 2). */
+#define CCSC_DFACTOR_AUTO 0
+#define CCSC_DFACTOR_CHOLESKY 1
+#define CCSC_DFACTOR_WOODBURY 2
+
 typedef struct ccsc_problem {
   int32_t variant;          /* CCSC_DPAR .. CCSC_HS23                               */
   int32_t ndim;             /* spatial dims of b: 2 (2D, 4D) or 3 (3D)              */
@@ -91,6 +101,7 @@ typedef struct ccsc_problem {
   int32_t precision;        /* CCSC_FP64 (reference precision) or CCSC_FP32         */
   int32_t trace_objective;  /* 1: evaluate the objective after every inner iter     */
   uint64_t seed;            /* device RNG seed for d0/z0 when not supplied          */
+  int32_t dfactor;          /* CCSC_DFACTOR_* (0 = AUTO)                            */
 } ccsc_problem;
 
 typedef struct ccsc_outputs {

@@ -41,6 +41,12 @@ def shard(N, rank, world):
 class DzPort:
     """State of the dzParallel learner with tol = 0 (fixed inner counts).
 
+    ``replicate_z0=False`` restates dParallel's iteration instead (dP:89-190:
+    z0 is the full size_z, not one block replicated; pass dP's constants
+    rho_d=500, rho_z=50, theta_div=50, max_it_d=10).  The z-step's filter
+    spectrum is block 1's d-solve output D1^ in both (dP:143 takes fft2(D{1})
+    = D1^ up to round-off, since D{1} = real(ifft2(D1^)) of a Hermitian D1^).
+
     Multi-rank restatement: with ``world > 1`` this instance
     owns the contiguous blocks ``shard(N, rank, world)`` (``b`` is then the
     rank-local patches) and the two exchanges of the engine are injected:
@@ -52,7 +58,7 @@ class DzPort:
 
     def __init__(self, b, d0, z0, lambda_prior, *, ni, rho_d=5000.0, rho_z=1.0, theta_div=1.0,
                  max_it_d=5, max_it_z=10, workers=None, N=None, rank=0, world=1,
-                 allreduce=None, bcast=None):
+                 allreduce=None, bcast=None, replicate_z0=True):
         self.w = workers if workers is not None else (os.cpu_count() or 1)
         b = np.asarray(b, dtype=np.float64)
         psf = d0.shape[0]
@@ -76,9 +82,13 @@ class DzPort:
         self.yD = [np.zeros_like(d) for _ in range(self.Nloc)]
         self.u = np.zeros_like(d)                                    # Pi(Dbar + Udbar), Q2
         z0 = np.asarray(z0, float)
-        self.z = np.concatenate([z0] * self.Nloc, axis=3)          # dZ:44-47
+        self.z = np.concatenate([z0] * self.Nloc, axis=3) if replicate_z0 else z0.copy()  # dZ:44-47 / dP:45
         self.yz = np.zeros_like(self.z)
         self.dhat = None
+
+    def dhat_full(self):
+        """Block 1's filter spectrum on the full X x Y grid (the objective's dup{1})."""
+        return np.fft.fft2(_c2r(self.dhat, self.X, self.Y, self.w), axes=(0, 1))
 
     def outer(self):
         X, Y, K, ni, w = self.X, self.Y, self.K, self.ni, self.w

@@ -50,7 +50,12 @@ def _case(variant, sb, psf, K, n, ni, seed):
                                            ((11, 10), 5, 3, 6, 3),
                                            # Woodbury D-factor (ni << K): K <= 64, K > 64, ni = 8
                                            ((12, 12), 5, 8, 4, 2), ((12, 12), 5, 70, 4, 2),
-                                           ((12, 12), 5, 32, 16, 8)])
+                                           ((12, 12), 5, 32, 16, 8),
+                                           # Cholesky D-factor, 9 <= K <= 64, ni > K / 4
+                                           ((12, 12), 5, 24, 24, 12),
+                                           # the headline block shape K = ni = 100 (C1/C2):
+                                           # 13 Cholesky panels, RPL = 2 d-solve, 2 blocks
+                                           ((12, 12), 5, 100, 200, 100)])
 def test_learn_2d_matches_oracle(gpu_ctx, variant, sb, psf, K, n, ni):
     from ccsc_code_iccv2017_amd import learners as E
     b, d0, z0 = _case(variant, sb, psf, K, n, ni, seed=7)
@@ -141,3 +146,69 @@ def test_learn_3d_matches_oracle(gpu_ctx, sb, psf, K, n, tol):
         for i, (dd, zd) in enumerate(zip(tr_o["d_diff"], tr_o["z_diff"])):
             np.testing.assert_allclose(tr["d_diff"][i, :len(dd)], dd, rtol=1e-6)
             np.testing.assert_allclose(tr["z_diff"][i, :len(zd)], zd, rtol=1e-6)
+
+
+@pytest.mark.parametrize("variant", ["dp", "dz"])
+def test_headline_block_on_110_grid_matches_port(gpu_ctx, variant):
+    """C1/C2's exact block: 100x100 patches (110x110 grid, the compile-time-planned z-step
+    kernel), K = ni = 100, 2 consensus blocks; checked against the half-spectrum port
+    (pinned to the literal oracle by tests/test_oracle.py) since the literal oracle's
+    12,100 pinv's per block take minutes.  Inner counts reduced to keep the CPU side short."""
+    from ccsc_code_iccv2017_amd import learners as E
+    from oracle.ccsc_port import DzPort
+    K, n, ni, mid, miz = 100, 200, 100, 3, 3
+    rng = np.random.default_rng(110)
+    b = rng.standard_normal((100, 100, n))
+    d0 = rng.standard_normal((11, 11, K))
+    z0 = rng.standard_normal((110, 110, K, ni if variant == "dz" else n))
+    init = {"d": d0, "z": z0}
+    if variant == "dz":
+        cst = dict(rho_d=5000.0, rho_z=1.0, theta_div=1.0)
+        fn = E.admm_learn_conv2D_large_dzParallel
+    else:
+        cst = dict(rho_d=500.0, rho_z=50.0, theta_div=50.0)
+        fn = E.admm_learn_conv2D_large_dParallel
+    d_e, z_e, DZ_e, it_e = fn(b, [11, 11, K], 1.0, 1.0, 2, 0.0, "brief", init, ni=ni,
+                              max_it_d=mid, max_it_z=miz, ctx=gpu_ctx)
+    port = DzPort(b, d0, z0, 1.0, ni=ni, max_it_d=mid, max_it_z=miz,
+                  replicate_z0=(variant == "dz"), **cst)
+    port.outer()
+    port.outer()
+    assert _rel(d_e, O.crop_filters(port.D[0], 2, 5)) < 1e-7
+    assert _rel(z_e, port.z) < 1e-7
+    obj = O.objective_2d(port.z, port.dhat_full(), b, 1.0, 1.0, 5)
+    assert abs(it_e["obj_vals_z"][-1] - obj) <= 1e-9 * abs(obj)
+
+
+@pytest.mark.parametrize("rho_d", [500.0, 5000.0])
+def test_dfactor_forms_agree(gpu_ctx, rho_d):
+    """CCSC_DFACTOR_WOODBURY and _CHOLESKY (the two D-factor forms, kernels.hpp
+    woodbury_ok) give the oracle's iterate on the same input, with large-magnitude codes
+    (|Zhat|^2 >> rho_D: the Woodbury solve's cancellation regime)."""
+    from ccsc_code_iccv2017_amd import learners as E
+    b, d0, z0 = _case("dp", (12, 12), 5, 32, 16, 8, seed=23)
+    z0 = 30.0 * z0
+    init = {"d": d0, "z": z0}
+    o = O.learn_2d_dparallel(b, [5, 5, 32], 1.0, 1.0, 2, 0.0, "brief", init, ni=8, rho_d=rho_d,
+                             trace_objective=True)
+    outs = {}
+    for form in ("woodbury", "cholesky"):
+        outs[form] = E.admm_learn_conv2D_large_dParallel(b, [5, 5, 32], 1.0, 1.0, 2, 0.0, "brief",
+                                                         init, ni=8, rho_d=rho_d, dfactor=form,
+                                                         trace_objective=True, ctx=gpu_ctx)
+    for form, e in outs.items():
+        assert _rel(e[0], o[0]) < 1e-7, form
+        assert _rel(e[1], o[1]) < 1e-7, form
+        np.testing.assert_allclose(e[3]["trace"]["obj_z"], np.array(o[4]["obj_z"]), rtol=1e-9)
+    assert _rel(outs["woodbury"][0], outs["cholesky"][0]) < 1e-8
+
+
+def test_dfactor_woodbury_rejected_when_blocks_too_large(gpu_ctx):
+    from ccsc_code_iccv2017_amd import _lib as L
+    from ccsc_code_iccv2017_amd import learners as E
+    b, d0, z0 = _case("dz", (12, 12), 5, 8, 24, 12, seed=3)
+    with pytest.raises(L.CCSCError) as ei:
+        E.admm_learn_conv2D_large_dzParallel(b, [5, 5, 8], 1.0, 1.0, 1, 0.0, "none",
+                                             {"d": d0, "z": z0}, ni=12, dfactor="woodbury",
+                                             ctx=gpu_ctx)
+    assert ei.value.code == L.CCSC_E_UNSUPPORTED

@@ -127,6 +127,43 @@ def test_half_spectrum_port_equals_literal_oracle():
     np.testing.assert_allclose(O.crop_filters(p.D[0], 2, 2), o[0], rtol=0, atol=1e-12)
 
 
+def test_half_spectrum_port_equals_literal_oracle_dparallel():
+    """replicate_z0=False with dP's constants restates dParallel (dP:89-190)."""
+    rng = _rng(16)
+    b = rng.standard_normal((10, 9, 6))
+    d0 = rng.standard_normal((5, 5, 3))
+    z0 = rng.standard_normal((14, 13, 3, 6))
+    o = O.learn_2d_dparallel(b, [5, 5, 3], 1.0, 1.0, 2, 0.0, "none", {"d": d0, "z": z0}, ni=3)
+    p = DzPort(b, d0, z0, 1.0, ni=3, workers=1, rho_d=500.0, rho_z=50.0, theta_div=50.0,
+               max_it_d=10, replicate_z0=False)
+    p.outer()
+    p.outer()
+    np.testing.assert_allclose(p.z, o[1], rtol=0, atol=1e-11)
+    np.testing.assert_allclose(O.crop_filters(p.D[0], 2, 2), o[0], rtol=0, atol=1e-12)
+
+
+@pytest.mark.parametrize("rho", [500.0, 5000.0])
+def test_woodbury_form_conditioning_large_codes(rho):
+    """The reference's pinv(rho I + A A^H) form (dP:230-236) == the K x K inverse at
+    realistic rho_D with large-magnitude code spectra (|A|^2 >> rho): the two D-factor
+    forms of the engine (CCSC_DFACTOR_WOODBURY / _CHOLESKY) solve the same system, the
+    Woodbury one losing ~log10(|A|^2 / rho) digits to cancellation -- still far inside
+    the engine's 1e-7 parity budget at the magnitudes the learners produce."""
+    rng = _rng(17)
+    ni, K = 8, 32
+    for scale in (1.0, 1e2, 1e3):
+        A = scale * (rng.standard_normal((ni, K)) + 1j * rng.standard_normal((ni, K)))
+        b = rng.standard_normal(K) + 1j * rng.standard_normal(K)
+        G = A.conj().T @ A + rho * np.eye(K)
+        x_chol = np.linalg.solve(G, b)
+        M = rho * np.eye(ni) + A @ A.conj().T
+        x_wb = (b - A.conj().T @ np.linalg.solve(M, A @ b)) / rho
+        err = np.linalg.norm(x_wb - x_chol) / np.linalg.norm(x_chol)
+        cond_ratio = np.linalg.norm(A, 2) ** 2 / rho
+        assert err <= 1e-15 * max(1.0, cond_ratio) * 100, (scale, err)
+        assert err < 1e-9
+
+
 def test_dp_objective_decreases():
     rng = _rng(7)
     b = rng.standard_normal((10, 10, 4))
