@@ -30,7 +30,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip table)
-ZKERNEL = "ccsc::k_zsplit"  # the dominant kernel (one z-iteration over the local patches)
+ZKERNEL_PREFIX = "ccsc::k_z"   # the dominant kernel: one z-iteration over the local patches
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_zsplit.json")   # tools/pmc_summary.py --json
 
 
@@ -75,19 +75,39 @@ def cpu_baseline(args):
 
 
 def pmc_traffic(n_local):
-    """HBM bytes per k_zsplit launch from the committed rocprofv3 PMC passes
-    (FETCH_SIZE doubled for 16-B streaming loads on gfx950 and WRITE_SIZE, both
-    kB per dispatch; MI355X_MICROARCH.md "HBM"), scaled to this run's patch count
-    when the profile was taken at another n.  None when no summary is committed."""
+    """HBM bytes per launch of the dominant z-step kernel from the committed rocprofv3
+    PMC passes (FETCH_SIZE doubled for 16-B streaming loads on gfx950 and WRITE_SIZE,
+    both kB per dispatch; MI355X_MICROARCH.md "HBM"), scaled to this run's patch count
+    when the profile was taken at another n.  Returns (bytes, source, kernel, stale):
+    stale is True when the kernel sources changed since the summary was taken
+    (tools/pmc_summary.py records their hash).  (None, ...) without a summary."""
+    from tools.pmc_summary import source_hash
     try:
         d = json.load(open(PMC_SUMMARY))
     except (OSError, ValueError):
-        return None, None
-    k = next((v for name, v in d.items() if name.startswith(ZKERNEL + "<")), None)
-    if not k or "FETCH_SIZE" not in k or "WRITE_SIZE" not in k:
-        return None, None
+        return None, None, None, None
+    cands = [(v.get("avg_s", 0) * v.get("dispatches", 0), name, v) for name, v in d.items()
+             if name.startswith(ZKERNEL_PREFIX) and isinstance(v, dict)]
+    if not cands:
+        return None, None, None, None
+    _, name, k = max(cands)
+    if "FETCH_SIZE" not in k or "WRITE_SIZE" not in k:
+        return None, None, None, None
     per = (2.0 * k["FETCH_SIZE"] + k["WRITE_SIZE"]) * 1024.0 * n_local / d.get("n_local", n_local)
-    return per, os.path.relpath(PMC_SUMMARY, ROOT)
+    stale = d.get("src_sha256") != source_hash()
+    return per, os.path.relpath(PMC_SUMMARY, ROOT), name, stale
+
+
+def step_alg_bytes(n, K, ni, P, F, mid, miz, s=8, V=1):
+    """algorithmic bytes of one outer iteration (precompute + max_it_d
+    d-iterations + max_it_z z-iterations), c = 2 s, N = n / ni blocks."""
+    c = 2 * s
+    N = n // ni
+    s_app = min(c * F * K * (K + 1) // 2, c * F * (ni * K + ni * (ni + 1) // 2))
+    z_it = n * K * (4 * s * P + 4 * c * F) + n * c * F * V
+    d_it = N * (4 * s * P * V * K + 5 * c * F * V * K + s_app)
+    pre = N * (c * F * K * ni + c * F * V * ni + s_app + c * F * V * K)
+    return pre + mid * d_it + miz * z_it
 
 
 def main():
@@ -139,6 +159,7 @@ def main():
     ctx = E.Context(local, rank, world, uid)
     sess = E.Session(ctx, p, b)
     del b
+    obj_start = sess.objective()        # sanity: the learner must decrease it (outside timing)
 
     def barrier():
         if world > 1:
@@ -171,12 +192,26 @@ def main():
     obj = sess.objective()
     if rank == 0:
         log(f"per-kernel (rank 0): {json.dumps(kstats)}")
-        log(f"objective after {sess.outer} outer iterations: {obj:.6e}; tim_vals {it['tim_vals']}")
+        log(f"objective {obj_start:.6e} at start, {obj:.6e} after {sess.outer} outer iterations; "
+            f"tim_vals {it['tim_vals']}")
 
+    if rank == 0 and not (np.isfinite(obj) and obj < obj_start):
+        log(f"WARNING: objective did not decrease: {obj_start:.6e} -> {obj:.6e}")
     avg_ms = zms / max(launches, 1)
     achieved = zbytes / (avg_ms * 1e-3) / 1e9 if launches else 0.0
-    traffic, traffic_src = pmc_traffic(n_local)
+    traffic, traffic_src, traffic_kernel, traffic_stale = pmc_traffic(n_local)
+    if traffic_stale:
+        log(f"WARNING: {traffic_src} predates the current kernel sources (traffic is stale)")
+    r = psf // 2
+    Pg, Fg = (100 + 2 * r) ** 2, (100 + 2 * r) * ((100 + 2 * r) // 2 + 1)
+    # compulsory HBM bytes of the fused z-step per launch: the state a read + written once
+    # (2 s P per slice) and the per-patch w read + written and B^ read (3 c F per patch)
+    compulsory = n_local * (K * 2 * 8 * Pg + 3 * 16 * Fg)
+    step_bytes = step_alg_bytes(args.n, K, ni, Pg, Fg, p.max_it_d, p.max_it_z)
+    step_s = dt / args.steps
     result = {
+        "objective_start": obj_start,
+        "objective_end": obj,
         "metric": "ADMM outer iters/sec x patches (whole node)",
         "value": args.n * args.steps / dt,
         "unit": "patch-iters/s",
@@ -199,15 +234,27 @@ def main():
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "k_zsplit (C2R of the w term + prox/dual + R2C + per-bin reduction, one WG/patch)",
+            "kernel": "z-step (C2R of the w term + prox/dual + R2C + per-bin reduction, one WG/patch)",
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
             "traffic_source": traffic_src,
+            "traffic_kernel": traffic_kernel,
+            "traffic_stale": traffic_stale,
             "alg_bytes_per_launch": zbytes,
             "avg_launch_ms": avg_ms,
+            # the fused kernel moves less than §8(d)'s staged model: its own compulsory bytes
+            # and the PMC-measured DRAM bytes against the same peak
+            "compulsory_bytes_per_launch": compulsory,
+            "frac_compulsory": compulsory / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if launches else None,
+            "frac_dram": (traffic / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
+                          if (traffic and launches) else None),
+            "observed_limiter": "fp64 VALU + LDS (slice FFTs in LDS, DESIGN.md §7)",
+            # whole outer iteration: §8(d) bytes of every stage / step time / node peak
+            "step_alg_bytes": step_bytes,
+            "step_frac": step_bytes / step_s / 1e9 / (HBM_PEAK_GBS * world),
         },
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

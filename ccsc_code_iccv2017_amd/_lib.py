@@ -139,6 +139,14 @@ def lib():
             raise ImportError(
                 f"{LIB_PATH} is missing: build it with `python -m ccsc_code_iccv2017_amd.build` "
                 "(the HIP engine has no CPU fallback)")
+        # One HIP runtime per process: PyTorch ships its own libamdhip64.so.7 (the soname of
+        # /opt/rocm's).  With torch loaded first libccsc binds to that copy; loaded the
+        # other way round the process maps both, and torch's then sees no GPU ("No HIP
+        # GPUs are available") once libccsc has initialised the device.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = C.CDLL(str(LIB_PATH))
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(L, name)

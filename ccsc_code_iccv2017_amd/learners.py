@@ -168,6 +168,8 @@ class Session:
     def __init__(self, ctx: Context, p: L.Problem, b, d0=None, z0=None, smooth_init=None):
         self.ctx = ctx
         self.p = resolve(p)
+        eb = L.errbuf()
+        L.check(L.lib().ccsc_supported(C.byref(self.p), eb, len(eb)), eb)   # CCSC_E_UNSUPPORTED
         self._b = _f64(b)
         self._d0 = _f64(d0)
         self._z0 = _f64(z0)

@@ -2,7 +2,22 @@
 """Summarise rocprofv3 --pmc CSVs per kernel: mean counter value per dispatch."""
 import collections
 import csv
+import hashlib
+import os
 import sys
+
+CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                    "ccsc_code_iccv2017_amd", "csrc")
+
+
+def source_hash():
+    """sha256 over the kernel sources: a PMC summary taken from other sources is stale."""
+    h = hashlib.sha256()
+    for f in sorted(os.listdir(CSRC)):
+        if f.endswith((".hip", ".hpp", ".cpp")):
+            h.update(f.encode())
+            h.update(open(os.path.join(CSRC, f), "rb").read())
+    return h.hexdigest()
 
 
 def summarize(path, match=("ccsc::",)):
@@ -30,7 +45,8 @@ if __name__ == "__main__":
         # --json OUT N_LOCAL csv...: one merged {kernel: {counter: mean per dispatch}} file
         import json
         out, n_local = args[1], int(args[2])
-        merged = {"n_local": n_local, "units": "FETCH_SIZE/WRITE_SIZE in kB per dispatch (raw)"}
+        merged = {"n_local": n_local, "units": "FETCH_SIZE/WRITE_SIZE in kB per dispatch (raw)",
+                  "src_sha256": source_hash()}
         for p in args[3:]:
             for k, d in summarize(p).items():
                 merged.setdefault(k, {}).update(d)
