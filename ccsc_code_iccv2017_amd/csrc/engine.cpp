@@ -17,6 +17,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <limits>
@@ -400,9 +401,9 @@ namespace ccsc {
 // memory plan shared by ccsc_plan_bytes and the session
 struct Plan2D {
   int64_t np, nbl, b0;
-  size_t z, yz, cbuf, W, dhw, D, yD, Bhat, b, L, h, Ch, Dh, Zh, E, misc;
+  size_t z, yz, cbuf, W, dhw, D, yD, Bhat, b, L, h, Ch, Dh, Zh, E, zl, misc;
   size_t total() const {
-    return z + yz + cbuf + W + dhw + D + yD + Bhat + b + L + h + Ch + Dh + Zh + E + misc;
+    return z + yz + cbuf + W + dhw + D + yD + Bhat + b + L + h + Ch + Dh + Zh + E + zl + misc;
   }
 };
 
@@ -436,6 +437,9 @@ static Plan2D plan2d(const ccsc_problem& p, const Geom& g, int rank, int nranks)
   m.Zh = (size_t)p.ni * K * F * 16;
   // 4D: view correlations E; 3D: spectra of the z-step's plane/t transforms
   m.E = (is4 || is3) ? m.np * K * F * 16 : 0;
+  // register-line z-step (zline.hip, 110 grid): B^ and the two filter spectra in
+  // bin-slot order, sden in bin-slot order
+  m.zl = (!is4 && !is3 && zline_grid(G)) ? m.np * F * 16 + 2 * K * F * 16 + F * 8 : 0;
   m.misc = (2 * K * NV * F) * 16 + F * 8 + (m.nbl + 2) * K * NV * SS * 8 * 2 +
            (4 * m.np * NV * g.Tn + 4 * K * NV * g.Tn + 64) * 8 + (size_t)(G.ntw + g.Gt.ntw) * 16 +
            (is3 ? F * 16 + P * 8 : 0);
@@ -476,6 +480,12 @@ struct Session2D {
   DevBuf W, dhatw;
   int zmode = 0;
   const cpx<double>* dw = nullptr;
+  // zmode 2 = register-line z-step (zline.hip, the 110 grid with tol = 0): `z` holds a
+  // in state order, W the last w in bin-slot order solved with dws (dhs or dhws);
+  // Bhs / dhs / sdens: B^, the current filter spectrum and sden in bin-slot order.
+  bool zl_on = false;
+  DevBuf Bhs, dhs, dhws, sdens, tw110;
+  const cpx<double>* dws = nullptr;
   DevBuf twt, oacc, odz;   // 3D: t-FFT twiddles, objective scratch
 
   // host-side log
@@ -607,6 +617,19 @@ struct Session2D {
     if (m.cbuf) cbuf.alloc(m.cbuf);
     if (m.W) W.alloc(m.W);
     if (m.dhw) dhatw.alloc(m.dhw);
+    {
+      const char* ev = std::getenv("CCSC_ZLINE");   // A/B switch: CCSC_ZLINE=0 keeps k_zsplit
+      zl_on = m.zl && !(p.tol > 0) && !(ev && ev[0] == '0');
+    }
+    if (zl_on) {
+      Bhs.alloc((size_t)np * F * 16);
+      dhs.alloc((size_t)K * F * 16);
+      dhws.alloc((size_t)K * F * 16);
+      sdens.alloc((size_t)F * 8);
+      auto t110 = zline_twiddles();
+      tw110.alloc(t110.size() * 16);
+      HIPCHK(hipMemcpy(tw110.p, t110.data(), tw110.bytes, hipMemcpyHostToDevice));
+    }
     D.alloc(m.D);
     yD.alloc(m.yD);
     Usup.alloc((size_t)KG * SS * 8);
@@ -630,6 +653,8 @@ struct Session2D {
     HIPCHK(hipMemcpy(bdev.p, b, m.b, hipMemcpyHostToDevice));
     fwd_embed(bdev.as<double>(), (int)p.sb[0], (int)p.sb[1], is3 ? (int)p.sb[2] : 1, r,
               Bhat.as<cpx<double>>(), np * NV);
+    if (zl_on)
+      HIPCHK(launch_to_slots<double>(Bhat.as<cpx<double>>(), Bhs.as<cpx<double>>(), np, st));
     // filters: init.d or device RNG (dP:38-39; 4D: [psf,psf,U,V,K], L4:39-40; 3D: psf^3, L3:39-40)
     DevBuf d0dev;
     const size_t nd0 = (size_t)SS * KG;
@@ -758,6 +783,15 @@ struct Session2D {
       HIPCHK(launch_plane_inv<double>(1, C, z.as<double>(), nullptr, nullptr,
                                       tol_on ? znorm.as<double>() : nullptr, 0, 1.0, r, np * K,
                                       Tn, twc, G, st));
+    } else if (zl_on) {
+      // register-line z-step (zline.hip): mode 0 reads (z, y) and leaves a in state order
+      HIPCHK(launch_zline<double>(z.as<double>(), z.as<double>(), z.as<double>(), yz.as<double>(),
+                                  W.as<cpx<double>>(), Bhs.as<cpx<double>>(),
+                                  zmode == 2 ? dws : dhs.as<cpx<double>>(), dhs.as<cpx<double>>(),
+                                  sdens.as<double>(), tw110.as<cpx<double>>(), np, K, theta,
+                                  zmode == 2 ? 2 : 0, st));
+      zmode = 2;
+      dws = dhs.as<cpx<double>>();
     } else if (!tol_on) {
       // one pass per patch over the pre-threshold state a (zsplit.hip): `z` holds a
       HIPCHK(launch_zsplit<double>(z.as<double>(), z.as<double>(), yz.as<double>(),
@@ -782,6 +816,14 @@ struct Session2D {
   // state a -> (z, y) materialised in place (objective, outputs)
   void materialize_z() {
     if (zmode == 0) return;
+    if (zmode == 2) {   // state order -> natural a in yz, then (z, y) from it
+      HIPCHK(launch_state_to_nat<double>(z.as<double>(), yz.as<double>(), np * K, st));
+      HIPCHK(launch_zmat<double>(yz.as<double>(), yz.as<double>(), W.as<cpx<double>>(), dws,
+                                 z.as<double>(), nullptr, nullptr, np, tw.as<cpx<double>>(), G, K,
+                                 theta, st, true));
+      zmode = 0;
+      return;
+    }
     HIPCHK(launch_zmat<double>(z.as<double>(), yz.as<double>(), W.as<cpx<double>>(), dw,
                                z.as<double>(), nullptr, nullptr, np, tw.as<cpx<double>>(), G, K,
                                theta, st));
@@ -863,9 +905,9 @@ struct Session2D {
     for (int64_t jl = 0; jl < nbl; ++jl) {
       if (zmode)  // fft2(z) of the state a: fft2(u - y) + XY conj(dw) w, u = soft(a)
         HIPCHK(launch_zhat_split<double>(z.as<double>() + (size_t)jl * ni * K * P,
-                                         W.as<cpx<double>>() + (size_t)jl * ni * F, dw,
-                                         Zh.as<cpx<double>>(), ni, tw.as<cpx<double>>(), G, K,
-                                         theta, st));
+                                         W.as<cpx<double>>() + (size_t)jl * ni * F,
+                                         zmode == 2 ? dws : dw, Zh.as<cpx<double>>(), ni,
+                                         tw.as<cpx<double>>(), G, K, theta, st, zmode == 2));
       else
         fwd_embed(z.as<double>() + (size_t)jl * ni * K * P, G.X, G.Y, Tn, 0,
                   Zh.as<cpx<double>>(), (int64_t)ni * K);
@@ -926,15 +968,23 @@ struct Session2D {
       if (tol_on && dd < p.tol) break;  // dP:130-132
     }
     // ---- Z precompute (dP:143-144): d = Dhat of block 1 ----
-    if (zmode && dw == dhat.as<cpx<double>>()) {  // keep the spectrum w was solved with
+    if (zmode == 1 && dw == dhat.as<cpx<double>>()) {  // keep the spectrum w was solved with
       std::swap(dhat.p, dhatw.p);
       dw = dhatw.as<cpx<double>>();
+    }
+    if (zmode == 2 && dws == dhs.as<cpx<double>>()) {
+      std::swap(dhs.p, dhws.p);
+      dws = dhws.as<cpx<double>>();
     }
     if (owner0) HIPCHK(hipMemcpyAsync(dhat.p, Dh.p, (size_t)KG * F * 16, hipMemcpyDeviceToDevice, st));
     bcast0(dhat.as<double>(), (size_t)2 * KG * F);
     // s(f) = sum over filters (and views, L4:277,330) of |dhat|^2
     HIPCHK(launch_sden<double>(dhat.as<cpx<double>>(), sden.as<double>(), F, KG, p.rho_z,
                                1.0 / (double)P, st));
+    if (zl_on) {
+      HIPCHK(launch_to_slots<double>(dhat.as<cpx<double>>(), dhs.as<cpx<double>>(), K, st));
+      HIPCHK(launch_to_slots_real<double>(sden.as<double>(), sdens.as<double>(), st));
+    }
     if (is4)   // L4:327 first term, constant over the z-iterations
       HIPCHK(launch_view_corr<double>(dhat.as<cpx<double>>(), Bhat.as<cpx<double>>(),
                                       E.as<cpx<double>>(), np, F, K, NV, st));

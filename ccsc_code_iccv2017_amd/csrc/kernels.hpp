@@ -3,6 +3,8 @@
 
 #include "fft.hpp"
 
+#include <vector>
+
 namespace ccsc {
 
 size_t slice_smem_bytes(const Grid2D& G, size_t tsize);
@@ -56,14 +58,33 @@ hipError_t launch_zsplit(const T* A, T* Ao, const T* Yz, cpx<T>* W, const cpx<T>
                          const cpx<T>* dcorr, const cpx<T>* dhat, const T* sden, int64_t npatch,
                          const cpx<T>* tw, const Grid2D& G, int K, T theta, int mode,
                          hipStream_t st);
+// wslot: W and dcorr in bin-slot order (zline state); astate: A in state order.
 template <typename T>
 hipError_t launch_zmat(const T* As, T* Yz, const cpx<T>* W, const cpx<T>* dcorr, T* Zd,
                        const T* zold, T* znorm, int64_t npatch, const cpx<T>* tw, const Grid2D& G,
-                       int K, T theta, hipStream_t st);
+                       int K, T theta, hipStream_t st, bool wslot = false);
 template <typename T>
 hipError_t launch_zhat_split(const T* A, const cpx<T>* W, const cpx<T>* dcorr, cpx<T>* dst,
                              int64_t npatch, const cpx<T>* tw, const Grid2D& G, int K, T theta,
-                             hipStream_t st);
+                             hipStream_t st, bool zline_order = false);
+
+// ---- zline.hip: register-line z-iteration on the 110 x 110 grid -------------
+// State a in "state order" and w, B^, d^, sden in "bin-slot order" (zline.hpp).
+// mode 0: (z, y) materialised in Zn / Yn (natural layout); mode 2: state in A.
+bool zline_grid(const Grid2D& G);
+size_t zline_smem_bytes();
+std::vector<cpx<double>> zline_twiddles();
+template <typename T>
+hipError_t launch_zline(const T* A, T* Ao, const T* Zn, const T* Yn, cpx<T>* W, const cpx<T>* Bs,
+                        const cpx<T>* dcorr, const cpx<T>* dhat, const T* sden,
+                        const cpx<T>* tw110, int64_t npatch, int K, T theta, int mode,
+                        hipStream_t st);
+template <typename T>
+hipError_t launch_to_slots(const cpx<T>* src, cpx<T>* dst, int64_t count, hipStream_t st);
+template <typename T>
+hipError_t launch_to_slots_real(const T* src, T* dst, hipStream_t st);
+template <typename T>
+hipError_t launch_state_to_nat(const T* st_, T* nat, int64_t count, hipStream_t st);
 
 // ---- dstep.hip ------------------------------------------------------------
 // Per frequency f of one block: G = A^H A + rho I (A = ni x K code spectra),

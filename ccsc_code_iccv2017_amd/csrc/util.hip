@@ -35,10 +35,17 @@ __global__ void k_randn(T* __restrict__ out, int64_t count, uint64_t seed, uint6
 
 template <typename T>
 hipError_t launch_randn(T* out, int64_t count, uint64_t seed, uint64_t offset, hipStream_t st) {
-  if (count <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_randn<T>, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, st, out,
-                     count, seed, offset);
-  return hipGetLastError();
+  // chunks of 2^30 elements: one dispatch holds at most 2^32 work-items (dP's z0 at
+  // C2 is 1.2e10 values)
+  constexpr int64_t kChunk = int64_t(1) << 30;
+  for (int64_t c0 = 0; c0 < count; c0 += kChunk) {
+    const int64_t n = count - c0 < kChunk ? count - c0 : kChunk;
+    hipLaunchKernelGGL(k_randn<T>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, out + c0,
+                       n, seed, offset + (uint64_t)c0);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 // D[rep][k][y][x] = d0(i, j, k) at x = (i - r) mod X, y = (j - r) mod Y; zero elsewhere.

@@ -1,0 +1,369 @@
+// Register-line z-iteration of the 2D learners on the 110 x 110 grid of C1/C2
+// (gfx950): the same math as k_zsplit (zsplit.hip; reference dP:150-154 with
+// solve_conv_term_Z dP:278-303, dZ:151-157, 283-308), re-laid out so that the
+// slice transforms live in registers and LDS only carries transposes.
+//
+// Every 110-point line transform is 110 = 10 x 11, split over the lanes of one
+// wave (five lines per wave):
+//   layout A ("time"): 10 lanes per line, lane n1 holds elements n1 + 10 n2,
+//                       n2 = 0..10 (11 complex registers);
+//   layout B ("freq"): 11 lanes per line, lane k2 holds elements k2 + 11 k1,
+//                       k1 = 0..9 (10 complex registers).
+//   forward A -> B:  DFT-11 over the registers, twiddle W_110^(n1 k2), a
+//                    wave-local transpose through LDS, DFT-10 over the registers;
+//   inverse B -> A:  the mirror image (conjugate twiddles).
+// A slice's 2D transforms are then y-lines (the 56 half-spectrum columns) and
+// x-lines (the 55 row pairs packed as complex, two-for-one), joined by one
+// workgroup-wide transpose buffer T [110 rows][57 complex] per direction change:
+//
+//   P1  y-C2R:  bins conj(dw_k) w (layout B, read straight from global in bin-slot
+//       order) -> inverse -> T[y][x']
+//   P2  barrier
+//   P3  x-C2R:  Hermitian rebuild of row pair j from T -> inverse -> layout A of
+//       the row pair = corr at (2j, x), (2j+1, x)
+//   P4  elementwise in registers: a' = soft(a) + corr (stored), c = u - y
+//   P5  x-R2C:  forward -> Z_j into T (rows 2j, 2j+1 of the pair)
+//   P6  barrier
+//   P7  y-R2C loads: two-for-one separation while reading the columns
+//   P8  barrier
+//   P9  forward of the columns -> bins C_k (layout B) -> acc += dhat_k C_k
+//
+// so the per-slice LDS traffic is four wave-local transposes and two
+// workgroup transposes (the Stockham form of k_zsplit made ten passes through
+// the slice), the elementwise stage and the bin accumulation never touch LDS,
+// and a slice costs four barriers instead of nineteen.  Wave-local exchanges
+// reuse the wave's own region of T (the columns of its y-lines, the rows of its
+// x-lines), which no other wave touches between the barriers.
+//
+// Layouts in HBM (engine-internal, z-step only):
+//   state a:    "state order", per (patch, filter) slice 6050 (row 2j, row 2j+1)
+//               pairs, pair n2*550 + j*10 + n1 holds x = n1 + 10 n2 (zl::state_off);
+//   w, B^, d^:  "bin-slot order" per 6160-bin spectrum, slot k1*616 + c*11 + k2
+//               holds bin (x' = c, y = k2 + 11 k1) (zl::bin_slot) -- lane-contiguous,
+//               so every per-slice global access is a coalesced 16-B stream.
+// k_zmat / k_zhat_split (zsplit.hip) read these orders; k_state_to_nat and
+// k_to_slots convert.
+#include "fft_fixed.hpp"
+#include "slice.hpp"
+#include "zline.hpp"
+
+#include <vector>
+
+namespace ccsc {
+
+
+template <typename T>
+__device__ __forceinline__ T soft_l(T a, T theta) {
+  return (fabs(a) > theta) ? a - copysign(theta, a) : (T)0;
+}
+
+__device__ __forceinline__ void wave_lds_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Forward 110-point transform of one line, layout A (v[n2], lane n1 = s < 10)
+// -> layout B (out[k1], lane k2 = s <= 10).  E: the line's 110 exchange slots,
+// slot i at E[i * ES].  tw: W_110^m in LDS.
+// Idle lanes (lane 10 of a line in layout A, lanes 55..63, the clamped lines of the
+// last wave) run on clamped indices and so duplicate a real lane exactly: their
+// LDS and global stores write the same value to the same address, no guards.
+template <typename T, int ES>
+__device__ __forceinline__ void fwd_line(cpx<T> (&v)[11], cpx<T> (&out)[10], cpx<T>* E,
+                                         const cpx<T>* tw, int s) {
+  const int sa = min(s, 9);
+  dft_sink<T, 11, -1>(v, [&](int k2, cpx<T> val) {
+    if (k2 > 0) val = cmul(val, tw[sa * k2]);
+    E[(sa * 11 + k2) * ES] = val;
+  });
+  wave_lds_fence();
+  cpx<T> in[10];
+#pragma unroll
+  for (int n1 = 0; n1 < 10; ++n1) in[n1] = E[(n1 * 11 + s) * ES];
+  dft_sink<T, 10, -1>(in, [&](int k1, cpx<T> val) { out[k1] = val; });
+}
+
+// Inverse (unnormalised) 110-point transform, layout B (in[k1], lane k2 = s)
+// -> layout A (out[n2], lane n1 = s < 10).
+template <typename T, int ES>
+__device__ __forceinline__ void inv_line(cpx<T> (&in)[10], cpx<T> (&out)[11], cpx<T>* E,
+                                         const cpx<T>* tw, int s) {
+  dft_sink<T, 10, +1>(in, [&](int n1, cpx<T> val) {
+    if (n1 > 0) val = cmulc(tw[s * n1], val);   // conj(W_110^(n1 k2)) val
+    E[(n1 * 11 + s) * ES] = val;
+  });
+  wave_lds_fence();
+  const int sa = min(s, 9);
+  cpx<T> v[11];
+#pragma unroll
+  for (int k2 = 0; k2 < 11; ++k2) v[k2] = E[(sa * 11 + k2) * ES];
+  dft_sink<T, 11, +1>(v, [&](int n2, cpx<T> val) { out[n2] = val; });
+}
+
+// 16-B global access at a 32-bit byte offset from a wave-uniform base (saddr form:
+// SGPR base + one VGPR offset, no 64-bit VGPR address per access).
+template <typename V>
+__device__ __forceinline__ V zld(const void* base, uint32_t boff) {
+  return *reinterpret_cast<const V*>(reinterpret_cast<const char*>(base) + boff);
+}
+template <typename V>
+__device__ __forceinline__ void zst(void* base, uint32_t boff, V v) {
+  *reinterpret_cast<V*>(reinterpret_cast<char*>(base) + boff) = v;
+}
+// an opaque copy of a lane index: per-lane address math is redone where it is used
+// instead of being hoisted out of the slice loop into (spilled) registers
+__device__ __forceinline__ int fresh(int v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
+// One workgroup per patch, loop over its K filter slices.  MODE 0: Zn / Yn hold
+// the materialised (z, y) in natural layout (a = z + y, no corr term); MODE 2:
+// A holds the state in state order and W the previous w (bin-slot order) solved
+// with dcorr.  Out: Ao <- a' (state order; Ao may alias A, or Zn in mode 0),
+// W <- w.  Bs, dcorr, dhat, sden in bin-slot order.
+template <typename T, int MODE>
+__global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn, const T* Yn,
+                                                  cpx<T>* __restrict__ W,
+                                                  const cpx<T>* __restrict__ Bs,
+                                                  const cpx<T>* __restrict__ dcorr,
+                                                  const cpx<T>* __restrict__ dhat,
+                                                  const T* __restrict__ sden,
+                                                  const cpx<T>* __restrict__ twg, int K, T theta) {
+  using V2 = typename vec2_t<T>::type;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  cpx<T>* sT = reinterpret_cast<cpx<T>*>(smem);
+  cpx<T>* sTw = sT + zl::TSZ;
+  for (int i = threadIdx.x; i < zl::NTW; i += zl::NT) sTw[i] = twg[i];
+  const int64_t p = blockIdx.x;
+  cpx<T> acc[10];
+#pragma unroll
+  for (int i = 0; i < 10; ++i) acc[i] = {(T)0, (T)0};
+  const cpx<T>* Wp = W + p * zl::F;
+  // the last wave owns one y-line and no x-line (55 row pairs = 11 waves of 5)
+  const bool xwave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6) < 11;
+  __syncthreads();   // twiddles
+
+  for (int k = 0; k < K; ++k) {
+    // lane roles, recomputed per slice from an opaque thread index (see fresh())
+    const int tid = fresh((int)threadIdx.x);
+    const int wave = tid >> 6, lane = tid & 63;
+    const int l = min(lane / 11, 4);   // line within the wave (lanes 55..63 alias line 4)
+    const int s = lane - 11 * l;       // n1 (layout A, < 10) or k2 (layout B); >= 11 idle
+    const int sb = min(s, 10), sa = min(s, 9);
+    const int c = min(5 * wave + l, 55);   // y-line (column)
+    const int j = min(5 * wave + l, 54);   // x-line (row pair)
+    cpx<T>* Ey = sT + c;                                       // column c: slot i at row i
+    cpx<T>* Ex = sT + 10 * min(wave, 10) * zl::RS + l * 110;   // the wave's rows, line l
+    const int64_t sl = (p * K + k) * zl::P;
+    cpx<T> corr[11];
+    if constexpr (MODE == 2) {
+      // ---- P1: y-C2R of conj(dcorr_k) w from bins to T[y][c] ----
+      const cpx<T>* dk = dcorr + (int64_t)k * zl::F;
+      const uint32_t bo = (uint32_t)(c * 11 + sb) * 16u;
+      cpx<T> b[10];
+#pragma unroll
+      for (int k1 = 0; k1 < 10; ++k1)
+        b[k1] = cmulc(zld<cpx<T>>(dk, bo + k1 * 616 * 16), zld<cpx<T>>(Wp, bo + k1 * 616 * 16));
+      cpx<T> yt[11];
+      inv_line<T, zl::RS>(b, yt, Ey, sTw, sb);
+#pragma unroll
+      for (int n2 = 0; n2 < 11; ++n2) sT[(sa + 10 * n2) * zl::RS + c] = yt[n2];
+      lds_sync();   // P2
+      // ---- P3: x-C2R of row pair j: Z(x) = R_2j(x) + i R_2j+1(x), Hermitian ext. ----
+      if (xwave) {
+        const int s3 = fresh(sb);
+        cpx<T> zb[10];
+        const cpx<T>* r0 = sT + 2 * j * zl::RS;
+#pragma unroll
+        for (int k1 = 0; k1 < 10; ++k1) {
+          const int x = s3 + 11 * k1;
+          const bool hi = x >= zl::Xh;
+          const int cc = hi ? zl::X - x : x;
+          cpx<T> a = r0[cc], bb = r0[zl::RS + cc];
+          const T sg = hi ? (T)-1 : (T)1;
+          a.y *= sg;
+          bb.y *= sg;
+          zb[k1] = {a.x - bb.y, a.y + bb.x};
+        }
+        inv_line<T, 1>(zb, corr, Ex, sTw, s3);
+      }
+    }
+    // ---- P4: elementwise on (row 2j, row 2j+1) at x = n1 + 10 n2 ----
+    cpx<T> zc[11];
+    V2 av[11];
+    const uint32_t po = (uint32_t)(j * 10 + fresh(sa)) * 16u;   // pair n2 at po + n2*550*16
+    if (xwave) {
+      if constexpr (MODE == 2) {
+#pragma unroll
+        for (int n2 = 0; n2 < 11; ++n2) av[n2] = zld<V2>(A + sl, po + n2 * 550 * 16);
+#pragma unroll
+        for (int n2 = 0; n2 < 11; ++n2) {
+          V2 a = av[n2];
+          a.x = soft_l(a.x, theta) + corr[n2].x;
+          a.y = soft_l(a.y, theta) + corr[n2].y;
+          zst<V2>(Ao + sl, po + n2 * 550 * 16, a);
+          const T ux = soft_l(a.x, theta), uy = soft_l(a.y, theta);
+          zc[n2] = {ux - (a.x - ux), uy - (a.y - uy)};
+        }
+      } else {
+        const T* z0 = Zn + sl + 2 * j * zl::X + sa;
+        const T* y0 = Yn + sl + 2 * j * zl::X + sa;
+#pragma unroll
+        for (int n2 = 0; n2 < 11; ++n2) {
+          av[n2].x = z0[10 * n2] + y0[10 * n2];
+          av[n2].y = z0[zl::X + 10 * n2] + y0[zl::X + 10 * n2];
+        }
+#pragma unroll
+        for (int n2 = 0; n2 < 11; ++n2) {
+          const V2 a = av[n2];
+          const T ux = soft_l(a.x, theta), uy = soft_l(a.y, theta);
+          zc[n2] = {ux - (a.x - ux), uy - (a.y - uy)};
+        }
+      }
+    }
+    if constexpr (MODE == 0) {
+      __syncthreads();   // the slice is read in natural order before it is rewritten in state order
+      if (xwave) {
+#pragma unroll
+        for (int n2 = 0; n2 < 11; ++n2) zst<V2>(Ao + sl, po + n2 * 550 * 16, av[n2]);
+      }
+    }
+    // ---- P5: x-R2C of the row pair -> Z_j into rows 2j, 2j+1 of T ----
+    if (xwave) {
+      const int s5 = fresh(sb);
+      cpx<T> zf[10];
+      fwd_line<T, 1>(zc, zf, Ex, sTw, s5);
+      cpx<T>* r0 = sT + 2 * j * zl::RS;
+#pragma unroll
+      for (int k1 = 0; k1 < 10; ++k1) r0[s5 + 11 * k1] = zf[k1];
+    }
+    lds_sync();   // P6
+    // ---- P7: column c, rows y = n1 + 10 n2: two-for-one separation ----
+    cpx<T> col[11];
+    {
+      const int n1 = fresh(sa);
+      const int cm = (c == 0) ? 0 : zl::X - c;
+      // even rows: (z1 + conj z2) / 2; odd rows: (z1 - conj z2) / 2i
+      const bool odd = n1 & 1;
+#pragma unroll
+      for (int n2 = 0; n2 < 11; ++n2) {
+        const int y = n1 + 10 * n2;
+        const cpx<T>* r0 = sT + (y >> 1) * (2 * zl::RS);
+        const cpx<T> z1 = r0[c], z2 = r0[cm];
+        const T ex = (T)0.5 * (z1.x + z2.x), ey = (T)0.5 * (z1.y - z2.y);
+        const T ox = (T)0.5 * (z1.y + z2.y), oy = (T)-0.5 * (z1.x - z2.x);
+        col[n2] = {odd ? ox : ex, odd ? oy : ey};
+      }
+    }
+    lds_sync();   // P8
+    // ---- P9: y-R2C of column c -> bins, accumulate sum_k dhat_k C_k ----
+    {
+      const int s9 = fresh(sb);
+      cpx<T> cb[10];
+      fwd_line<T, zl::RS>(col, cb, Ey, sTw, s9);
+      const cpx<T>* dk = dhat + (int64_t)k * zl::F;
+      const uint32_t bo = (uint32_t)(c * 11 + s9) * 16u;
+#pragma unroll
+      for (int k1 = 0; k1 < 10; ++k1)
+        acc[k1] = cadd(acc[k1], cmul(zld<cpx<T>>(dk, bo + k1 * 616 * 16), cb[k1]));
+    }
+  }
+  // w = (B - acc) * sden  (sden = 1/((rho + s) X Y)); each lane owns its slots
+  {
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int l = lane / 11, s = lane - 11 * l, line = 5 * wave + l;
+    if (l < 5 && line < 56) {
+      cpx<T>* Wo = W + p * zl::F;
+      const cpx<T>* Bp = Bs + p * zl::F;
+#pragma unroll
+      for (int k1 = 0; k1 < 10; ++k1) {
+        const int sl2 = k1 * 616 + line * 11 + s;
+        Wo[sl2] = cscale(csub(Bp[sl2], acc[k1]), sden[sl2]);
+      }
+    }
+  }
+}
+
+// dst[b][bin_slot(f)] = src[b][f]  (complex spectra, `count` of them)
+template <typename T>
+__global__ void k_to_slots(const cpx<T>* __restrict__ src, cpx<T>* __restrict__ dst,
+                           int64_t count) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count * zl::F) return;
+  const int64_t b = i / zl::F;
+  const int f = (int)(i - b * zl::F);
+  dst[b * zl::F + zl::bin_slot(f)] = src[i];
+}
+template <typename T>
+__global__ void k_to_slots_real(const T* __restrict__ src, T* __restrict__ dst) {
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f < zl::F) dst[zl::bin_slot(f)] = src[f];
+}
+// natural[s][e] = state[s][state_off(e)], one workgroup per slice (a flat grid over
+// the 1.2e10 elements of C2 would exceed the 2^32 work-items of one dispatch)
+template <typename T>
+__global__ void k_state_to_nat(const T* __restrict__ st, T* __restrict__ nat) {
+  const int64_t b = blockIdx.x;
+  for (int e = threadIdx.x; e < zl::P; e += blockDim.x)
+    nat[b * zl::P + e] = st[b * zl::P + zl::state_off(e)];
+}
+
+bool zline_grid(const Grid2D& G) { return grid_is<Grid110>(G); }
+
+template <typename T>
+hipError_t launch_zline(const T* A, T* Ao, const T* Zn, const T* Yn, cpx<T>* W, const cpx<T>* Bs,
+                        const cpx<T>* dcorr, const cpx<T>* dhat, const T* sden,
+                        const cpx<T>* tw110, int64_t npatch, int K, T theta, int mode,
+                        hipStream_t st) {
+  if (npatch <= 0) return hipSuccess;
+  if (mode == 0)
+    hipLaunchKernelGGL((k_zline<T, 0>), dim3((unsigned)npatch), dim3(zl::NT), zl::kSmem, st, A, Ao,
+                       Zn, Yn, W, Bs, dcorr, dhat, sden, tw110, K, theta);
+  else
+    hipLaunchKernelGGL((k_zline<T, 2>), dim3((unsigned)npatch), dim3(zl::NT), zl::kSmem, st, A, Ao,
+                       Zn, Yn, W, Bs, dcorr, dhat, sden, tw110, K, theta);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_to_slots(const cpx<T>* src, cpx<T>* dst, int64_t count, hipStream_t st) {
+  if (count <= 0) return hipSuccess;
+  const int64_t n = count * zl::F;
+  hipLaunchKernelGGL(k_to_slots<T>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, src, dst,
+                     count);
+  return hipGetLastError();
+}
+template <typename T>
+hipError_t launch_to_slots_real(const T* src, T* dst, hipStream_t st) {
+  hipLaunchKernelGGL(k_to_slots_real<T>, dim3((zl::F + 255) / 256), dim3(256), 0, st, src, dst);
+  return hipGetLastError();
+}
+template <typename T>
+hipError_t launch_state_to_nat(const T* st_, T* nat, int64_t count, hipStream_t st) {
+  if (count <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_state_to_nat<T>, dim3((unsigned)count), dim3(256), 0, st, st_, nat);
+  return hipGetLastError();
+}
+
+std::vector<cpx<double>> zline_twiddles() {
+  std::vector<cpx<double>> t(zl::NTW);
+  const long double pi = 3.141592653589793238462643383279502884L;
+  for (int m = 0; m < zl::NTW; ++m) {
+    const long double a = -2.0L * pi * (long double)m / 110.0L;
+    t[m] = {(double)cosl(a), (double)sinl(a)};
+  }
+  return t;
+}
+size_t zline_smem_bytes() { return zl::kSmem; }
+
+template hipError_t launch_zline<double>(const double*, double*, const double*, const double*,
+                                         cpx<double>*, const cpx<double>*, const cpx<double>*,
+                                         const cpx<double>*, const double*, const cpx<double>*,
+                                         int64_t, int, double, int, hipStream_t);
+template hipError_t launch_to_slots<double>(const cpx<double>*, cpx<double>*, int64_t, hipStream_t);
+template hipError_t launch_to_slots_real<double>(const double*, double*, hipStream_t);
+template hipError_t launch_state_to_nat<double>(const double*, double*, int64_t, hipStream_t);
+
+}  // namespace ccsc

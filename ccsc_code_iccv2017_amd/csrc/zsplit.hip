@@ -29,6 +29,7 @@
 // start, after an objective) forms a = z + y on the fly.
 #include "fft_fixed.hpp"
 #include "slice.hpp"
+#include "zline.hpp"
 
 #include <type_traits>
 
@@ -219,7 +220,8 @@ __global__ __launch_bounds__(NT) void k_zsplit(const T* A, T* Ao, const T* __res
 // Zd may alias As (each element read, then written, by one thread).  With
 // zold != NULL also ||Zd - zold||^2, ||Zd||^2 per slice (the tol test,
 // dP:156-157; zold may alias Zd, read before written).
-template <typename T, class FG>
+// WSLOT: W and dcorr in the bin-slot order of zline.hip (110 grid only).
+template <typename T, class FG, bool WSLOT = false>
 __global__ __launch_bounds__(kNT) void k_zmat(const T* As, T* __restrict__ Yz,
                                               const cpx<T>* __restrict__ W,
                                               const cpx<T>* __restrict__ dcorr, T* Zd,
@@ -240,7 +242,8 @@ __global__ __launch_bounds__(kNT) void k_zmat(const T* As, T* __restrict__ Yz,
   const cpx<T>* Wp = W + p * F;
   for (int f = tid; f < F; f += kNT) {
     const int y = f / GO::Xh(Gd);
-    lds_cpx_store(S.slice + y * RS + 2 * (f - y * GO::Xh(Gd)), 1, cmulc(dk[f], Wp[f]));
+    const int fw = WSLOT ? zl::bin_slot(f) : f;
+    lds_cpx_store(S.slice + y * RS + 2 * (f - y * GO::Xh(Gd)), 1, cmulc(dk[fw], Wp[fw]));
   }
   GO::c2r(S.slice, Gd, S.tw, tid);
   const int64_t off = slice * P;
@@ -272,7 +275,8 @@ __global__ __launch_bounds__(kNT) void k_zmat(const T* As, T* __restrict__ Yz,
 // fft2(z) from the state for the D-precompute (dP:97 uses zhat), one
 // workgroup per slice: fft2(u - y) + X*Y conj(dcorr_k) w_p  with u = soft(a),
 // y = a - u.  Slices s = 0..count-1 of patches starting at A/W (K per patch).
-template <typename T, class FG>
+// ZL: A in the state order and W, dcorr in the bin-slot order of zline.hip.
+template <typename T, class FG, bool ZL = false>
 __global__ __launch_bounds__(kNT) void k_zhat_split(const T* __restrict__ A,
                                                     const cpx<T>* __restrict__ W,
                                                     const cpx<T>* __restrict__ dcorr,
@@ -292,7 +296,7 @@ __global__ __launch_bounds__(kNT) void k_zhat_split(const T* __restrict__ A,
   const int64_t off = slice * P;
   for (int e = tid; e < P; e += kNT) {
     const int y = e / X, x = e - y * X;
-    const T a = A[off + e];
+    const T a = A[off + (ZL ? zl::state_off(e) : e)];
     const T u = soft(a, theta);
     S.slice[y * RS + x] = u - (a - u);
   }
@@ -306,7 +310,8 @@ __global__ __launch_bounds__(kNT) void k_zhat_split(const T* __restrict__ A,
   for (int f = tid; f < F; f += kNT) {
     const int y = f / GO::Xh(Gd);
     const cpx<T> c = lds_cpx(S.slice + y * RS + 2 * (f - y * GO::Xh(Gd)), 1);
-    const cpx<T> q = cmulc(dk[f], Wp[f]);
+    const int fw = ZL ? zl::bin_slot(f) : f;
+    const cpx<T> q = cmulc(dk[fw], Wp[fw]);
     out[f] = {c.x + sc * q.x, c.y + sc * q.y};
   }
 }
@@ -361,11 +366,15 @@ hipError_t launch_zsplit(const T* U, T* Uo, const T* Yz, cpx<T>* W, const cpx<T>
 template <typename T>
 hipError_t launch_zmat(const T* As, T* Yz, const cpx<T>* W, const cpx<T>* dcorr, T* Zd,
                        const T* zold, T* znorm, int64_t npatch, const cpx<T>* tw, const Grid2D& G,
-                       int K, T theta, hipStream_t st) {
+                       int K, T theta, hipStream_t st, bool wslot) {
   if (npatch <= 0) return hipSuccess;
   const dim3 grid((unsigned)(npatch * K));
   const size_t sm = slice_smem_bytes(G, sizeof(T));
-  if (grid_is<Grid110>(G))
+  if (wslot && !grid_is<Grid110>(G)) return hipErrorInvalidValue;
+  if (wslot)
+    hipLaunchKernelGGL((k_zmat<T, Grid110, true>), grid, dim3(kNT), sm, st, As, Yz, W, dcorr, Zd,
+                       zold, znorm, tw, G, K, theta);
+  else if (grid_is<Grid110>(G))
     hipLaunchKernelGGL((k_zmat<T, Grid110>), grid, dim3(kNT), sm, st, As, Yz, W, dcorr, Zd, zold,
                        znorm, tw, G, K, theta);
   else
@@ -377,11 +386,15 @@ hipError_t launch_zmat(const T* As, T* Yz, const cpx<T>* W, const cpx<T>* dcorr,
 template <typename T>
 hipError_t launch_zhat_split(const T* A, const cpx<T>* W, const cpx<T>* dcorr, cpx<T>* dst,
                              int64_t npatch, const cpx<T>* tw, const Grid2D& G, int K, T theta,
-                             hipStream_t st) {
+                             hipStream_t st, bool zline_order) {
   if (npatch <= 0) return hipSuccess;
   const dim3 grid((unsigned)(npatch * K));
   const size_t sm = slice_smem_bytes(G, sizeof(T));
-  if (grid_is<Grid110>(G))
+  if (zline_order && !grid_is<Grid110>(G)) return hipErrorInvalidValue;
+  if (zline_order)
+    hipLaunchKernelGGL((k_zhat_split<T, Grid110, true>), grid, dim3(kNT), sm, st, A, W, dcorr, dst,
+                       tw, G, K, theta);
+  else if (grid_is<Grid110>(G))
     hipLaunchKernelGGL((k_zhat_split<T, Grid110>), grid, dim3(kNT), sm, st, A, W, dcorr, dst, tw,
                        G, K, theta);
   else
@@ -398,10 +411,10 @@ template hipError_t launch_zsplit<double>(const double*, double*, const double*,
 template hipError_t launch_zmat<double>(const double*, double*, const cpx<double>*,
                                         const cpx<double>*, double*, const double*, double*,
                                         int64_t, const cpx<double>*, const Grid2D&, int, double,
-                                        hipStream_t);
+                                        hipStream_t, bool);
 template hipError_t launch_zhat_split<double>(const double*, const cpx<double>*,
                                               const cpx<double>*, cpx<double>*, int64_t,
                                               const cpx<double>*, const Grid2D&, int, double,
-                                              hipStream_t);
+                                              hipStream_t, bool);
 
 }  // namespace ccsc

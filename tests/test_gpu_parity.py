@@ -148,8 +148,9 @@ def test_learn_3d_matches_oracle(gpu_ctx, sb, psf, K, n, tol):
             np.testing.assert_allclose(tr["z_diff"][i, :len(zd)], zd, rtol=1e-6)
 
 
+@pytest.mark.parametrize("verbose", ["brief", "none"])
 @pytest.mark.parametrize("variant", ["dp", "dz"])
-def test_headline_block_on_110_grid_matches_port(gpu_ctx, variant):
+def test_headline_block_on_110_grid_matches_port(gpu_ctx, variant, verbose):
     """C1/C2's exact block: 100x100 patches (110x110 grid, the compile-time-planned z-step
     kernel), K = ni = 100, 2 consensus blocks; checked against the half-spectrum port
     (pinned to the literal oracle by tests/test_oracle.py) since the literal oracle's
@@ -168,7 +169,7 @@ def test_headline_block_on_110_grid_matches_port(gpu_ctx, variant):
     else:
         cst = dict(rho_d=500.0, rho_z=50.0, theta_div=50.0)
         fn = E.admm_learn_conv2D_large_dParallel
-    d_e, z_e, DZ_e, it_e = fn(b, [11, 11, K], 1.0, 1.0, 2, 0.0, "brief", init, ni=ni,
+    d_e, z_e, DZ_e, it_e = fn(b, [11, 11, K], 1.0, 1.0, 2, 0.0, verbose, init, ni=ni,
                               max_it_d=mid, max_it_z=miz, ctx=gpu_ctx)
     port = DzPort(b, d0, z0, 1.0, ni=ni, max_it_d=mid, max_it_z=miz,
                   replicate_z0=(variant == "dz"), **cst)
@@ -176,8 +177,9 @@ def test_headline_block_on_110_grid_matches_port(gpu_ctx, variant):
     port.outer()
     assert _rel(d_e, O.crop_filters(port.D[0], 2, 5)) < 1e-7
     assert _rel(z_e, port.z) < 1e-7
-    obj = O.objective_2d(port.z, port.dhat_full(), b, 1.0, 1.0, 5)
-    assert abs(it_e["obj_vals_z"][-1] - obj) <= 1e-9 * abs(obj)
+    if verbose != "none":   # 'none': z-iterations run on the state without (z, y) in between
+        obj = O.objective_2d(port.z, port.dhat_full(), b, 1.0, 1.0, 5)
+        assert abs(it_e["obj_vals_z"][-1] - obj) <= 1e-9 * abs(obj)
 
 
 @pytest.mark.parametrize("rho_d", [500.0, 5000.0])
@@ -212,3 +214,26 @@ def test_dfactor_woodbury_rejected_when_blocks_too_large(gpu_ctx):
                                              {"d": d0, "z": z0}, ni=12, dfactor="woodbury",
                                              ctx=gpu_ctx)
     assert ei.value.code == L.CCSC_E_UNSUPPORTED
+
+
+@pytest.mark.parametrize("miz", [1, 2, 4])
+def test_zline_state_path_matches_port(gpu_ctx, miz):
+    """The register-line z-step's steady state (zline.hip mode 2: state order, bin-slot
+    spectra, the corr C2R, k_zhat_split from the state) -- reached only when no objective
+    forces (z, y) between z-iterations (verbose 'none'), as in the bench -- against the
+    port on C2's 110x110 grid."""
+    from ccsc_code_iccv2017_amd import learners as E
+    from oracle.ccsc_port import DzPort
+    K, n, ni = 4, 4, 2
+    rng = np.random.default_rng(55)
+    b = rng.standard_normal((100, 100, n))
+    d0 = rng.standard_normal((11, 11, K))
+    z0 = rng.standard_normal((110, 110, K, ni))
+    d_e, z_e, DZ_e, _ = E.admm_learn_conv2D_large_dzParallel(
+        b, [11, 11, K], 1.0, 1.0, 2, 0.0, "none", {"d": d0, "z": z0}, ni=ni, max_it_d=2,
+        max_it_z=miz, ctx=gpu_ctx)
+    port = DzPort(b, d0, z0, 1.0, ni=ni, max_it_d=2, max_it_z=miz)
+    port.outer()
+    port.outer()
+    assert _rel(z_e, port.z) < 1e-7
+    assert _rel(d_e, O.crop_filters(port.D[0], 2, 5)) < 1e-7
