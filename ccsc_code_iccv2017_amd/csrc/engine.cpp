@@ -484,7 +484,7 @@ struct Session2D {
   // in state order, W the last w in bin-slot order solved with dws (dhs or dhws);
   // Bhs / dhs / sdens: B^, the current filter spectrum and sden in bin-slot order.
   bool zl_on = false;
-  DevBuf Bhs, dhs, dhws, sdens, tw110;
+  DevBuf Bhs, dhs, dhws, sdens;
   const cpx<double>* dws = nullptr;
   DevBuf twt, oacc, odz;   // 3D: t-FFT twiddles, objective scratch
 
@@ -626,9 +626,6 @@ struct Session2D {
       dhs.alloc((size_t)K * F * 16);
       dhws.alloc((size_t)K * F * 16);
       sdens.alloc((size_t)F * 8);
-      auto t110 = zline_twiddles();
-      tw110.alloc(t110.size() * 16);
-      HIPCHK(hipMemcpy(tw110.p, t110.data(), tw110.bytes, hipMemcpyHostToDevice));
     }
     D.alloc(m.D);
     yD.alloc(m.yD);
@@ -788,8 +785,7 @@ struct Session2D {
       HIPCHK(launch_zline<double>(z.as<double>(), z.as<double>(), z.as<double>(), yz.as<double>(),
                                   W.as<cpx<double>>(), Bhs.as<cpx<double>>(),
                                   zmode == 2 ? dws : dhs.as<cpx<double>>(), dhs.as<cpx<double>>(),
-                                  sdens.as<double>(), tw110.as<cpx<double>>(), np, K, theta,
-                                  zmode == 2 ? 2 : 0, st));
+                                  sdens.as<double>(), np, K, theta, zmode == 2 ? 2 : 0, st));
       zmode = 2;
       dws = dhs.as<cpx<double>>();
     } else if (!tol_on) {

@@ -3,8 +3,6 @@
 
 #include "fft.hpp"
 
-#include <vector>
-
 namespace ccsc {
 
 size_t slice_smem_bytes(const Grid2D& G, size_t tsize);
@@ -73,12 +71,10 @@ hipError_t launch_zhat_split(const T* A, const cpx<T>* W, const cpx<T>* dcorr, c
 // mode 0: (z, y) materialised in Zn / Yn (natural layout); mode 2: state in A.
 bool zline_grid(const Grid2D& G);
 size_t zline_smem_bytes();
-std::vector<cpx<double>> zline_twiddles();
 template <typename T>
 hipError_t launch_zline(const T* A, T* Ao, const T* Zn, const T* Yn, cpx<T>* W, const cpx<T>* Bs,
-                        const cpx<T>* dcorr, const cpx<T>* dhat, const T* sden,
-                        const cpx<T>* tw110, int64_t npatch, int K, T theta, int mode,
-                        hipStream_t st);
+                        const cpx<T>* dcorr, const cpx<T>* dhat, const T* sden, int64_t npatch,
+                        int K, T theta, int mode, hipStream_t st);
 template <typename T>
 hipError_t launch_to_slots(const cpx<T>* src, cpx<T>* dst, int64_t count, hipStream_t st);
 template <typename T>

@@ -3,15 +3,16 @@
 // solve_conv_term_Z dP:278-303, dZ:151-157, 283-308), re-laid out so that the
 // slice transforms live in registers and LDS only carries transposes.
 //
-// Every 110-point line transform is 110 = 10 x 11, split over the lanes of one
+// Every 110-point line transform is the prime-factor (Good-Thomas) split
+// 110 = 10 x 11 (coprime factors: no twiddle multiplies), over the lanes of one
 // wave (five lines per wave):
-//   layout A ("time"): 10 lanes per line, lane n1 holds elements n1 + 10 n2,
-//                       n2 = 0..10 (11 complex registers);
-//   layout B ("freq"): 11 lanes per line, lane k2 holds elements k2 + 11 k1,
-//                       k1 = 0..9 (10 complex registers).
-//   forward A -> B:  DFT-11 over the registers, twiddle W_110^(n1 k2), a
-//                    wave-local transpose through LDS, DFT-10 over the registers;
-//   inverse B -> A:  the mirror image (conjugate twiddles).
+//   layout A ("time"): 10 lanes per line, lane n1 holds elements (11 n1 + 10 n2)
+//                       mod 110, n2 = 0..10 (11 complex registers);
+//   layout B ("freq"): 11 lanes per line, lane k2 holds elements (11 k1 + 100 k2)
+//                       mod 110, k1 = 0..9 (10 complex registers).
+//   forward A -> B:  DFT-11 over the registers, a wave-local transpose through
+//                    LDS, DFT-10 over the registers;
+//   inverse B -> A:  the mirror image.
 // A slice's 2D transforms are then y-lines (the 56 half-spectrum columns) and
 // x-lines (the 55 row pairs packed as complex, two-for-one), joined by one
 // workgroup-wide transpose buffer T [110 rows][57 complex] per direction change:
@@ -37,9 +38,9 @@
 //
 // Layouts in HBM (engine-internal, z-step only):
 //   state a:    "state order", per (patch, filter) slice 6050 (row 2j, row 2j+1)
-//               pairs, pair n2*550 + j*10 + n1 holds x = n1 + 10 n2 (zl::state_off);
+//               pairs, pair n2*550 + j*10 + n1 holds x = elem_a(n1, n2) (zl::state_off);
 //   w, B^, d^:  "bin-slot order" per 6160-bin spectrum, slot k1*616 + c*11 + k2
-//               holds bin (x' = c, y = k2 + 11 k1) (zl::bin_slot) -- lane-contiguous,
+//               holds bin (x' = c, y = elem_b(k2, k1)) (zl::bin_slot) -- lane-contiguous,
 //               so every per-slice global access is a coalesced 16-B stream.
 // k_zmat / k_zhat_split (zsplit.hip) read these orders; k_state_to_nat and
 // k_to_slots convert.
@@ -47,7 +48,6 @@
 #include "slice.hpp"
 #include "zline.hpp"
 
-#include <vector>
 
 namespace ccsc {
 
@@ -65,41 +65,39 @@ __device__ __forceinline__ void wave_lds_fence() {
 
 // Forward 110-point transform of one line, layout A (v[n2], lane n1 = s < 10)
 // -> layout B (out[k1], lane k2 = s <= 10).  E: the line's 110 exchange slots,
-// slot i at E[i * ES].  tw: W_110^m in LDS.
+// slot n1*11 + k2 at E[(n1*11 + k2) * ES].
 // Idle lanes (lane 10 of a line in layout A, lanes 55..63, the clamped lines of the
 // last wave) run on clamped indices and so duplicate a real lane exactly: their
 // LDS and global stores write the same value to the same address, no guards.
-template <typename T, int ES>
-__device__ __forceinline__ void fwd_line(cpx<T> (&v)[11], cpx<T> (&out)[10], cpx<T>* E,
-                                         const cpx<T>* tw, int s) {
+// The outputs stream to sink(k1, value) as the last stage forms them.
+template <typename T, int ES, typename Sink>
+__device__ __forceinline__ void fwd_line(cpx<T> (&v)[11], cpx<T>* E, int s, Sink&& sink) {
   const int sa = min(s, 9);
-  dft_sink<T, 11, -1>(v, [&](int k2, cpx<T> val) {
-    if (k2 > 0) val = cmul(val, tw[sa * k2]);
-    E[(sa * 11 + k2) * ES] = val;
-  });
+  dft_sink<T, 11, -1>(v, [&](int k2, cpx<T> val) { E[(sa * 11 + k2) * ES] = val; });
   wave_lds_fence();
   cpx<T> in[10];
 #pragma unroll
   for (int n1 = 0; n1 < 10; ++n1) in[n1] = E[(n1 * 11 + s) * ES];
-  dft_sink<T, 10, -1>(in, [&](int k1, cpx<T> val) { out[k1] = val; });
+  dft_sink<T, 10, -1>(in, sink);
 }
 
 // Inverse (unnormalised) 110-point transform, layout B (in[k1], lane k2 = s)
 // -> layout A (out[n2], lane n1 = s < 10).
-template <typename T, int ES>
-__device__ __forceinline__ void inv_line(cpx<T> (&in)[10], cpx<T> (&out)[11], cpx<T>* E,
-                                         const cpx<T>* tw, int s) {
-  dft_sink<T, 10, +1>(in, [&](int n1, cpx<T> val) {
-    if (n1 > 0) val = cmulc(tw[s * n1], val);   // conj(W_110^(n1 k2)) val
-    E[(n1 * 11 + s) * ES] = val;
-  });
+template <typename T, int ES, typename Sink>
+__device__ __forceinline__ void inv_line(cpx<T> (&in)[10], cpx<T>* E, int s, Sink&& sink) {
+  dft_sink<T, 10, +1>(in, [&](int n1, cpx<T> val) { E[(n1 * 11 + s) * ES] = val; });
   wave_lds_fence();
   const int sa = min(s, 9);
   cpx<T> v[11];
 #pragma unroll
   for (int k2 = 0; k2 < 11; ++k2) v[k2] = E[(sa * 11 + k2) * ES];
-  dft_sink<T, 11, +1>(v, [&](int n2, cpx<T> val) { out[n2] = val; });
+  dft_sink<T, 11, +1>(v, sink);
 }
+
+// (e mod 110) for 0 <= e < 220
+__device__ __forceinline__ int mod110(int e) { return e >= 110 ? e - 110 : e; }
+// slot of element x of a row pair's spectrum Z_j in layout-B order (k1*11 + k2)
+__device__ __forceinline__ int zslot(int x) { return (x % 10) * 11 + (x % 11); }
 
 // 16-B global access at a 32-bit byte offset from a wave-uniform base (saddr form:
 // SGPR base + one VGPR offset, no 64-bit VGPR address per access).
@@ -129,13 +127,10 @@ __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn
                                                   const cpx<T>* __restrict__ Bs,
                                                   const cpx<T>* __restrict__ dcorr,
                                                   const cpx<T>* __restrict__ dhat,
-                                                  const T* __restrict__ sden,
-                                                  const cpx<T>* __restrict__ twg, int K, T theta) {
+                                                  const T* __restrict__ sden, int K, T theta) {
   using V2 = typename vec2_t<T>::type;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   cpx<T>* sT = reinterpret_cast<cpx<T>*>(smem);
-  cpx<T>* sTw = sT + zl::TSZ;
-  for (int i = threadIdx.x; i < zl::NTW; i += zl::NT) sTw[i] = twg[i];
   const int64_t p = blockIdx.x;
   cpx<T> acc[10];
 #pragma unroll
@@ -143,7 +138,6 @@ __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn
   const cpx<T>* Wp = W + p * zl::F;
   // the last wave owns one y-line and no x-line (55 row pairs = 11 waves of 5)
   const bool xwave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6) < 11;
-  __syncthreads();   // twiddles
 
   for (int k = 0; k < K; ++k) {
     // lane roles, recomputed per slice from an opaque thread index (see fresh())
@@ -157,7 +151,8 @@ __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn
     cpx<T>* Ey = sT + c;                                       // column c: slot i at row i
     cpx<T>* Ex = sT + 10 * min(wave, 10) * zl::RS + l * 110;   // the wave's rows, line l
     const int64_t sl = (p * K + k) * zl::P;
-    cpx<T> corr[11];
+    cpx<T> zc[11];   // c = u - y of the row pair (x-lines, layout A) for the R2C
+    const uint32_t po = (uint32_t)(j * 10 + fresh(sa)) * 16u;   // pair n2 at po + n2*550*16
     if constexpr (MODE == 2) {
       // ---- P1: y-C2R of conj(dcorr_k) w from bins to T[y][c] ----
       const cpx<T>* dk = dcorr + (int64_t)k * zl::F;
@@ -166,19 +161,19 @@ __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn
 #pragma unroll
       for (int k1 = 0; k1 < 10; ++k1)
         b[k1] = cmulc(zld<cpx<T>>(dk, bo + k1 * 616 * 16), zld<cpx<T>>(Wp, bo + k1 * 616 * 16));
-      cpx<T> yt[11];
-      inv_line<T, zl::RS>(b, yt, Ey, sTw, sb);
-#pragma unroll
-      for (int n2 = 0; n2 < 11; ++n2) sT[(sa + 10 * n2) * zl::RS + c] = yt[n2];
+      inv_line<T, zl::RS>(b, Ey, sb, [&](int n2, cpx<T> val) {
+        sT[mod110(11 * sa + 10 * n2) * zl::RS + c] = val;
+      });
       lds_sync();   // P2
-      // ---- P3: x-C2R of row pair j: Z(x) = R_2j(x) + i R_2j+1(x), Hermitian ext. ----
       if (xwave) {
+        // ---- P3: x-C2R of row pair j: Z(x) = R_2j(x) + i R_2j+1(x), Hermitian ext. ----
         const int s3 = fresh(sb);
+        const int xb = s3 ? 110 - 10 * s3 : 0;   // elem_b(k2, 0)
         cpx<T> zb[10];
         const cpx<T>* r0 = sT + 2 * j * zl::RS;
 #pragma unroll
         for (int k1 = 0; k1 < 10; ++k1) {
-          const int x = s3 + 11 * k1;
+          const int x = mod110(xb + 11 * k1);
           const bool hi = x >= zl::Xh;
           const int cc = hi ? zl::X - x : x;
           cpx<T> a = r0[cc], bb = r0[zl::RS + cc];
@@ -187,33 +182,31 @@ __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn
           bb.y *= sg;
           zb[k1] = {a.x - bb.y, a.y + bb.x};
         }
-        inv_line<T, 1>(zb, corr, Ex, sTw, s3);
-      }
-    }
-    // ---- P4: elementwise on (row 2j, row 2j+1) at x = n1 + 10 n2 ----
-    cpx<T> zc[11];
-    V2 av[11];
-    const uint32_t po = (uint32_t)(j * 10 + fresh(sa)) * 16u;   // pair n2 at po + n2*550*16
-    if (xwave) {
-      if constexpr (MODE == 2) {
+        // ---- P4: state (row 2j, row 2j+1) at x = elem_a(n1, n2), in flight under the C2R;
+        // each corr value is consumed as the last inverse stage forms it ----
+        V2 av[11];
 #pragma unroll
         for (int n2 = 0; n2 < 11; ++n2) av[n2] = zld<V2>(A + sl, po + n2 * 550 * 16);
-#pragma unroll
-        for (int n2 = 0; n2 < 11; ++n2) {
+        inv_line<T, 1>(zb, Ex, s3, [&](int n2, cpx<T> corr) {
           V2 a = av[n2];
-          a.x = soft_l(a.x, theta) + corr[n2].x;
-          a.y = soft_l(a.y, theta) + corr[n2].y;
+          a.x = soft_l(a.x, theta) + corr.x;
+          a.y = soft_l(a.y, theta) + corr.y;
           zst<V2>(Ao + sl, po + n2 * 550 * 16, a);
           const T ux = soft_l(a.x, theta), uy = soft_l(a.y, theta);
           zc[n2] = {ux - (a.x - ux), uy - (a.y - uy)};
-        }
-      } else {
-        const T* z0 = Zn + sl + 2 * j * zl::X + sa;
-        const T* y0 = Yn + sl + 2 * j * zl::X + sa;
+        });
+      }
+    } else {
+      // ---- P4 (mode 0): a = z + y from the materialised natural layout ----
+      V2 av[11];
+      if (xwave) {
+        const T* z0 = Zn + sl + 2 * j * zl::X;
+        const T* y0 = Yn + sl + 2 * j * zl::X;
 #pragma unroll
         for (int n2 = 0; n2 < 11; ++n2) {
-          av[n2].x = z0[10 * n2] + y0[10 * n2];
-          av[n2].y = z0[zl::X + 10 * n2] + y0[zl::X + 10 * n2];
+          const int x = mod110(11 * sa + 10 * n2);
+          av[n2].x = z0[x] + y0[x];
+          av[n2].y = z0[zl::X + x] + y0[zl::X + x];
         }
 #pragma unroll
         for (int n2 = 0; n2 < 11; ++n2) {
@@ -222,8 +215,6 @@ __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn
           zc[n2] = {ux - (a.x - ux), uy - (a.y - uy)};
         }
       }
-    }
-    if constexpr (MODE == 0) {
       __syncthreads();   // the slice is read in natural order before it is rewritten in state order
       if (xwave) {
 #pragma unroll
@@ -233,25 +224,22 @@ __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn
     // ---- P5: x-R2C of the row pair -> Z_j into rows 2j, 2j+1 of T ----
     if (xwave) {
       const int s5 = fresh(sb);
-      cpx<T> zf[10];
-      fwd_line<T, 1>(zc, zf, Ex, sTw, s5);
-      cpx<T>* r0 = sT + 2 * j * zl::RS;
-#pragma unroll
-      for (int k1 = 0; k1 < 10; ++k1) r0[s5 + 11 * k1] = zf[k1];
+      cpx<T>* r0 = sT + 2 * j * zl::RS;   // Z_j in layout-B slot order (zslot)
+      fwd_line<T, 1>(zc, Ex, s5, [&](int k1, cpx<T> val) { r0[k1 * 11 + s5] = val; });
     }
     lds_sync();   // P6
     // ---- P7: column c, rows y = n1 + 10 n2: two-for-one separation ----
     cpx<T> col[11];
     {
       const int n1 = fresh(sa);
-      const int cm = (c == 0) ? 0 : zl::X - c;
-      // even rows: (z1 + conj z2) / 2; odd rows: (z1 - conj z2) / 2i
+      const int zc1 = zslot(c), zc2 = zslot((c == 0) ? 0 : zl::X - c);
+      // even rows: (z1 + conj z2) / 2; odd rows: (z1 - conj z2) / 2i (row parity = n1's)
       const bool odd = n1 & 1;
 #pragma unroll
       for (int n2 = 0; n2 < 11; ++n2) {
-        const int y = n1 + 10 * n2;
+        const int y = mod110(11 * n1 + 10 * n2);
         const cpx<T>* r0 = sT + (y >> 1) * (2 * zl::RS);
-        const cpx<T> z1 = r0[c], z2 = r0[cm];
+        const cpx<T> z1 = r0[zc1], z2 = r0[zc2];
         const T ex = (T)0.5 * (z1.x + z2.x), ey = (T)0.5 * (z1.y - z2.y);
         const T ox = (T)0.5 * (z1.y + z2.y), oy = (T)-0.5 * (z1.x - z2.x);
         col[n2] = {odd ? ox : ex, odd ? oy : ey};
@@ -261,13 +249,11 @@ __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn
     // ---- P9: y-R2C of column c -> bins, accumulate sum_k dhat_k C_k ----
     {
       const int s9 = fresh(sb);
-      cpx<T> cb[10];
-      fwd_line<T, zl::RS>(col, cb, Ey, sTw, s9);
       const cpx<T>* dk = dhat + (int64_t)k * zl::F;
       const uint32_t bo = (uint32_t)(c * 11 + s9) * 16u;
-#pragma unroll
-      for (int k1 = 0; k1 < 10; ++k1)
-        acc[k1] = cadd(acc[k1], cmul(zld<cpx<T>>(dk, bo + k1 * 616 * 16), cb[k1]));
+      fwd_line<T, zl::RS>(col, Ey, s9, [&](int k1, cpx<T> cb) {
+        acc[k1] = cadd(acc[k1], cmul(zld<cpx<T>>(dk, bo + k1 * 616 * 16), cb));
+      });
     }
   }
   // w = (B - acc) * sden  (sden = 1/((rho + s) X Y)); each lane owns its slots
@@ -314,16 +300,15 @@ bool zline_grid(const Grid2D& G) { return grid_is<Grid110>(G); }
 
 template <typename T>
 hipError_t launch_zline(const T* A, T* Ao, const T* Zn, const T* Yn, cpx<T>* W, const cpx<T>* Bs,
-                        const cpx<T>* dcorr, const cpx<T>* dhat, const T* sden,
-                        const cpx<T>* tw110, int64_t npatch, int K, T theta, int mode,
-                        hipStream_t st) {
+                        const cpx<T>* dcorr, const cpx<T>* dhat, const T* sden, int64_t npatch,
+                        int K, T theta, int mode, hipStream_t st) {
   if (npatch <= 0) return hipSuccess;
   if (mode == 0)
     hipLaunchKernelGGL((k_zline<T, 0>), dim3((unsigned)npatch), dim3(zl::NT), zl::kSmem, st, A, Ao,
-                       Zn, Yn, W, Bs, dcorr, dhat, sden, tw110, K, theta);
+                       Zn, Yn, W, Bs, dcorr, dhat, sden, K, theta);
   else
     hipLaunchKernelGGL((k_zline<T, 2>), dim3((unsigned)npatch), dim3(zl::NT), zl::kSmem, st, A, Ao,
-                       Zn, Yn, W, Bs, dcorr, dhat, sden, tw110, K, theta);
+                       Zn, Yn, W, Bs, dcorr, dhat, sden, K, theta);
   return hipGetLastError();
 }
 
@@ -347,21 +332,12 @@ hipError_t launch_state_to_nat(const T* st_, T* nat, int64_t count, hipStream_t 
   return hipGetLastError();
 }
 
-std::vector<cpx<double>> zline_twiddles() {
-  std::vector<cpx<double>> t(zl::NTW);
-  const long double pi = 3.141592653589793238462643383279502884L;
-  for (int m = 0; m < zl::NTW; ++m) {
-    const long double a = -2.0L * pi * (long double)m / 110.0L;
-    t[m] = {(double)cosl(a), (double)sinl(a)};
-  }
-  return t;
-}
 size_t zline_smem_bytes() { return zl::kSmem; }
 
 template hipError_t launch_zline<double>(const double*, double*, const double*, const double*,
                                          cpx<double>*, const cpx<double>*, const cpx<double>*,
-                                         const cpx<double>*, const double*, const cpx<double>*,
-                                         int64_t, int, double, int, hipStream_t);
+                                         const cpx<double>*, const double*, int64_t, int, double,
+                                         int, hipStream_t);
 template hipError_t launch_to_slots<double>(const cpx<double>*, cpx<double>*, int64_t, hipStream_t);
 template hipError_t launch_to_slots_real<double>(const double*, double*, hipStream_t);
 template hipError_t launch_state_to_nat<double>(const double*, double*, int64_t, hipStream_t);
