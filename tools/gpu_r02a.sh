@@ -1,0 +1,9 @@
+#!/bin/bash
+# one-off round-2 measurement call: gram/chol ablation, SQ pass, full round profile
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+bash tools/ab_bench.sh abv base nogram nochol || exit 1
+cp abv/libccsc_base.so ccsc_code_iccv2017_amd/libccsc.so
+grep -h per-kernel gpurun_out/ab/*.err
+bash tools/sq_profile.sh zl1 || exit 1
+bash tools/round_profile.sh r02a || exit 1
