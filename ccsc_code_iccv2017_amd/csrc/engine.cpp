@@ -398,6 +398,12 @@ struct ccsc_ctx {
 
 namespace ccsc {
 
+// the register-line z-step serves the 110 grid (A/B switch: CCSC_ZLINE=0 keeps k_zsplit)
+static bool zline_usable(const Grid2D& G) {
+  const char* ev = std::getenv("CCSC_ZLINE");
+  return zline_grid(G) && !(ev && ev[0] == '0');
+}
+
 // memory plan shared by ccsc_plan_bytes and the session
 struct Plan2D {
   int64_t np, nbl, b0;
@@ -422,8 +428,10 @@ static Plan2D plan2d(const ccsc_problem& p, const Geom& g, int rank, int nranks)
   m.yz = m.z;
   // 2D split z-state (zsplit.hip): w per patch + the filter spectrum it was
   // solved with; with tol > 0 a u buffer so z_old survives for the tol test
-  // (the 4D and 3D z-steps compare per slice/plane)
-  m.cbuf = (p.tol > 0 && !is4 && !is3) ? m.z : 0;
+  // (the 4D and 3D z-steps compare per slice/plane; the register-line z-step of
+  // the 110 grid keeps z_old in the y buffer, zline.hip)
+  const bool zline = !is4 && !is3 && zline_usable(G);
+  m.cbuf = (p.tol > 0 && !is4 && !is3 && !zline) ? m.z : 0;
   m.W = (!is4 && !is3) ? m.np * F * 16 : 0;
   m.dhw = (!is4 && !is3) ? K * F * 16 : 0;
   m.D = m.nbl * K * NV * P * 8;
@@ -439,7 +447,7 @@ static Plan2D plan2d(const ccsc_problem& p, const Geom& g, int rank, int nranks)
   m.E = (is4 || is3) ? m.np * K * F * 16 : 0;
   // register-line z-step (zline.hip, 110 grid): B^ and the two filter spectra in
   // bin-slot order, sden in bin-slot order
-  m.zl = (!is4 && !is3 && zline_grid(G)) ? m.np * F * 16 + 2 * K * F * 16 + F * 8 : 0;
+  m.zl = zline ? m.np * F * 16 + 2 * K * F * 16 + F * 8 : 0;
   m.misc = (2 * K * NV * F) * 16 + F * 8 + (m.nbl + 2) * K * NV * SS * 8 * 2 +
            (4 * m.np * NV * g.Tn + 4 * K * NV * g.Tn + 64) * 8 + (size_t)(G.ntw + g.Gt.ntw) * 16 +
            (is3 ? F * 16 + P * 8 : 0);
@@ -486,6 +494,12 @@ struct Session2D {
   bool zl_on = false;
   DevBuf Bhs, dhs, dhws, sdens;
   const cpx<double>* dws = nullptr;
+  // tol > 0 with the register-line z-step: what `yz` holds (state order) while the
+  // state is in zmode 2 -- ZT_PREV: the z of the iterate before the current one
+  // (the next launch measures the current iterate against it), ZT_CUR: the
+  // current iterate's z (its test is done), ZT_NONE: nothing (y, or stale).
+  enum { ZT_NONE, ZT_PREV, ZT_CUR };
+  int zt = ZT_NONE;
   DevBuf twt, oacc, odz;   // 3D: t-FFT twiddles, objective scratch
 
   // host-side log
@@ -617,10 +631,7 @@ struct Session2D {
     if (m.cbuf) cbuf.alloc(m.cbuf);
     if (m.W) W.alloc(m.W);
     if (m.dhw) dhatw.alloc(m.dhw);
-    {
-      const char* ev = std::getenv("CCSC_ZLINE");   // A/B switch: CCSC_ZLINE=0 keeps k_zsplit
-      zl_on = m.zl && !(p.tol > 0) && !(ev && ev[0] == '0');
-    }
+    zl_on = m.zl != 0;
     if (zl_on) {
       Bhs.alloc((size_t)np * F * 16);
       dhs.alloc((size_t)K * F * 16);
@@ -761,8 +772,11 @@ struct Session2D {
                                     supp.as<double>(), dnorm.as<double>(), owner0 ? KG : 0,
                                     1.0 / (double)P, r, nbl * KG, Tn, twc, G, st));
   }
-  // one z-iteration over the local patches (dP:147-157; 4D L4:163-167; 3D L3:164-178)
-  void zstep_iter(bool tol_on) {
+  // one z-iteration over the local patches (dP:147-157; 4D L4:163-167; 3D L3:164-178).
+  // Returns true when the launch measured the iterate it started from instead of the
+  // one it produced (register-line z-step with tol > 0, see zline.hip); the others
+  // leave the test of the produced iterate in znorm when tol_on.
+  bool zstep_iter(bool tol_on) {
     const auto* twc = tw.as<cpx<double>>();
     if (is4) {
       HIPCHK(launch_zstep_diag<double>(z.as<double>(), yz.as<double>(), E.as<cpx<double>>(),
@@ -781,13 +795,21 @@ struct Session2D {
                                       tol_on ? znorm.as<double>() : nullptr, 0, 1.0, r, np * K,
                                       Tn, twc, G, st));
     } else if (zl_on) {
-      // register-line z-step (zline.hip): mode 0 reads (z, y) and leaves a in state order
+      // register-line z-step (zline.hip): mode 0 reads (z, y) and leaves a in state order.
+      // tol > 0: the launch stores the z it starts from in `yz` and, when `yz` holds the
+      // one before it, measures it (the test of the previous iteration, returned true)
+      const int mode = zmode == 2 ? 2 : 0;
+      int tolv = 0;
+      if (tol_on) tolv = mode == 0 ? 1 : (zt == ZT_PREV ? 2 : (zt == ZT_CUR ? 0 : 1));
       HIPCHK(launch_zline<double>(z.as<double>(), z.as<double>(), z.as<double>(), yz.as<double>(),
                                   W.as<cpx<double>>(), Bhs.as<cpx<double>>(),
                                   zmode == 2 ? dws : dhs.as<cpx<double>>(), dhs.as<cpx<double>>(),
-                                  sdens.as<double>(), np, K, theta, zmode == 2 ? 2 : 0, st));
+                                  sdens.as<double>(), np, K, theta, mode, st, tolv,
+                                  yz.as<double>(), znorm.as<double>()));
       zmode = 2;
       dws = dhs.as<cpx<double>>();
+      if (tol_on) zt = ZT_PREV;
+      return tolv == 2;
     } else if (!tol_on) {
       // one pass per patch over the pre-threshold state a (zsplit.hip): `z` holds a
       HIPCHK(launch_zsplit<double>(z.as<double>(), z.as<double>(), yz.as<double>(),
@@ -808,10 +830,45 @@ struct Session2D {
                                  znorm.as<double>(), np, twc, G, K, theta, st));
       zmode = 0;
     }
+    return false;
+  }
+  // register-line state + tol: the test of the current iterate against the z before it
+  // (in `yz`, ZT_PREV) without advancing (end of a z-phase)
+  void zl_finalize() {
+    HIPCHK(launch_zline<double>(z.as<double>(), z.as<double>(), z.as<double>(), yz.as<double>(),
+                                W.as<cpx<double>>(), Bhs.as<cpx<double>>(), dws,
+                                dhs.as<cpx<double>>(), sdens.as<double>(), np, K, theta, 3, st, 2,
+                                yz.as<double>(), znorm.as<double>()));
+    zt = ZT_CUR;
+  }
+  // register-line state + tol: materialise (z, y) of the current iterate and measure it
+  // against the z before it (`yz`, ZT_PREV): both slices to natural order in place, then
+  // k_zmat with z_old = yz (read before it is overwritten by y)
+  void zl_materialize_tol() {
+    HIPCHK(launch_state_to_nat_inplace<double>(z.as<double>(), np * K, st));
+    HIPCHK(launch_state_to_nat_inplace<double>(yz.as<double>(), np * K, st));
+    HIPCHK(launch_zmat<double>(z.as<double>(), yz.as<double>(), W.as<cpx<double>>(), dws,
+                               z.as<double>(), yz.as<double>(), znorm.as<double>(), np,
+                               tw.as<cpx<double>>(), G, K, theta, st, true));
+    zmode = 0;
+    zt = ZT_NONE;
+  }
+  // register-line state + tol: the launch just made was one iteration past the break
+  // (its test of the iterate it started from fired).  That iterate is intact: `yz` holds
+  // its z and `z` its pre-threshold value a = z + y (the launch's state write); the
+  // launch's w is dropped.  (z, y) natural <- (yz, z - yz).
+  void zl_rollback() {
+    HIPCHK(launch_state_to_nat_inplace<double>(z.as<double>(), np * K, st));
+    HIPCHK(launch_state_to_nat_inplace<double>(yz.as<double>(), np * K, st));
+    HIPCHK(launch_sub_inplace<double>(z.as<double>(), yz.as<double>(), np * K * (int64_t)P, st));
+    std::swap(z.p, yz.p);   // z <- z, yz <- y
+    zmode = 0;
+    zt = ZT_NONE;
   }
   // state a -> (z, y) materialised in place (objective, outputs)
   void materialize_z() {
     if (zmode == 0) return;
+    zt = ZT_NONE;   // `yz` receives y
     if (zmode == 2) {   // state order -> natural a in yz, then (z, y) from it
       HIPCHK(launch_state_to_nat<double>(z.as<double>(), yz.as<double>(), np * K, st));
       HIPCHK(launch_zmat<double>(yz.as<double>(), yz.as<double>(), W.as<cpx<double>>(), dws,
@@ -987,26 +1044,53 @@ struct Session2D {
     // ---- Z iterations (dP:147-168) ----
     const bool want_oz = verbose_refresh_z() || p.trace_objective;
     int nz = 0;
+    // z_diff of iteration iz (dP:156-157, dZ:163-164) from `count` partial pairs
+    auto z_test = [&](int iz, int64_t count) {
+      HIPCHK(launch_sum_pairs<double>(znorm.as<double>(), (int)count, pair.as<double>(), st));
+      allreduce(pair.as<double>(), 2);
+      double h2[2];
+      pair_to_host(h2);
+      const double zd = std::sqrt(h2[0]) / std::sqrt(h2[1]);
+      last_z = zd;
+      tr_zd[(size_t)it * p.max_it_z + iz] = zd;
+      return zd;
+    };
+    // register-line z-step with tol (zline.hip): a launch measures the iterate it
+    // starts from, so the test of iteration iz arrives with launch iz + 1, which
+    // was then speculative when the test fires (zl_rollback); the objective's
+    // materialisation measures without the lag (zl_materialize_tol)
+    const bool zl_tol = zl_on && tol_on;
+    bool zbreak = false;
     for (int iz = 0; iz < p.max_it_z; ++iz) {
-      timed(0, [&] { zstep_iter(tol_on); });
+      bool lagged = false;
+      timed(0, [&] { lagged = zstep_iter(tol_on); });
       ++nz;
+      if (lagged && z_test(iz - 1, np) < p.tol) {   // dP:165-167 for iteration iz - 1
+        zl_rollback();
+        --nz;
+        zbreak = true;
+        break;
+      }
       double zd = std::numeric_limits<double>::quiet_NaN();
-      if (tol_on) {
-        HIPCHK(launch_sum_pairs<double>(znorm.as<double>(), (int)(np * K * Tn),
-                                        pair.as<double>(), st));
-        allreduce(pair.as<double>(), 2);
-        double h2[2];
-        pair_to_host(h2);
-        zd = std::sqrt(h2[0]) / std::sqrt(h2[1]);
-        last_z = zd;
-        tr_zd[(size_t)it * p.max_it_z + iz] = zd;
+      if (zl_tol && want_oz) {
+        zl_materialize_tol();
+        zd = z_test(iz, np * K);
+      } else if (tol_on && !zl_tol) {
+        zd = z_test(iz, np * K * Tn);
       }
       if (want_oz) {
         const double o = objective_timed(dhat.as<cpx<double>>());
         if (verbose_refresh_z()) obj_z = o;
         if (p.trace_objective) tr_oz[(size_t)it * p.max_it_z + iz] = o;
       }
-      if (tol_on && zd < p.tol) break;  // dP:165-167
+      if (tol_on && zd < p.tol) {  // dP:165-167
+        zbreak = true;
+        break;
+      }
+    }
+    if (zl_tol && !zbreak && zt == ZT_PREV) {   // the last iteration's test
+      zl_finalize();
+      z_test(nz - 1, np);
     }
     HIPCHK(hipEventRecord(e1, st));
     HIPCHK(hipEventSynchronize(e1));

@@ -71,10 +71,15 @@ hipError_t launch_zhat_split(const T* A, const cpx<T>* W, const cpx<T>* dcorr, c
 // mode 0: (z, y) materialised in Zn / Yn (natural layout); mode 2: state in A.
 bool zline_grid(const Grid2D& G);
 size_t zline_smem_bytes();
+// tol: 0 off; 1 z of the starting iterate -> Zt (state order); 2 also the patch
+// sums of ||z - Zt||^2, ||z||^2 -> zpart[2p..2p+1]; mode 3 = finalize (tol 2, no advance).
 template <typename T>
 hipError_t launch_zline(const T* A, T* Ao, const T* Zn, const T* Yn, cpx<T>* W, const cpx<T>* Bs,
                         const cpx<T>* dcorr, const cpx<T>* dhat, const T* sden, int64_t npatch,
-                        int K, T theta, int mode, hipStream_t st);
+                        int K, T theta, int mode, hipStream_t st, int tol = 0, T* Zt = nullptr,
+                        T* zpart = nullptr);
+template <typename T>
+hipError_t launch_state_to_nat_inplace(T* a, int64_t count, hipStream_t st);
 template <typename T>
 hipError_t launch_to_slots(const cpx<T>* src, cpx<T>* dst, int64_t count, hipStream_t st);
 template <typename T>
@@ -189,5 +194,7 @@ hipError_t launch_embed_filters(const T* d0, T* D, int nrep, int K, int psf, con
                                 int Tn, hipStream_t st);
 template <typename T>
 hipError_t launch_replicate(const T* src, T* dst, int64_t n, int nrep, hipStream_t st);
+template <typename T>
+hipError_t launch_sub_inplace(T* a, const T* b, int64_t n, hipStream_t st);
 
 }  // namespace ccsc

@@ -4,6 +4,8 @@
 // (dZ:44-47 gives every block the same z0, Q4).
 #include "kernels.hpp"
 
+#include <algorithm>
+
 namespace ccsc {
 
 __device__ __forceinline__ uint64_t mix64(uint64_t x) {
@@ -86,6 +88,24 @@ hipError_t launch_replicate(const T* src, T* dst, int64_t n, int nrep, hipStream
   return hipSuccess;
 }
 
+// a <- a - b over n elements (grid-stride: z-sized arrays exceed 2^32 work-items)
+template <typename T>
+__global__ void k_sub_inplace(T* __restrict__ a, const T* __restrict__ b, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    a[i] -= b[i];
+}
+
+template <typename T>
+hipError_t launch_sub_inplace(T* a, const T* b, int64_t n, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const int64_t want = (n + 255) / 256;
+  const unsigned grid = (unsigned)std::min<int64_t>(want, 256 * 64);
+  hipLaunchKernelGGL(k_sub_inplace<T>, dim3(grid), dim3(256), 0, st, a, b, n);
+  return hipGetLastError();
+}
+
+template hipError_t launch_sub_inplace<double>(double*, const double*, int64_t, hipStream_t);
 template hipError_t launch_randn<double>(double*, int64_t, uint64_t, uint64_t, hipStream_t);
 template hipError_t launch_embed_filters<double>(const double*, double*, int, int, int,
                                                  const Grid2D&, int, hipStream_t);

@@ -121,13 +121,28 @@ __device__ __forceinline__ int fresh(int v) {
 // A holds the state in state order and W the previous w (bin-slot order) solved
 // with dcorr.  Out: Ao <- a' (state order; Ao may alias A, or Zn in mode 0),
 // W <- w.  Bs, dcorr, dhat, sden in bin-slot order.
-template <typename T, int MODE>
+//
+// The tol test (dP:156-157 / dZ:163-169: ||z - z_old|| / ||z|| after every
+// z-iteration) without a third z-sized buffer: the z of the iterate a launch
+// starts from, z_cur = (u - y)(A) + corr (mode 2) or the materialised z (mode 0),
+// is formed in registers anyway; TOL 1 stores it in state order to Zt (the
+// otherwise idle y buffer; in mode 0 Zt may alias Yn: read before written),
+// TOL 2 also reads the z before it from Zt and adds ||z_cur - z_prev||^2 and
+// ||z_cur||^2 of the patch into zpart[2p], [2p + 1] -- the test for the iterate
+// the launch started from, one launch late (the engine treats the launch as
+// speculative).  MODE 3 ("finalize"): TOL 2 without advancing:
+// no state write, no R2C, W untouched.
+template <typename T, int MODE, int TOL>
 __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn, const T* Yn,
                                                   cpx<T>* __restrict__ W,
                                                   const cpx<T>* __restrict__ Bs,
                                                   const cpx<T>* __restrict__ dcorr,
                                                   const cpx<T>* __restrict__ dhat,
-                                                  const T* __restrict__ sden, int K, T theta) {
+                                                  const T* __restrict__ sden, int K, T theta,
+                                                  T* Zt, T* __restrict__ zpart) {
+  static_assert(MODE == 0 || MODE == 2 || MODE == 3, "zline mode");
+  static_assert(TOL >= 0 && TOL <= 2 && (MODE != 0 || TOL < 2) && (MODE != 3 || TOL == 2),
+                "zline tol variant");
   using V2 = typename vec2_t<T>::type;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   cpx<T>* sT = reinterpret_cast<cpx<T>*>(smem);
@@ -138,6 +153,7 @@ __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn
   const cpx<T>* Wp = W + p * zl::F;
   // the last wave owns one y-line and no x-line (55 row pairs = 11 waves of 5)
   const bool xwave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6) < 11;
+  T nd = (T)0, nz = (T)0;   // TOL 2: ||z_cur - z_prev||^2, ||z_cur||^2 of the lanes' own elements
 
   for (int k = 0; k < K; ++k) {
     // lane roles, recomputed per slice from an opaque thread index (see fresh())
@@ -153,7 +169,7 @@ __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn
     const int64_t sl = (p * K + k) * zl::P;
     cpx<T> zc[11];   // c = u - y of the row pair (x-lines, layout A) for the R2C
     const uint32_t po = (uint32_t)(j * 10 + fresh(sa)) * 16u;   // pair n2 at po + n2*550*16
-    if constexpr (MODE == 2) {
+    if constexpr (MODE >= 2) {
       // ---- P1: y-C2R of conj(dcorr_k) w from bins to T[y][c] ----
       const cpx<T>* dk = dcorr + (int64_t)k * zl::F;
       const uint32_t bo = (uint32_t)(c * 11 + sb) * 16u;
@@ -187,13 +203,34 @@ __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn
         V2 av[11];
 #pragma unroll
         for (int n2 = 0; n2 < 11; ++n2) av[n2] = zld<V2>(A + sl, po + n2 * 550 * 16);
+        V2 zo[TOL == 2 ? 11 : 1];
+        if constexpr (TOL == 2) {
+#pragma unroll
+          for (int n2 = 0; n2 < 11; ++n2) zo[n2] = zld<V2>(Zt + sl, po + n2 * 550 * 16);
+        }
+        // lanes that own their elements (not a clamped duplicate) count in the norms
+        const T own = (s < 10 && lane < 55) ? (T)1 : (T)0;
         inv_line<T, 1>(zb, Ex, s3, [&](int n2, cpx<T> corr) {
           V2 a = av[n2];
-          a.x = soft_l(a.x, theta) + corr.x;
-          a.y = soft_l(a.y, theta) + corr.y;
-          zst<V2>(Ao + sl, po + n2 * 550 * 16, a);
-          const T ux = soft_l(a.x, theta), uy = soft_l(a.y, theta);
-          zc[n2] = {ux - (a.x - ux), uy - (a.y - uy)};
+          const T sx = soft_l(a.x, theta), sy = soft_l(a.y, theta);
+          if constexpr (TOL >= 1) {   // z_cur = (u - y)(A) + corr
+            V2 zn;
+            zn.x = (sx - (a.x - sx)) + corr.x;
+            zn.y = (sy - (a.y - sy)) + corr.y;
+            if constexpr (TOL == 2) {
+              const T ex = zn.x - zo[n2].x, ey = zn.y - zo[n2].y;
+              nd += own * (ex * ex + ey * ey);
+              nz += own * (zn.x * zn.x + zn.y * zn.y);
+            }
+            zst<V2>(Zt + sl, po + n2 * 550 * 16, zn);
+          }
+          if constexpr (MODE == 2) {
+            a.x = sx + corr.x;
+            a.y = sy + corr.y;
+            zst<V2>(Ao + sl, po + n2 * 550 * 16, a);
+            const T ux = soft_l(a.x, theta), uy = soft_l(a.y, theta);
+            zc[n2] = {ux - (a.x - ux), uy - (a.y - uy)};
+          }
         });
       }
     } else {
@@ -215,11 +252,30 @@ __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn
           zc[n2] = {ux - (a.x - ux), uy - (a.y - uy)};
         }
       }
+      V2 zv[TOL == 1 ? 11 : 1];
+      if constexpr (TOL == 1) {
+        if (xwave) {
+          const T* z0 = Zn + sl + 2 * j * zl::X;
+#pragma unroll
+          for (int n2 = 0; n2 < 11; ++n2) {
+            const int x = mod110(11 * sa + 10 * n2);
+            zv[n2].x = z0[x];
+            zv[n2].y = z0[zl::X + x];
+          }
+        }
+      }
       __syncthreads();   // the slice is read in natural order before it is rewritten in state order
       if (xwave) {
 #pragma unroll
-        for (int n2 = 0; n2 < 11; ++n2) zst<V2>(Ao + sl, po + n2 * 550 * 16, av[n2]);
+        for (int n2 = 0; n2 < 11; ++n2) {
+          zst<V2>(Ao + sl, po + n2 * 550 * 16, av[n2]);
+          if constexpr (TOL == 1) zst<V2>(Zt + sl, po + n2 * 550 * 16, zv[n2]);
+        }
       }
+    }
+    if constexpr (MODE == 3) {
+      lds_sync();   // T is rewritten by the next slice's P1
+      continue;
     }
     // ---- P5: x-R2C of the row pair -> Z_j into rows 2j, 2j+1 of T ----
     if (xwave) {
@@ -256,6 +312,28 @@ __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn
       });
     }
   }
+  if constexpr (TOL == 2) {   // patch sums of the tol norms (T is free after the last slice)
+    T* red = reinterpret_cast<T*>(smem);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    nd = wave_sum(nd);
+    nz = wave_sum(nz);
+    lds_sync();
+    if (lane == 0) {
+      red[2 * wave] = nd;
+      red[2 * wave + 1] = nz;
+    }
+    lds_sync();
+    if (threadIdx.x == 0) {
+      T sd = 0, sz = 0;
+      for (int w = 0; w < zl::NW; ++w) {
+        sd += red[2 * w];
+        sz += red[2 * w + 1];
+      }
+      zpart[2 * p] = sd;
+      zpart[2 * p + 1] = sz;
+    }
+  }
+  if constexpr (MODE == 3) return;
   // w = (B - acc) * sden  (sden = 1/((rho + s) X Y)); each lane owns its slots
   {
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -296,19 +374,45 @@ __global__ void k_state_to_nat(const T* __restrict__ st, T* __restrict__ nat) {
     nat[b * zl::P + e] = st[b * zl::P + zl::state_off(e)];
 }
 
+// in place: slice <- natural order of its state-order contents (one workgroup per
+// slice; the whole slice passes through LDS, 96.8 KB)
+template <typename T>
+__global__ __launch_bounds__(1024) void k_state_to_nat_inplace(T* a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  T* s = reinterpret_cast<T*>(smem);
+  T* sl = a + (int64_t)blockIdx.x * zl::P;
+  for (int q = threadIdx.x; q < zl::P; q += 1024) s[q] = sl[q];
+  __syncthreads();
+  for (int e = threadIdx.x; e < zl::P; e += 1024) sl[e] = s[zl::state_off(e)];
+}
+
 bool zline_grid(const Grid2D& G) { return grid_is<Grid110>(G); }
+
+template <typename T, int MODE, int TOL>
+static void zline_go(hipStream_t st, int64_t npatch, const T* A, T* Ao, const T* Zn, const T* Yn,
+                     cpx<T>* W, const cpx<T>* Bs, const cpx<T>* dcorr, const cpx<T>* dhat,
+                     const T* sden, int K, T theta, T* Zt, T* zpart) {
+  hipLaunchKernelGGL((k_zline<T, MODE, TOL>), dim3((unsigned)npatch), dim3(zl::NT), zl::kSmem, st,
+                     A, Ao, Zn, Yn, W, Bs, dcorr, dhat, sden, K, theta, Zt, zpart);
+}
 
 template <typename T>
 hipError_t launch_zline(const T* A, T* Ao, const T* Zn, const T* Yn, cpx<T>* W, const cpx<T>* Bs,
                         const cpx<T>* dcorr, const cpx<T>* dhat, const T* sden, int64_t npatch,
-                        int K, T theta, int mode, hipStream_t st) {
+                        int K, T theta, int mode, hipStream_t st, int tol, T* Zt, T* zpart) {
   if (npatch <= 0) return hipSuccess;
-  if (mode == 0)
-    hipLaunchKernelGGL((k_zline<T, 0>), dim3((unsigned)npatch), dim3(zl::NT), zl::kSmem, st, A, Ao,
-                       Zn, Yn, W, Bs, dcorr, dhat, sden, K, theta);
-  else
-    hipLaunchKernelGGL((k_zline<T, 2>), dim3((unsigned)npatch), dim3(zl::NT), zl::kSmem, st, A, Ao,
-                       Zn, Yn, W, Bs, dcorr, dhat, sden, K, theta);
+  if (tol && !Zt) return hipErrorInvalidValue;
+  if ((tol == 2 || mode == 3) && !zpart) return hipErrorInvalidValue;
+  const int v = mode * 10 + tol;
+  switch (v) {
+    case 0: zline_go<T, 0, 0>(st, npatch, A, Ao, Zn, Yn, W, Bs, dcorr, dhat, sden, K, theta, Zt, zpart); break;
+    case 1: zline_go<T, 0, 1>(st, npatch, A, Ao, Zn, Yn, W, Bs, dcorr, dhat, sden, K, theta, Zt, zpart); break;
+    case 20: zline_go<T, 2, 0>(st, npatch, A, Ao, Zn, Yn, W, Bs, dcorr, dhat, sden, K, theta, Zt, zpart); break;
+    case 21: zline_go<T, 2, 1>(st, npatch, A, Ao, Zn, Yn, W, Bs, dcorr, dhat, sden, K, theta, Zt, zpart); break;
+    case 22: zline_go<T, 2, 2>(st, npatch, A, Ao, Zn, Yn, W, Bs, dcorr, dhat, sden, K, theta, Zt, zpart); break;
+    case 32: zline_go<T, 3, 2>(st, npatch, A, Ao, Zn, Yn, W, Bs, dcorr, dhat, sden, K, theta, Zt, zpart); break;
+    default: return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 
@@ -332,14 +436,23 @@ hipError_t launch_state_to_nat(const T* st_, T* nat, int64_t count, hipStream_t 
   return hipGetLastError();
 }
 
+template <typename T>
+hipError_t launch_state_to_nat_inplace(T* a, int64_t count, hipStream_t st) {
+  if (count <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_state_to_nat_inplace<T>, dim3((unsigned)count), dim3(1024),
+                     (size_t)zl::P * sizeof(T), st, a);
+  return hipGetLastError();
+}
+
 size_t zline_smem_bytes() { return zl::kSmem; }
 
 template hipError_t launch_zline<double>(const double*, double*, const double*, const double*,
                                          cpx<double>*, const cpx<double>*, const cpx<double>*,
                                          const cpx<double>*, const double*, int64_t, int, double,
-                                         int, hipStream_t);
+                                         int, hipStream_t, int, double*, double*);
 template hipError_t launch_to_slots<double>(const cpx<double>*, cpx<double>*, int64_t, hipStream_t);
 template hipError_t launch_to_slots_real<double>(const double*, double*, hipStream_t);
 template hipError_t launch_state_to_nat<double>(const double*, double*, int64_t, hipStream_t);
+template hipError_t launch_state_to_nat_inplace<double>(double*, int64_t, hipStream_t);
 
 }  // namespace ccsc

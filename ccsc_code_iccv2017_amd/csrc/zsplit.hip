@@ -219,10 +219,11 @@ __global__ __launch_bounds__(NT) void k_zsplit(const T* A, T* Ao, const T* __res
 //   u = soft(a), y = a - u, z = (u - y) + ifft2(conj(dcorr_k) w_p)
 // Zd may alias As (each element read, then written, by one thread).  With
 // zold != NULL also ||Zd - zold||^2, ||Zd||^2 per slice (the tol test,
-// dP:156-157; zold may alias Zd, read before written).
+// dP:156-157; zold may alias Zd or Yz: each element is read before it is written,
+// by the same thread).
 // WSLOT: W and dcorr in the bin-slot order of zline.hip (110 grid only).
 template <typename T, class FG, bool WSLOT = false>
-__global__ __launch_bounds__(kNT) void k_zmat(const T* As, T* __restrict__ Yz,
+__global__ __launch_bounds__(kNT) void k_zmat(const T* As, T* Yz,
                                               const cpx<T>* __restrict__ W,
                                               const cpx<T>* __restrict__ dcorr, T* Zd,
                                               const T* zold, T* __restrict__ znorm,

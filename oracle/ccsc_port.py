@@ -58,7 +58,7 @@ class DzPort:
 
     def __init__(self, b, d0, z0, lambda_prior, *, ni, rho_d=5000.0, rho_z=1.0, theta_div=1.0,
                  max_it_d=5, max_it_z=10, workers=None, N=None, rank=0, world=1,
-                 allreduce=None, bcast=None, replicate_z0=True):
+                 allreduce=None, bcast=None, replicate_z0=True, tol=0.0):
         self.w = workers if workers is not None else (os.cpu_count() or 1)
         b = np.asarray(b, dtype=np.float64)
         psf = d0.shape[0]
@@ -85,6 +85,12 @@ class DzPort:
         self.z = np.concatenate([z0] * self.Nloc, axis=3) if replicate_z0 else z0.copy()  # dZ:44-47 / dP:45
         self.yz = np.zeros_like(self.z)
         self.dhat = None
+        # tol > 0 (single rank): the d / z break tests dZ:125-132, 163-169 (dP:125-132,
+        # 156-167) and the outer termination dZ:186-188; per outer iteration the
+        # relative changes and the inner counts
+        self.tol = tol
+        self.trace = {"d_diff": [], "z_diff": [], "n_d": [], "n_z": []}
+        self.finished = False
 
     def dhat_full(self):
         """Block 1's filter spectrum on the full X x Y grid (the objective's dup{1})."""
@@ -107,7 +113,9 @@ class DzPort:
         r, s = self.r, 2 * self.r + 1
         sup = (np.r_[X - r:X, 0:r + 1][:, None], np.r_[Y - r:Y, 0:r + 1][None, :])
         dh_loc = None
+        dds, zds = [], []
         for _ in range(self.mid):
+            d_old = self.D[0]
             u = self.u
             for nn in range(self.Nloc):
                 self.yD[nn] = self.yD[nn] + (self.D[nn] - u)
@@ -123,11 +131,15 @@ class DzPort:
             full = np.zeros_like(u)
             full[sup[0], sup[1]] = tot / self.N
             self.u = kernel_constraint_proj(full, r, 2)
+            dds.append(np.linalg.norm(self.D[0] - d_old) / np.linalg.norm(self.D[0]))
+            if self.tol > 0 and dds[-1] < self.tol:
+                break
         self.dhat = self.bcast(np.ascontiguousarray(dh_loc))         # block 1 lives on rank 0
         # Z iterations (dZ:147-172) with the simplified Sherman-Morrison solve
         dh = self.dhat                                              # [Xh, Y, K]
         s = np.sum(np.abs(dh) ** 2, axis=2)
         for _ in range(self.miz):
+            z_old = self.z
             a = self.z + self.yz
             aa = np.abs(a)
             with np.errstate(divide="ignore", invalid="ignore"):
@@ -139,4 +151,11 @@ class DzPort:
             wv = (self.Bh - rr) / (self.rho_z + s)[..., None]
             Zh = Ch + np.conj(dh)[..., None] * wv[:, :, None, :]
             self.z = _c2r(Zh, X, Y, w)
+            zds.append(np.linalg.norm(self.z - z_old) / np.linalg.norm(self.z))
+            if self.tol > 0 and zds[-1] < self.tol:
+                break
+        for key, v in (("d_diff", dds), ("z_diff", zds), ("n_d", len(dds)), ("n_z", len(zds))):
+            self.trace[key].append(v)
+        if self.tol > 0 and zds[-1] < self.tol and dds[-1] < self.tol:
+            self.finished = True
         return self

@@ -237,3 +237,46 @@ def test_zline_state_path_matches_port(gpu_ctx, miz):
     port.outer()
     assert _rel(z_e, port.z) < 1e-7
     assert _rel(d_e, O.crop_filters(port.D[0], 2, 5)) < 1e-7
+
+
+@pytest.mark.parametrize("verbose", ["none", "brief"])
+@pytest.mark.parametrize("variant", ["dz", "dp"])
+def test_zline_tol_matches_port(gpu_ctx, variant, verbose):
+    """tol > 0 on C2's 110x110 grid (the reference driver runs tol = 1e-3,
+    learn_kernels_2D_large.m:24) through the register-line z-step, which keeps z_old in
+    the y buffer (no third z-sized buffer): 'none' takes the one-launch-late test with
+    the speculative launch rolled back when it fires, 'brief' the objective's
+    materialisation.  Inner counts, d/z diffs and the iterate match the port, whose
+    tol branches are pinned to the literal oracle (tests/test_oracle.py); the tol is
+    picked >= 5% away from every diff, so no break decision sits on round-off."""
+    from ccsc_code_iccv2017_amd import learners as E
+    from oracle.ccsc_port import DzPort
+    from tests.test_oracle import pick_tol
+    K, n, ni, mid, miz = 4, 4, 2, 3, 8
+    rng = np.random.default_rng(77)
+    b = rng.standard_normal((100, 100, n))
+    d0 = rng.standard_normal((11, 11, K))
+    z0 = rng.standard_normal((110, 110, K, ni if variant == "dz" else n))
+    if variant == "dz":
+        cst, fn = dict(), E.admm_learn_conv2D_large_dzParallel
+    else:
+        cst = dict(rho_d=500.0, rho_z=50.0, theta_div=50.0, replicate_z0=False)
+        fn = E.admm_learn_conv2D_large_dParallel
+    p0 = DzPort(b, d0, z0, 1.0, ni=ni, max_it_d=mid, max_it_z=miz, **cst)
+    p0.outer()
+    tol = pick_tol(p0.trace["z_diff"][0], p0.trace["d_diff"][0], at=3)
+    port = DzPort(b, d0, z0, 1.0, ni=ni, max_it_d=mid, max_it_z=miz, tol=tol, **cst)
+    for _ in range(3):
+        if not port.finished:
+            port.outer()
+    assert port.trace["n_z"][0] < miz          # a z break fires in outer iteration 1
+    d_e, z_e, DZ_e, it_e = fn(b, [11, 11, K], 1.0, 1.0, 3, tol, verbose, {"d": d0, "z": z0},
+                              ni=ni, max_it_d=mid, max_it_z=miz, ctx=gpu_ctx)
+    tr = it_e["trace"]
+    np.testing.assert_array_equal(tr["n_z"], port.trace["n_z"])
+    np.testing.assert_array_equal(tr["n_d"], port.trace["n_d"])
+    for i, (dd, zd) in enumerate(zip(port.trace["d_diff"], port.trace["z_diff"])):
+        np.testing.assert_allclose(tr["d_diff"][i, :len(dd)], dd, rtol=1e-6)
+        np.testing.assert_allclose(tr["z_diff"][i, :len(zd)], zd, rtol=1e-6)
+    assert _rel(z_e, port.z) < 1e-7
+    assert _rel(d_e, O.crop_filters(port.D[0], 2, 5)) < 1e-7

@@ -142,6 +142,45 @@ def test_half_spectrum_port_equals_literal_oracle_dparallel():
     np.testing.assert_allclose(O.crop_filters(p.D[0], 2, 2), o[0], rtol=0, atol=1e-12)
 
 
+def pick_tol(zdiffs, ddiffs, at=2):
+    """A tol between two consecutive z-diffs of outer iteration 1 (from z-iteration `at`
+    on, so the z break fires after a few iterations) that is >= 5% away from every
+    recorded d- and z-diff: no break decision sits on a round-off margin."""
+    vals = np.array(list(zdiffs) + list(ddiffs))
+    for i in list(range(at, len(zdiffs))) + list(range(1, at)):
+        tol = float(np.sqrt(zdiffs[i - 1] * zdiffs[i]))
+        if zdiffs[i] < tol and np.all(np.abs(vals - tol) > 0.05 * tol):
+            return tol
+    raise AssertionError("no tol with margins")
+
+
+@pytest.mark.parametrize("variant", ["dz", "dp"])
+def test_port_tol_breaks_equal_literal_oracle(variant):
+    """The port's tol tests (d: dZ:125-132, z: dZ:163-169, outer: dZ:186-188) take the
+    literal oracle's branches: same inner counts, d/z diffs, iterate."""
+    rng = _rng(26)
+    b = rng.standard_normal((10, 9, 6))
+    d0 = rng.standard_normal((5, 5, 3))
+    z0 = rng.standard_normal((14, 13, 3, 3 if variant == "dz" else 6))
+    init = {"d": d0, "z": z0}
+    fn = O.learn_2d_dzparallel if variant == "dz" else O.learn_2d_dparallel
+    kw = {} if variant == "dz" else dict(rho_d=500.0, rho_z=50.0, theta_div=50.0, max_it_d=10,
+                                         replicate_z0=False)
+    tr0 = fn(b, [5, 5, 3], 1.0, 1.0, 1, 0.0, "none", init, ni=3, trace_objective=True)[4]
+    tol = pick_tol(tr0["z_diff"][0], tr0["d_diff"][0], at=3)
+    o = fn(b, [5, 5, 3], 1.0, 1.0, 3, tol, "none", init, ni=3, trace_objective=True)
+    p = DzPort(b, d0, z0, 1.0, ni=3, workers=1, tol=tol, **kw)
+    for _ in range(3):
+        if not p.finished:
+            p.outer()
+    tr = o[4]
+    assert p.trace["n_z"] == tr["n_z"] and p.trace["n_d"] == tr["n_d"]
+    assert tr["n_z"][0] < 10           # the z break fired
+    for a, e in zip(p.trace["z_diff"] + p.trace["d_diff"], tr["z_diff"] + tr["d_diff"]):
+        np.testing.assert_allclose(a, e, rtol=1e-9)
+    np.testing.assert_allclose(p.z, o[1], rtol=0, atol=1e-11)
+
+
 @pytest.mark.parametrize("rho", [500.0, 5000.0])
 def test_woodbury_form_conditioning_large_codes(rho):
     """The reference's pinv(rho I + A A^H) form (dP:230-236) == the K x K inverse at
