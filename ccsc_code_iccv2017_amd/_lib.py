@@ -20,7 +20,7 @@ CCSC_E_UNSUPPORTED = -5
 CCSC_E_STATE = -6
 
 CCSC_DPAR, CCSC_DZPAR, CCSC_L3D, CCSC_L4D, CCSC_HS23 = 0, 1, 2, 3, 4
-ABI_VERSION = 3
+ABI_VERSION = 4
 VERBOSE = {"none": 0, "brief": 1, "all": 2}
 CCSC_FP64, CCSC_FP32 = 0, 1
 DFACTOR = {"auto": 0, "cholesky": 1, "woodbury": 2}
@@ -96,6 +96,7 @@ SIGNATURES = {
                                  C.c_size_t]),
     "ccsc_create_hostcomm": (C.c_void_p, [C.c_int32, C.c_int32, C.c_int32, COMM_FN, C.c_void_p,
                                           C.c_char_p, C.c_size_t]),
+    "ccsc_create_multi": (C.c_void_p, [C.POINTER(C.c_int32), C.c_int32, C.c_char_p, C.c_size_t]),
     "ccsc_destroy": (None, [C.c_void_p]),
     "ccsc_learn": (C.c_int32, [C.c_void_p, C.POINTER(Problem), _dp, _dp, _dp,
                                C.POINTER(Outputs), C.POINTER(IterLog), CB, C.c_void_p,

@@ -15,6 +15,9 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
+#include <mutex>
+#include <thread>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -385,6 +388,62 @@ struct DevBuf {
 
 using namespace ccsc;
 
+namespace ccsc {
+// In-process exchange between the device threads of a multi-device context whose
+// device list repeats a device (RCCL needs distinct GPUs): every rank deposits its
+// buffer, the last to arrive combines them in rank order (deterministic sums) and
+// releases the others.  abort() wakes every waiter when one device thread failed.
+struct HostGroup {
+  int n;
+  std::mutex mu;
+  std::condition_variable cv;
+  int arrived = 0;
+  uint64_t gen = 0;
+  bool aborted = false;
+  std::vector<std::vector<double>> slot;
+  std::vector<double> res;
+  explicit HostGroup(int n_) : n(n_), slot(n_) {}
+  int exchange(int rank, int op, double* buf, int64_t count) {
+    std::unique_lock<std::mutex> lk(mu);
+    if (aborted) return -1;
+    const uint64_t g = gen;
+    slot[rank].assign(buf, buf + count);
+    if (++arrived == n) {
+      if (op == CCSC_COMM_BCAST0) {
+        res = slot[0];
+      } else {
+        res = slot[0];
+        for (int r = 1; r < n; ++r)
+          for (int64_t i = 0; i < count; ++i) res[i] += slot[r][i];
+      }
+      arrived = 0;
+      ++gen;
+      cv.notify_all();
+    } else {
+      cv.wait(lk, [&] { return gen != g || aborted; });
+      if (aborted) return -1;
+    }
+    // the next exchange cannot complete (and replace res) before every rank has
+    // arrived at it, i.e. has copied this result
+    std::copy(res.begin(), res.begin() + count, buf);
+    return 0;
+  }
+  void abort() {
+    std::lock_guard<std::mutex> lk(mu);
+    aborted = true;
+    cv.notify_all();
+  }
+};
+struct HostGroupRank {
+  HostGroup* g;
+  int rank;
+};
+static int32_t host_group_fn(void* user, int32_t op, double* buf, int64_t count) {
+  auto* u = static_cast<HostGroupRank*>(user);
+  return u->g->exchange(u->rank, op, buf, count);
+}
+}  // namespace ccsc
+
 struct ccsc_ctx {
   int device = 0;
   int rank = 0;
@@ -394,6 +453,11 @@ struct ccsc_ctx {
   ccsc_comm_fn hostfn = nullptr;   // host-staged transport (tests)
   void* hostuser = nullptr;
   std::vector<double> stage;
+  // single-process multi-device context (ccsc_create_multi): one sub-context per
+  // device, rank i of ndev, driven by one host thread each inside ccsc_learn
+  std::vector<ccsc_ctx*> subs;
+  std::unique_ptr<ccsc::HostGroup> hg;           // repeated devices: in-process exchange
+  std::vector<ccsc::HostGroupRank> hg_ranks;
 };
 
 namespace ccsc {
@@ -1589,6 +1653,89 @@ struct ccsc_session {
   ccsc_ctx* ctx() const { return s2 ? s2->ctx : hs->ctx; }
 };
 
+namespace ccsc {
+// ccsc_learn on a multi-device context: the caller's whole problem (b, z0, outputs
+// over all n patches) is split at the block boundaries of ccsc_shard; rank i runs
+// on sub-context i in its own host thread, the calling thread drives rank 0 and is
+// the only one that calls back (include/ccsc.h threading rule).  Collectives
+// inside the sessions (RCCL, or the in-process exchange) keep the ranks in step.
+static void learn_group(ccsc_ctx* ctx, const ccsc_problem& pin, const double* b, const double* d0,
+                        const double* z0, ccsc_outputs* out, ccsc_iterlog* log, ccsc_cb cb,
+                        void* user) {
+  ccsc_problem q = pin;
+  resolve_problem(q);
+  Geom g;
+  check_supported(q, &g);
+  const int nd = (int)ctx->subs.size();
+  const bool is4 = q.variant == CCSC_L4D, is3 = q.variant == CCSC_L3D;
+  const int64_t NV = (int64_t)q.views[0] * q.views[1];
+  const int64_t bpatch = q.sb[0] * q.sb[1] * (is3 ? q.sb[2] : 1) * NV;   // b [sb.., (U,V), n]
+  const int64_t zpatch = (int64_t)q.K * (int64_t)g.P();                  // z [X,Y,(T),K, n]
+  const int64_t xpatch = is4 ? NV * q.sb[0] * q.sb[1] : (int64_t)g.P();  // DZ per patch
+  const int64_t KG = (int64_t)q.K * NV;
+  const int64_t SS = (int64_t)q.psf * q.psf * (is3 ? q.psf : 1);
+  std::vector<std::vector<double>> dscr(nd), oscr(nd);
+  std::vector<std::string> errs(nd);
+  std::vector<int> codes(nd, CCSC_OK);
+  auto fail_all = [&] {
+    if (ctx->hg) ctx->hg->abort();
+    for (ccsc_ctx* u : ctx->subs)
+      if (u->comm) ncclCommAbort(u->comm), u->comm = nullptr;
+  };
+  auto run = [&](int i) {
+    try {
+      ccsc_ctx* u = ctx->subs[i];
+      HIPCHK(hipSetDevice(u->device));
+      int64_t b0 = 0, nb = 0;
+      shard(q, i, nd, b0, nb);
+      const int64_t p0 = b0 * q.ni;
+      const double* zi = z0 ? (q.variant == CCSC_DZPAR ? z0 : z0 + p0 * zpatch) : nullptr;
+      Session2D S(u, q, b + p0 * bpatch, d0, zi);
+      S.ensure_trace_capacity(S.p.max_it);
+      for (int it = 0; it < S.p.max_it && !S.finished; ++it) {
+        S.outer_iteration();
+        if (i == 0 && cb) cb(user, S.outer_done, S.v_obj_d.back(), S.v_obj_z.back(), S.v_tim.back());
+      }
+      ccsc_outputs o{};
+      if (out) {
+        // d_res and obj_val are collectives: every rank asks when the caller does
+        if (out->d_res) {
+          dscr[i].resize(i == 0 ? 0 : (size_t)(KG * SS));
+          o.d_res = i == 0 ? out->d_res : dscr[i].data();
+        }
+        if (out->obj_val) {
+          oscr[i].resize(1);
+          o.obj_val = i == 0 ? out->obj_val : oscr[i].data();
+        }
+        if (out->z_res) o.z_res = out->z_res + p0 * zpatch;
+        if (out->DZ) o.DZ = out->DZ + p0 * xpatch;
+      }
+      S.results(out ? &o : nullptr);
+      if (i == 0) S.iterlog(log);
+    } catch (const Err& e) {
+      errs[i] = e.what();
+      codes[i] = e.code;
+      fail_all();
+    } catch (const std::exception& e) {
+      errs[i] = e.what();
+      codes[i] = CCSC_E_INVALID;
+      fail_all();
+    }
+  };
+  std::vector<std::thread> th;
+  for (int i = 1; i < nd; ++i) th.emplace_back(run, i);
+  run(0);
+  for (auto& t : th) t.join();
+  HIPCHK(hipSetDevice(ctx->device));
+  for (int i = 0; i < nd; ++i)   // the first failure (others are its consequences)
+    if (codes[i] != CCSC_OK && !errs[i].empty() && errs[i].find("host communicator") == std::string::npos)
+      throw Err(codes[i], "device " + std::to_string(ctx->subs[i]->device) + " (rank " +
+                              std::to_string(i) + "): " + errs[i]);
+  for (int i = 0; i < nd; ++i)
+    if (codes[i] != CCSC_OK) throw Err(codes[i], "rank " + std::to_string(i) + ": " + errs[i]);
+}
+}  // namespace ccsc
+
 // ===========================================================================
 // C-ABI
 // ===========================================================================
@@ -1697,8 +1844,58 @@ ccsc_ctx* ccsc_create_hostcomm(int32_t device, int32_t rank, int32_t nranks, ccs
   return rc == CCSC_OK ? ctx : nullptr;
 }
 
+ccsc_ctx* ccsc_create_multi(const int32_t* devices, int32_t ndev, char* err, size_t errlen) {
+  ccsc_ctx* ctx = nullptr;
+  const int rc = guarded(err, errlen, [&] {
+    if (!devices || ndev < 1) throw Err(CCSC_E_INVALID, "empty device list");
+    int count = 0;
+    HIPCHK(hipGetDeviceCount(&count));
+    for (int i = 0; i < ndev; ++i)
+      if (devices[i] < 0 || devices[i] >= count)
+        throw Err(CCSC_E_INVALID, "device " + std::to_string(devices[i]) + " out of range (" +
+                                      std::to_string(count) + " visible)");
+    std::unique_ptr<ccsc_ctx> c(new ccsc_ctx());
+    c->device = devices[0];
+    c->nranks = ndev;
+    HIPCHK(hipSetDevice(devices[0]));
+    HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    if (ndev > 1) {
+      bool distinct = true;
+      for (int i = 0; i < ndev; ++i)
+        for (int j = 0; j < i; ++j) distinct = distinct && devices[i] != devices[j];
+      std::vector<ncclComm_t> comms(ndev, nullptr);
+      if (distinct) {
+        NCCLCHK(ncclCommInitAll(comms.data(), ndev, devices));
+      } else {
+        c->hg.reset(new HostGroup(ndev));
+        c->hg_ranks.resize(ndev);
+      }
+      for (int i = 0; i < ndev; ++i) {
+        std::unique_ptr<ccsc_ctx> u(new ccsc_ctx());
+        u->device = devices[i];
+        u->rank = i;
+        u->nranks = ndev;
+        u->comm = comms[i];
+        if (c->hg) {
+          c->hg_ranks[i] = HostGroupRank{c->hg.get(), i};
+          u->hostfn = host_group_fn;
+          u->hostuser = &c->hg_ranks[i];
+        }
+        HIPCHK(hipSetDevice(devices[i]));
+        HIPCHK(hipStreamCreateWithFlags(&u->stream, hipStreamNonBlocking));
+        c->subs.push_back(u.release());
+      }
+      HIPCHK(hipSetDevice(devices[0]));
+    }
+    ctx = c.release();
+  });
+  return rc == CCSC_OK ? ctx : nullptr;
+}
+
 void ccsc_destroy(ccsc_ctx* ctx) {
   if (!ctx) return;
+  for (ccsc_ctx* u : ctx->subs) ccsc_destroy(u);
+  ctx->subs.clear();
   hipSetDevice(ctx->device);
   if (ctx->stream) hipStreamSynchronize(ctx->stream);
   if (ctx->comm) ncclCommDestroy(ctx->comm);
@@ -1713,6 +1910,9 @@ ccsc_session* ccsc_session_create(ccsc_ctx* ctx, const ccsc_problem* p, const do
     if (!ctx || !p) throw Err(CCSC_E_INVALID, "NULL ctx/problem");
     if (p->variant == CCSC_HS23)
       throw Err(CCSC_E_INVALID, "the 2-3D learner takes smooth_init: use ccsc_session_create_hs23");
+    if (!ctx->subs.empty())
+      throw Err(CCSC_E_UNSUPPORTED, "sessions run on a one-device context (one per rank); a "
+                                    "multi-device context serves ccsc_learn");
     HIPCHK(hipSetDevice(ctx->device));
     std::unique_ptr<ccsc_session> s(new ccsc_session());
     s->s2.reset(new Session2D(ctx, *p, b, d0, z0));
@@ -1727,6 +1927,8 @@ ccsc_session* ccsc_session_create_hs23(ccsc_ctx* ctx, const ccsc_problem* p, con
   ccsc_session* out = nullptr;
   guarded(err, errlen, [&] {
     if (!ctx || !p) throw Err(CCSC_E_INVALID, "NULL ctx/problem");
+    if (!ctx->subs.empty())
+      throw Err(CCSC_E_UNSUPPORTED, "the 2-3D learner runs on one device");
     HIPCHK(hipSetDevice(ctx->device));
     std::unique_ptr<ccsc_session> s(new ccsc_session());
     s->hs.reset(new SessionHS(ctx, *p, b, smooth_init, d0, z0));
@@ -1808,6 +2010,9 @@ int32_t ccsc_learn_hs23(ccsc_ctx* ctx, const ccsc_problem* p, const double* b,
                         size_t errlen) {
   return guarded(err, errlen, [&] {
     if (!ctx || !p) throw Err(CCSC_E_INVALID, "NULL ctx/problem");
+    if (!ctx->subs.empty())
+      throw Err(CCSC_E_UNSUPPORTED, "the 2-3D learner runs on one device (its d-solve couples "
+                                    "every image per frequency)");
     HIPCHK(hipSetDevice(ctx->device));
     SessionHS S(ctx, *p, b, smooth_init, d0, z0);
     S.ensure_trace_capacity(S.p.max_it);
@@ -1827,6 +2032,10 @@ int32_t ccsc_learn(ccsc_ctx* ctx, const ccsc_problem* p, const double* b, const 
     if (!ctx || !p) throw Err(CCSC_E_INVALID, "NULL ctx/problem");
     if (p->variant == CCSC_HS23)
       throw Err(CCSC_E_INVALID, "the 2-3D learner takes smooth_init: use ccsc_learn_hs23");
+    if (!ctx->subs.empty()) {
+      learn_group(ctx, *p, b, d0, z0, out, log, cb, user);
+      return;
+    }
     HIPCHK(hipSetDevice(ctx->device));
     Session2D S(ctx, *p, b, d0, z0);
     S.ensure_trace_capacity(S.p.max_it);

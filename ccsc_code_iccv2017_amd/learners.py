@@ -64,6 +64,27 @@ class Context:
             raise L.CCSCError(L.CCSC_E_HIP, eb.value.decode(errors="replace"))
         self.device, self.rank, self.nranks = device, rank, nranks
 
+    @classmethod
+    def multi(cls, devices):
+        """Single-process multi-device context (ccsc_create_multi): the learners then take
+        the WHOLE problem and run rank i on devices[i] in its own host thread -- the
+        drop-in path of one MATLAB call over a node's GPUs.  A repeated device ({0, 0})
+        exchanges through host memory (one-GPU testing); distinct devices use RCCL."""
+        self = cls.__new__(cls)
+        self._lib = L.lib()
+        eb = L.errbuf()
+        devs = (C.c_int32 * len(devices))(*devices)
+        self.ptr = self._lib.ccsc_create_multi(devs, len(devices), eb, len(eb))
+        if not self.ptr:
+            raise L.CCSCError(L.CCSC_E_HIP, eb.value.decode(errors="replace"))
+        self.device, self.rank, self.nranks = devices[0], 0, 1
+        self.devices = list(devices)
+        return self
+
+    @property
+    def group(self):
+        return len(getattr(self, "devices", ())) > 1
+
     def close(self):
         if self.ptr:
             self._lib.ccsc_destroy(self.ptr)
@@ -322,6 +343,8 @@ def _learn_2d(variant, b, kernel_size, lambda_residual, lambda_prior, max_it, to
         if init is not None and len(init) > 0:
             d0 = init.get("d")
             z0 = init.get("z")
+        if ctx.group:
+            return learn_once(ctx, p, b, d0, z0, want_z=want_z, want_DZ=want_DZ)
         s = Session(ctx, p, b, d0, z0)
         try:
             done = False
@@ -335,6 +358,41 @@ def _learn_2d(variant, b, kernel_size, lambda_residual, lambda_prior, max_it, to
         if own:
             ctx.close()
     return d_res, z_res, DZ, iterations
+
+
+def learn_once(ctx, p, b, d0=None, z0=None, want_z=True, want_DZ=True):
+    """One ccsc_learn call over the whole problem (the MEX path): on a multi-device
+    context the engine shards it over the devices.  2D learners; returns
+    (d_res, z_res, DZ, iterations) like the session path."""
+    p = resolve(p)
+    psf, K = p.psf, p.K
+    r = psf // 2
+    X, Y = p.sb[0] + 2 * r, p.sb[1] + 2 * r
+    b = np.asfortranarray(b, dtype=np.float64)
+    d0 = None if d0 is None else np.asfortranarray(d0, dtype=np.float64)
+    z0 = None if z0 is None else np.asfortranarray(z0, dtype=np.float64)
+    d_res = np.zeros((psf, psf, K), order="F")
+    z_res = np.zeros((X, Y, K, p.n), order="F") if want_z else None
+    DZ = np.zeros((X, Y, 1, p.n), order="F") if want_DZ else None
+    out = L.Outputs(L.dptr(d_res), L.dptr(z_res), L.dptr(DZ), L.dptr(None))
+    cap = p.max_it + 1
+    a = {k: np.full(cap, np.nan) for k in ("obj_vals_d", "obj_vals_z", "tim_vals")}
+    tr = {"d_diff": np.full(cap * p.max_it_d, np.nan), "z_diff": np.full(cap * p.max_it_z, np.nan)}
+    nd = np.zeros(cap, dtype=np.int32)
+    nz = np.zeros(cap, dtype=np.int32)
+    lg = L.IterLog(cap, 0, L.dptr(a["obj_vals_d"]), L.dptr(a["obj_vals_z"]),
+                   L.dptr(a["tim_vals"]), L.dptr(None), L.dptr(None), L.dptr(tr["d_diff"]),
+                   L.dptr(tr["z_diff"]), L.iptr(nd), L.iptr(nz), L.iptr(None))
+    eb = L.errbuf()
+    L.check(L.lib().ccsc_learn(ctx.ptr, C.byref(p), L.dptr(b), L.dptr(d0), L.dptr(z0),
+                               C.byref(out), C.byref(lg), L.CB(), None, eb, len(eb)), eb)
+    cnt = lg.count
+    it = {k: v[:cnt].copy() for k, v in a.items()}
+    nout = max(cnt - 1, 0)
+    it["trace"] = {"d_diff": tr["d_diff"][: nout * p.max_it_d].reshape(nout, p.max_it_d),
+                   "z_diff": tr["z_diff"][: nout * p.max_it_z].reshape(nout, p.max_it_z),
+                   "n_d": nd[:nout].copy(), "n_z": nz[:nout].copy()}
+    return d_res, z_res, DZ, it
 
 
 def admm_learn_conv2D_large_dParallel(b, kernel_size, lambda_residual, lambda_prior, max_it, tol,

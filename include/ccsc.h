@@ -23,13 +23,15 @@
  *    No C++ exception crosses the ABI.
  *  - Calls on one context come from one thread (MATLAB's / Python's).  The
  *    progress callback runs on that calling thread only.
- *  - Multi-GPU: one process per GPU.  Rank 0 calls ccsc_get_unique_id(); the
+ *  - Multi-GPU, one process per GPU (bench, MPI/torch jobs): rank 0 calls ccsc_get_unique_id(); the
  *    caller ships the 128 bytes to every rank (torch.distributed / MPI / file)
  *    and each rank calls ccsc_create(device, rank, nranks, uid).  Blocks of
  *    `ni` patches are sharded contiguously over ranks (ccsc_shard); the
  *    consensus mean of the reference (dP:114-121) becomes one RCCL all-reduce
  *    per d-iteration, the z-step's use of block 1's filters (dP:143) one RCCL
  *    broadcast per outer iteration.
+ *  - Multi-GPU, one process (the MATLAB drop-in): ccsc_create_multi(devices, ndev)
+ *    and one ccsc_learn call over the whole problem; same sharding and exchanges.
  */
 #ifndef CCSC_H_
 #define CCSC_H_
@@ -41,7 +43,7 @@
 extern "C" {
 #endif
 
-#define CCSC_ABI_VERSION 3
+#define CCSC_ABI_VERSION 4
 
 /* status codes */
 #define CCSC_OK 0
@@ -166,6 +168,16 @@ ccsc_ctx* ccsc_create(int32_t device, int32_t rank, int32_t nranks, const uint8_
 typedef int32_t (*ccsc_comm_fn)(void* user, int32_t op, double* buf, int64_t count);
 ccsc_ctx* ccsc_create_hostcomm(int32_t device, int32_t rank, int32_t nranks, ccsc_comm_fn fn,
                                void* user, char* err, size_t errlen);
+/* Single-process multi-device context: the drop-in path of one MATLAB call over a
+ * node's GPUs (learn_kernels_2D_large.m:28 calls the learner once).
+ * devices[0..ndev-1] become ranks 0..ndev-1 (one stream each, ncclCommInitAll over
+ * xGMI; a list that repeats a device, e.g. {0, 0} on a one-GPU host, exchanges
+ * through host memory instead).  ccsc_learn on this context takes the caller's
+ * WHOLE problem (b and z0 over all n patches, outputs for all n), shards the blocks
+ * with ccsc_shard, runs rank i in a host thread on devices[i] and calls back on the
+ * calling thread only.  Sessions and the 2-3D learner need a one-device context
+ * (CCSC_E_UNSUPPORTED here).  ndev == 1 is ccsc_create(devices[0], 0, 1, NULL). */
+ccsc_ctx* ccsc_create_multi(const int32_t* devices, int32_t ndev, char* err, size_t errlen);
 void ccsc_destroy(ccsc_ctx* ctx);
 
 /* ---- one-shot learner: the literal drop-in for the .m functions --------- */

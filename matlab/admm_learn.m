@@ -12,6 +12,10 @@ function [ d_res, z_res, Dz, obj_val ] = admm_learn(b, kernel_size, ...
     size_z = [sb(1:2) + 2 * r, kernel_size(4), sb(4)];
     if ~isempty(init) && isfield(init, 'd'), d0 = init.d; else, d0 = randn(kernel_size([1 2 4])); end
     if ~isempty(init) && isfield(init, 'z'), z0 = init.z; else, z0 = randn(size_z); end
-    [d_res, z_res, Dz, obj_val] = ccsc_mex(4, b, kernel_size, lambda_residual, ...
+    o = ccsc_call([1 3 4 5], nargout, 4, b, kernel_size, lambda_residual, ...
         lambda_prior, max_it, tol, verbose, d0, z0, ccsc_device(), smooth_init);
+    d_res = o{1};
+    if nargout > 1, z_res = o{3}; end
+    if nargout > 2, Dz = o{4}; end
+    if nargout > 3, obj_val = o{5}; end
 end

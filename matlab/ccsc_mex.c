@@ -6,9 +6,14 @@
  *
  * Called by the .m wrappers in this directory, which keep the reference
  * signatures (2D/admm_learn_conv2D_large_dParallel.m:1-4 etc.):
- *   [d_res, z_res, DZ, obj_val, iter] = ccsc_mex(variant, b, kernel_size,
- *        lambda_residual, lambda_prior, max_it, tol, verbose, d0, z0, device
+ *   [d_res, iter, z_res, DZ, obj_val] = ccsc_mex(variant, b, kernel_size,
+ *        lambda_residual, lambda_prior, max_it, tol, verbose, d0, z0, devices
  *        [, smooth_init])                      (smooth_init: 2-3D learner only)
+ * Outputs are ordered so that the wrappers pass their own nargout through:
+ * z_res / DZ / obj_val are only allocated and copied when asked for (z_res is
+ * ~97 GB at C2).  `devices` is a vector of GPU indices (ccsc_device.m): more
+ * than one runs the learner over those GPUs from this one call
+ * (ccsc_create_multi: one host thread per device, RCCL over xGMI).
  * Output shapes per variant (what the library writes, include/ccsc.h):
  *   dP / dZ  d_res [s,s,K]      z_res [X,Y,K,n]      DZ [X,Y,1,n]
  *   3D       d_res [s,s,s,K]    z_res [X,Y,T,K,n]    DZ [X,Y,T,n]
@@ -20,12 +25,33 @@
 
 #include <string.h>
 
+#define CCSC_MEX_MAXDEV 64
 static ccsc_ctx* g_ctx = NULL;
-static int g_dev = -1;
+static int32_t g_devs[CCSC_MEX_MAXDEV];
+static int g_ndev = 0;
 
 static void cleanup(void) {
   if (g_ctx) ccsc_destroy(g_ctx);
   g_ctx = NULL;
+  g_ndev = 0;
+}
+
+/* the cached context when it serves the same device list, else a new one */
+static ccsc_ctx* context_for(const mxArray* a, char* err, size_t errlen) {
+  const mwSize nd = mxGetNumberOfElements(a);
+  if (nd < 1 || nd > CCSC_MEX_MAXDEV)
+    mexErrMsgIdAndTxt("ccsc:devices", "devices must list 1..%d GPU indices", CCSC_MEX_MAXDEV);
+  int32_t devs[CCSC_MEX_MAXDEV];
+  const double* dv = mxGetDoubles(a);
+  for (mwSize i = 0; i < nd; ++i) devs[i] = (int32_t)dv[i];
+  if (g_ctx && g_ndev == (int)nd && !memcmp(g_devs, devs, nd * sizeof(int32_t))) return g_ctx;
+  cleanup();
+  g_ctx = ccsc_create_multi(devs, (int32_t)nd, err, errlen);
+  if (!g_ctx) mexErrMsgIdAndTxt("ccsc:hip", "%s", err);
+  memcpy(g_devs, devs, nd * sizeof(int32_t));
+  g_ndev = (int)nd;
+  mexAtExit(cleanup);
+  return g_ctx;
 }
 
 static void progress(void* user, int32_t it, double od, double oz, double t) {
@@ -82,14 +108,8 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     smooth = mxGetDoubles(prhs[11]);
   }
 
-  const int dev = (int)mxGetScalar(prhs[10]);
-  if (!g_ctx || g_dev != dev) {
-    cleanup();
-    g_ctx = ccsc_create(dev, 0, 1, NULL, err, sizeof err);
-    if (!g_ctx) mexErrMsgIdAndTxt("ccsc:hip", "%s", err);
-    g_dev = dev;
-    mexAtExit(cleanup);
-  }
+  if (!mxIsDouble(prhs[10])) mexErrMsgIdAndTxt("ccsc:devices", "devices must be double");
+  ccsc_ctx* ctx = context_for(prhs[10], err, sizeof err);
   const double* d0 = mxIsEmpty(prhs[8]) ? NULL : mxGetDoubles(prhs[8]);
   const double* z0 = mxIsEmpty(prhs[9]) ? NULL : mxGetDoubles(prhs[9]);
 
@@ -126,16 +146,16 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
   memset(&out, 0, sizeof out);
   plhs[0] = zeros_nd(ndd, dd);
   out.d_res = mxGetDoubles(plhs[0]);
-  if (nlhs > 1) {
-    plhs[1] = zeros_nd(nzd, zd);
-    out.z_res = mxGetDoubles(plhs[1]);
-  }
   if (nlhs > 2) {
-    plhs[2] = zeros_nd(nxd, xd);
-    out.DZ = mxGetDoubles(plhs[2]);
+    plhs[2] = zeros_nd(nzd, zd);
+    out.z_res = mxGetDoubles(plhs[2]);
+  }
+  if (nlhs > 3) {
+    plhs[3] = zeros_nd(nxd, xd);
+    out.DZ = mxGetDoubles(plhs[3]);
   }
   double obj = 0;
-  if (nlhs > 3) out.obj_val = &obj;
+  if (nlhs > 4) out.obj_val = &obj;
 
   const int cap = p.max_it + 1;
   mxArray* od = mxCreateDoubleMatrix(1, cap, mxREAL);
@@ -150,21 +170,21 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
 
   ccsc_cb cb = p.verbose == CCSC_VERBOSE_NONE ? NULL : progress;
   const int rc = variant == CCSC_HS23
-                     ? ccsc_learn_hs23(g_ctx, &p, mxGetDoubles(b), smooth, d0, z0, &out, &lg, cb,
+                     ? ccsc_learn_hs23(ctx, &p, mxGetDoubles(b), smooth, d0, z0, &out, &lg, cb,
                                        NULL, err, sizeof err)
-                     : ccsc_learn(g_ctx, &p, mxGetDoubles(b), d0, z0, &out, &lg, cb, NULL, err,
+                     : ccsc_learn(ctx, &p, mxGetDoubles(b), d0, z0, &out, &lg, cb, NULL, err,
                                   sizeof err);
   if (rc) mexErrMsgIdAndTxt("ccsc:learn", "%s (code %d)", err, rc);
   mxSetN(od, lg.count);
   mxSetN(oz, lg.count);
   mxSetN(tv, lg.count);
-  if (nlhs > 3) plhs[3] = mxCreateDoubleScalar(obj);
-  if (nlhs > 4) {
+  if (nlhs > 4) plhs[4] = mxCreateDoubleScalar(obj);
+  if (nlhs > 1) {
     const char* f[] = {"obj_vals_d", "obj_vals_z", "tim_vals"};
-    plhs[4] = mxCreateStructMatrix(1, 1, 3, f);
-    mxSetField(plhs[4], 0, "obj_vals_d", od);
-    mxSetField(plhs[4], 0, "obj_vals_z", oz);
-    mxSetField(plhs[4], 0, "tim_vals", tv);
+    plhs[1] = mxCreateStructMatrix(1, 1, 3, f);
+    mxSetField(plhs[1], 0, "obj_vals_d", od);
+    mxSetField(plhs[1], 0, "obj_vals_z", oz);
+    mxSetField(plhs[1], 0, "tim_vals", tv);
   } else {
     mxDestroyArray(od);
     mxDestroyArray(oz);

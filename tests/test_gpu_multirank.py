@@ -88,3 +88,46 @@ def test_two_ranks_equal_one_rank(tmp_path, gpu_ctx, variant, tol):
     np.testing.assert_allclose(DZ, DZ_o, rtol=0, atol=1e-9 * np.abs(DZ_o).max())
     if tol > 0:
         np.testing.assert_allclose(parts[0]["zd"], np.array(tr_o["z_diff"]), rtol=1e-6)
+
+
+@pytest.mark.parametrize("variant,tol,nblk", [("dz", 0.0, 3), ("dp", 0.0, 2), ("dz", 1e-12, 2)])
+def test_multi_device_context_equals_one_device(gpu_ctx, variant, tol, nblk):
+    """ccsc_create_multi({0, 0}) + one ccsc_learn over the whole problem (the MEX path of
+    one MATLAB call over several GPUs; a repeated device exchanges through host memory,
+    distinct devices through RCCL) gives the one-device result: blocks sharded by
+    ccsc_shard, outputs written back at each rank's patch offset, iterlog from rank 0."""
+    from ccsc_code_iccv2017_amd import learners as E
+    rng = np.random.default_rng(31)
+    ni, K, psf = 2, 3, 5
+    n = ni * nblk
+    b = rng.standard_normal((12, 11, n))
+    d0 = rng.standard_normal((psf, psf, K))
+    z0 = rng.standard_normal((16, 15, K, ni if variant == "dz" else n))
+    fn = (E.admm_learn_conv2D_large_dzParallel if variant == "dz"
+          else E.admm_learn_conv2D_large_dParallel)
+    args = (b, [psf, psf, K], 1.0, 1.0, 2, tol, "brief", {"d": d0, "z": z0})
+    d1, z1, DZ1, it1 = fn(*args, ni=ni, ctx=gpu_ctx)
+    mctx = E.Context.multi([0, 0])
+    try:
+        d2, z2, DZ2, it2 = fn(*args, ni=ni, ctx=mctx)
+    finally:
+        mctx.close()
+    np.testing.assert_allclose(d2, d1, rtol=0, atol=1e-10 * np.abs(d1).max())
+    np.testing.assert_allclose(z2, z1, rtol=0, atol=1e-10 * np.abs(z1).max())
+    np.testing.assert_allclose(DZ2, DZ1, rtol=0, atol=1e-10 * np.abs(DZ1).max())
+    np.testing.assert_allclose(it2["obj_vals_z"], it1["obj_vals_z"], rtol=1e-10)
+    if tol > 0:
+        np.testing.assert_array_equal(it2["trace"]["n_z"], it1["trace"]["n_z"])
+
+
+def test_multi_device_context_rejects_sessions(gpu_ctx):
+    from ccsc_code_iccv2017_amd import _lib as L
+    from ccsc_code_iccv2017_amd import learners as E
+    mctx = E.Context.multi([0, 0])
+    try:
+        p = E.make_problem(L.CCSC_DZPAR, (12, 11, 4), [5, 5, 3], 1.0, 1.0, 1, 0.0, "none", ni=2)
+        with pytest.raises(L.CCSCError) as ei:
+            E.Session(mctx, p, np.zeros((12, 11, 4)))
+        assert ei.value.code == L.CCSC_E_UNSUPPORTED
+    finally:
+        mctx.close()

@@ -1,0 +1,113 @@
+"""The MEX gateway (matlab/ccsc_mex.c), the literal drop-in of the .m learners.
+
+No MATLAB exists here, so tests/mex_stub/ holds a TEST-ONLY mex.h with MATLAB's
+signatures and a minimal mxArray runtime.  CPU: the gateway compiles with
+-Wall -Wextra -Werror against it.  GPU: mexFunction runs exactly as MATLAB would
+call it (the .m wrappers' argument list) and must give the engine's result, with
+one device and with the device list [0, 0] (ccsc_create_multi: the one-call
+multi-GPU path), and must allocate only the outputs nargout asks for."""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+STUB = os.path.join(ROOT, "tests", "mex_stub")
+HARNESS = os.path.join(STUB, "_build", "libccsc_mexharness.so")
+
+
+def test_gateway_compiles_warning_free():
+    r = subprocess.run(["gcc", "-std=c11", "-Wall", "-Wextra", "-Werror", "-Wno-unused-parameter",
+                        "-fsyntax-only", "-I", STUB, "-I", os.path.join(ROOT, "include"),
+                        os.path.join(ROOT, "matlab", "ccsc_mex.c")], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+
+
+def _harness():
+    from ccsc_code_iccv2017_amd import _lib as L
+    L.lib()                       # libccsc first (one HIP runtime per process, _lib.lib)
+    if not os.path.exists(HARNESS):
+        pytest.fail(f"{HARNESS} missing: run tests/mex_stub/build.sh")
+    h = C.CDLL(HARNESS)
+    P = C.c_void_p
+    h.hx_double.restype = P
+    h.hx_double.argtypes = [C.POINTER(C.c_double), C.c_int, C.POINTER(C.c_int64)]
+    h.hx_string.restype = P
+    h.hx_string.argtypes = [C.c_char_p]
+    h.hx_ndims.argtypes = [P]
+    h.hx_dim.restype = C.c_int64
+    h.hx_dim.argtypes = [P, C.c_int]
+    h.hx_data.restype = C.POINTER(C.c_double)
+    h.hx_data.argtypes = [P]
+    h.hx_field.restype = P
+    h.hx_field.argtypes = [P, C.c_char_p]
+    h.hx_free.argtypes = [P]
+    h.hx_call.argtypes = [C.c_int, C.POINTER(P), C.c_int, C.POINTER(P), C.c_char_p, C.c_size_t]
+    return h
+
+
+def _mx(h, a):
+    a = np.asfortranarray(np.atleast_1d(np.asarray(a, dtype=np.float64)))
+    dims = (C.c_int64 * a.ndim)(*a.shape)
+    return h.hx_double(a.ctypes.data_as(C.POINTER(C.c_double)), a.ndim, dims)
+
+
+def _np(h, m):
+    nd = h.hx_ndims(m)
+    shape = tuple(h.hx_dim(m, i) for i in range(nd))
+    n = int(np.prod(shape))
+    return np.ctypeslib.as_array(h.hx_data(m), shape=(n,)).reshape(shape, order="F").copy()
+
+
+def _call(h, nlhs, args):
+    prhs = (C.c_void_p * len(args))(*args)
+    plhs = (C.c_void_p * max(nlhs, 1))()
+    err = C.create_string_buffer(2048)
+    rc = h.hx_call(nlhs, plhs, len(args), prhs, err, len(err))
+    return rc, err.value.decode(), [plhs[i] for i in range(nlhs)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("devices", [[0], [0, 0]])
+def test_mexfunction_matches_engine(gpu_ctx, devices):
+    from ccsc_code_iccv2017_amd import learners as E
+    h = _harness()
+    rng = np.random.default_rng(41)
+    # the dzParallel wrapper's call carries no ni: the variant default (100, dZ:11) holds
+    K, psf, ni, n = 3, 5, 100, 200
+    b = rng.standard_normal((12, 11, n))
+    d0 = rng.standard_normal((psf, psf, K))
+    z0 = rng.standard_normal((16, 15, K, ni))
+    d_e, z_e, DZ_e, it_e = E.admm_learn_conv2D_large_dzParallel(
+        b, [psf, psf, K], 1.0, 1.0, 2, 0.0, "brief", {"d": d0, "z": z0}, ctx=gpu_ctx)
+    args = [_mx(h, 1), _mx(h, b), _mx(h, [psf, psf, K]), _mx(h, 1.0), _mx(h, 1.0), _mx(h, 2),
+            _mx(h, 0.0), h.hx_string(b"brief"), _mx(h, d0), _mx(h, z0), _mx(h, devices)]
+    try:
+        rc, err, out = _call(h, 4, args)          # [d_res, iterations, z_res, DZ]
+        assert rc == 0, err
+        d_m, z_m, DZ_m = _np(h, out[0]), _np(h, out[2]), _np(h, out[3])
+        oz = _np(h, h.hx_field(out[1], b"obj_vals_z")).ravel()
+        for m in out:
+            h.hx_free(m)
+        np.testing.assert_allclose(d_m, d_e, rtol=0, atol=1e-10 * np.abs(d_e).max())
+        np.testing.assert_allclose(z_m, z_e, rtol=0, atol=1e-10 * np.abs(z_e).max())
+        np.testing.assert_allclose(DZ_m.reshape(DZ_e.shape), DZ_e, rtol=0,
+                                   atol=1e-10 * np.abs(DZ_e).max())
+        np.testing.assert_allclose(oz, it_e["obj_vals_z"], rtol=1e-10)
+        # nargout = 1: only d_res is produced (z_res is ~97 GB at C2)
+        rc, err, out = _call(h, 1, args)
+        assert rc == 0, err
+        np.testing.assert_allclose(_np(h, out[0]), d_e, rtol=0, atol=1e-10 * np.abs(d_e).max())
+        h.hx_free(out[0])
+        # shape errors surface as MATLAB errors, not crashes (n % ni != 0, Q13)
+        bad = list(args)
+        bad[1] = _mx(h, b[:, :, :150])
+        rc, err, _ = _call(h, 1, bad)
+        assert rc == 1 and "ccsc:" in err
+        h.hx_free(bad[1])
+    finally:
+        for a in args:
+            h.hx_free(a)
+        h.hx_exit()
