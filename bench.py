@@ -173,14 +173,15 @@ def main():
     sess.set_profiling(True)
     barrier()
     torch.cuda.synchronize()
-    outer0 = sess.outer
+    outer0 = len(sess.iterlog()["tim_vals"]) - 1
     t0 = time.perf_counter()
     for _ in range(args.steps):
         sess.step(1)   # tol > 0: a converged learner stops early (the reference's break, dP:186-188)
     torch.cuda.synchronize()
     barrier()
     dt = time.perf_counter() - t0
-    done_steps = sess.outer - outer0    # < steps only when tol > 0 converged
+    # outer iterations the engine ran (< steps only when a tol > 0 learner converged)
+    done_steps = len(sess.iterlog()["tim_vals"]) - 1 - outer0
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -128,6 +128,6 @@ def test_multi_device_context_rejects_sessions(gpu_ctx):
         p = E.make_problem(L.CCSC_DZPAR, (12, 11, 4), [5, 5, 3], 1.0, 1.0, 1, 0.0, "none", ni=2)
         with pytest.raises(L.CCSCError) as ei:
             E.Session(mctx, p, np.zeros((12, 11, 4)))
-        assert ei.value.code == L.CCSC_E_UNSUPPORTED
+        assert "one-device context" in str(ei.value)
     finally:
         mctx.close()
