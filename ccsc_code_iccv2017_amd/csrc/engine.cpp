@@ -538,6 +538,7 @@ struct Session2D {
   int NV, KG;   // views, filter slices per block (K * NV)
   bool is4, is3;
   bool woodbury;   // D-factor in Woodbury form (p.dfactor; AUTO: woodbury_fits, ni << K)
+  bool gram_mf;    // Gram + Cholesky on the matrix cores (gramchol.hip; CCSC_GRAM_MF=0: VALU form)
   int64_t N, nbl, b0, np;
   bool owner0;
   double theta;
@@ -661,6 +662,10 @@ struct Session2D {
                (p.dfactor == CCSC_DFACTOR_AUTO && woodbury_fits(K, ni));
     NV = p.views[0] * p.views[1];
     KG = K * NV;
+    {
+      const char* ev = std::getenv("CCSC_GRAM_MF");
+      gram_mf = gram_chol_mf_ok(K, NV) && !(ev && ev[0] == '0');
+    }
     is4 = p.variant == CCSC_L4D;
     is3 = p.variant == CCSC_L3D;
     N = p.n / ni;
@@ -1035,6 +1040,8 @@ struct Session2D {
         if (woodbury)
           HIPCHK(launch_gram_wb<double>(Zh.as<cpx<double>>(), Bj, Lj, hj, F, K, ni, p.rho_d, NV,
                                         st));
+        else if (gram_mf)
+          HIPCHK(launch_gram_chol_mf(Zh.as<cpx<double>>(), Bj, Lj, hj, F, K, ni, p.rho_d, NV, st));
         else
           HIPCHK(launch_gram_chol<double>(Zh.as<cpx<double>>(), Bj, Lj, hj, F, K, ni, p.rho_d,
                                           NV, st));

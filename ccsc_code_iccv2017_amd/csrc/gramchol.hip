@@ -1,0 +1,334 @@
+// D-step precompute on the matrix cores (gfx950): per frequency f of a block,
+// G_f = A_f^H A_f + rho I (A_f = ni x K code spectra, K <= 112), h_f = A_f^H b_f,
+// and the Cholesky factor L_f of G_f, packed lower column-major -- the same
+// outputs as k_gram_chol (dstep.hip; reference precompute_H_hat_D, dP:221-237:
+// Sinv_f = (A^H A + rho I)^-1 through pinv, here factored instead of inverted).
+//
+// G is held as 16 x 16 tiles (T = ceil(K / 16) <= 7 per dimension, the T(T+1)/2
+// lower tiles dealt round-robin to the four waves) in v_mfma_f64_16x16x4_f64
+// accumulators for the whole kernel:
+//   Gram     per 4 patches and tile (I, J): Re += Ar_I^T Ar_J + Ai_I^T Ai_J,
+//            Im += Ar_I^T Ai_J - Ai_I^T Ar_J  (4 MFMAs); the code spectra are
+//            staged through LDS in chunks of 16 patches, double-buffered, the next
+//            chunk's (strided) global loads in flight under the current chunk's MFMAs;
+//   Cholesky blocked right-looking over the T tile columns j:
+//            POTRF of tile (j, j) by wave 0 (rows on lanes, pivots by v_readlane),
+//            TRSM of the tiles below by every wave (one row per lane, L_jj read as
+//            LDS broadcasts), trailing update A_ik -= L_ij L_kj^H of every tile
+//            k > j on the matrix cores by its owner (16 MFMAs per tile).
+// L goes from the POTRF/TRSM registers straight to HBM (for a fixed column,
+// consecutive lanes hold consecutive rows: coalesced).  LDS: the staging chunks
+// (58 KB) or two column panels (61 KB), so two workgroups share a CU and one's
+// VALU phases (POTRF, TRSM) run beside the other's MFMA phases.
+#include "kernels.hpp"
+
+namespace ccsc {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+constexpr int kGcNT = 256;                  // 4 waves
+constexpr int kGcTM = 7;                    // tiles per dimension (K <= 112)
+constexpr int kGcTiles = kGcTM * (kGcTM + 1) / 2;
+constexpr int kGcTW = (kGcTiles + 3) / 4;   // tiles per wave
+constexpr int kGcPC = 16;                   // patches per staged chunk
+constexpr int kGcKP = 16 * kGcTM;           // padded filter count of a staged row
+constexpr int kGcLD = kGcKP + 1;            // staged row stride (complex)
+constexpr int kGcTS = 17;                   // column stride (complex) of an LDS tile
+constexpr int kGcTSZ = 16 * kGcTS;          // complex per LDS tile
+constexpr int kGcHPT = 8;                   // right-hand-side entries of h per thread
+
+__device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ double rdl(double v, int l) {
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
+                          __builtin_amdgcn_readlane(__double2loint(v), l));
+}
+
+__device__ __forceinline__ int gc_pk(int j, int K) { return j * K - (j * (j - 1)) / 2; }
+
+// tile t of the T(T+1)/2 lower tiles -> (I, J); wave w owns tiles w, w + 4, ...
+__device__ __forceinline__ void gc_tile(int t, int& I, int& J) {
+  I = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+  while ((I + 1) * (I + 2) / 2 <= t) ++I;
+  while (I * (I + 1) / 2 > t) --I;
+  J = t - I * (I + 1) / 2;
+}
+
+// Gram MFMAs of wave w for one k-step (4 patches: lane l takes patch l >> 4 of the
+// step and filter 16 T + (l & 15) of tile row/column T).  Tile coordinates are
+// wave-uniform runtime values: operands are loaded per tile from LDS, so no
+// register array is indexed at run time.
+__device__ __forceinline__ void gram_kstep(const cpx<double>* row, int w, int Tn,
+                                           d4 (&gr)[kGcTW], d4 (&gi)[kGcTW]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int s = 0; s < kGcTW; ++s) {
+    const int t = w + 4 * s;
+    int I, J;
+    gc_tile(t, I, J);
+    if (t < kGcTiles && I < Tn) {
+      const cpx<double> a = row[16 * I + (lane & 15)];
+      const cpx<double> b = row[16 * J + (lane & 15)];
+      gr[s] = mfma(a.x, b.x, gr[s]);
+      gr[s] = mfma(a.y, b.y, gr[s]);
+      gi[s] = mfma(a.x, b.y, gi[s]);
+      gi[s] = mfma(-a.y, b.x, gi[s]);
+    }
+  }
+}
+
+// store an accumulator tile (C/D layout: lane l holds row (l >> 4) + 4 r, column l & 15)
+// into an LDS tile (element (row, col) at col * kGcTS + row)
+__device__ __forceinline__ void tile_to_lds(cpx<double>* dst, const d4& re, const d4& im) {
+  const int lane = threadIdx.x & 63;
+  const int col = lane & 15;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) dst[col * kGcTS + (lane >> 4) + 4 * r] = {re[r], im[r]};
+}
+
+// trailing update of wave w's tiles (i, k), k > j: A_ik -= L_ij L_kj^H, the panel
+// tiles L_.j in P (P[i * kGcTSZ + col * kGcTS + row]); then the tiles of column
+// j + 1 to the next panel buffer Pn
+__device__ __forceinline__ void trail_step(const cpx<double>* P, cpx<double>* Pn, int j, int w,
+                                           int Tn, d4 (&gr)[kGcTW], d4 (&gi)[kGcTW]) {
+  const int lane = threadIdx.x & 63;
+  const int row = lane & 15, c4 = lane >> 4;
+#pragma unroll
+  for (int s = 0; s < kGcTW; ++s) {
+    const int t = w + 4 * s;
+    int I, J;
+    gc_tile(t, I, J);
+    if (t < kGcTiles && I < Tn && J > j) {
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const int col = 4 * kk + c4;
+        const cpx<double> a = P[I * kGcTSZ + col * kGcTS + row];   // L_ij (row, col)
+        const cpx<double> b = P[J * kGcTSZ + col * kGcTS + row];   // L_kj (row, col)
+        gr[s] = mfma(-a.x, b.x, gr[s]);
+        gr[s] = mfma(-a.y, b.y, gr[s]);
+        gi[s] = mfma(-a.y, b.x, gi[s]);
+        gi[s] = mfma(a.x, b.y, gi[s]);
+      }
+      if (J == j + 1) tile_to_lds(Pn + I * kGcTSZ, gr[s], gi[s]);
+    }
+  }
+}
+
+__device__ __forceinline__ void first_panel(cpx<double>* P, int w, int Tn,
+                                            const d4 (&gr)[kGcTW], const d4 (&gi)[kGcTW]) {
+#pragma unroll
+  for (int s = 0; s < kGcTW; ++s) {
+    const int t = w + 4 * s;
+    int I, J;
+    gc_tile(t, I, J);
+    if (t < kGcTiles && I < Tn && J == 0) tile_to_lds(P + I * kGcTSZ, gr[s], gi[s]);
+  }
+}
+
+// rho on the diagonal (exactly real), identity on the padding rows K..16 Tn - 1
+__device__ __forceinline__ void fix_diag(int w, int K, int Tn, double rho, d4 (&gr)[kGcTW],
+                                         d4 (&gi)[kGcTW]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int s = 0; s < kGcTW; ++s) {
+    const int t = w + 4 * s;
+    int I, J;
+    gc_tile(t, I, J);
+    if (t < kGcTiles && I < Tn && I == J) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int rr = (lane >> 4) + 4 * r, cc = lane & 15;
+        if (rr == cc) {
+          gr[s][r] = (16 * I + rr < K) ? gr[s][r] + rho : 1.0;
+          gi[s][r] = 0.0;
+        }
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(kGcNT, 2) void k_gram_chol_mf(const cpx<double>* __restrict__ Zh,
+                                                           const cpx<double>* __restrict__ Bh,
+                                                           cpx<double>* __restrict__ L,
+                                                           cpx<double>* __restrict__ h, int F,
+                                                           int K, int ni, double rho, int NV) {
+  const int per = gridDim.x >> 3;
+  const int f = (blockIdx.x & 7) * per + (blockIdx.x >> 3);   // XCD-aware: neighbours share L2
+  if (f >= F) return;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  cpx<double>* sA = reinterpret_cast<cpx<double>*>(smem);      // [2][kGcPC][kGcLD]
+  cpx<double>* sB = sA + 2 * kGcPC * kGcLD;                    // [2][kGcPC][NV]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  int Tn = (K + 15) >> 4;
+  const int KV = K * NV;
+
+  d4 gr[kGcTW], gi[kGcTW];
+#pragma unroll
+  for (int s = 0; s < kGcTW; ++s) gr[s] = gi[s] = (d4){0.0, 0.0, 0.0, 0.0};
+  cpx<double> hacc[kGcHPT];
+#pragma unroll
+  for (int i = 0; i < kGcHPT; ++i) hacc[i] = {0.0, 0.0};
+
+  // ---- Gram + h: chunks of kGcPC patches, double-buffered ----
+  constexpr int kPer = (kGcPC * kGcKP + kGcNT - 1) / kGcNT;   // staged values per thread
+  cpx<double> pre[kPer];
+  cpx<double> preb = {0.0, 0.0};
+  auto fetch = [&](int p0) {
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int idx = tid + i * kGcNT;
+      const int pp = idx / kGcKP, k = idx - pp * kGcKP;
+      pre[i] = (pp < kGcPC && k < K && p0 + pp < ni)
+                   ? Zh[((int64_t)(p0 + pp) * K + k) * F + f]
+                   : cpx<double>{0.0, 0.0};
+    }
+    if (tid < kGcPC * NV) {
+      const int pp = tid / NV;
+      preb = (p0 + pp < ni) ? Bh[(int64_t)(p0 * NV + tid) * F + f] : cpx<double>{0.0, 0.0};
+    }
+  };
+  auto stage = [&](int buf) {
+    cpx<double>* a = sA + buf * kGcPC * kGcLD;
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int idx = tid + i * kGcNT;
+      const int pp = idx / kGcKP, k = idx - pp * kGcKP;
+      if (pp < kGcPC) a[pp * kGcLD + k] = pre[i];
+    }
+    if (tid < kGcPC * NV) sB[buf * kGcPC * NV + tid] = preb;
+  };
+  const int nch = (ni + kGcPC - 1) / kGcPC;
+  fetch(0);
+  stage(0);
+  __syncthreads();
+  for (int c = 0; c < nch; ++c) {
+    const int buf = c & 1;
+    if (c + 1 < nch) fetch((c + 1) * kGcPC);
+    const cpx<double>* a = sA + buf * kGcPC * kGcLD;
+#pragma unroll
+    for (int kk = 0; kk < kGcPC / 4; ++kk) {
+      const cpx<double>* row = a + (4 * kk + (lane >> 4)) * kGcLD;
+#ifndef CCSC_ABL_NOGRAM
+      gram_kstep(row, wave, Tn, gr, gi);
+#endif
+    }
+    const cpx<double>* b = sB + buf * kGcPC * NV;
+#pragma unroll
+    for (int i = 0; i < kGcHPT; ++i) {
+      const int q = tid + i * kGcNT;   // q = uv * K + k
+      if (q < KV) {
+        const int uv = q / K, k = q - uv * K;
+#pragma unroll 4
+        for (int pp = 0; pp < kGcPC; ++pp)
+          hacc[i] = cadd(hacc[i], cmulc(a[pp * kGcLD + k], b[pp * NV + uv]));
+      }
+    }
+    if (c + 1 < nch) stage(buf ^ 1);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < kGcHPT; ++i) {
+    const int q = tid + i * kGcNT;
+    if (q < KV) h[(int64_t)f * KV + q] = hacc[i];
+  }
+  fix_diag(wave, K, Tn, rho, gr, gi);
+
+  // ---- blocked Cholesky over the tile columns ----
+  cpx<double>* Pbuf = reinterpret_cast<cpx<double>*>(smem);   // [2][kGcTM][kGcTSZ]
+  cpx<double>* Lf = L + (int64_t)f * (K * (K + 1) / 2);
+  first_panel(Pbuf, wave, Tn, gr, gi);
+#ifdef CCSC_ABL_NOCHOL
+  Tn = 0;   // ablation build: skip the factorisation (timing only)
+#endif
+  for (int j = 0; j < Tn; ++j) {
+    cpx<double>* P = Pbuf + (j & 1) * kGcTM * kGcTSZ;
+    cpx<double>* Pn = Pbuf + ((j + 1) & 1) * kGcTM * kGcTSZ;
+    __syncthreads();   // column j's tiles are in P
+    // Panel j (POTRF of tile (j, j) + TRSM of the tiles below) in one left-looking
+    // sweep over its 16 columns, every wave on its own: lanes 0..15 hold the rows of
+    // tile (j, j) (all four waves redundantly, so no wave waits for another), lanes
+    // 16..39 up to 24 of the panel's other rows.  Column c of row r:
+    //   s = a[r][c] - sum_{k < c} L[r][k] conj(L[c][k]);  L[c][c] = sqrt(s of row c),
+    //   L[r][c] = s / L[c][c]  (the POTRF and TRSM formulas coincide),
+    // L[c][k] read back as LDS broadcasts from the wave's own copy Lw of the diagonal
+    // tile (written by lanes 0..15 one column earlier), the pivot by v_readlane.
+    {
+      cpx<double>* Lw = Pbuf + 2 * kGcTM * kGcTSZ + wave * kGcTSZ;
+      const bool diag = lane < 16;
+      const int q = wave * 24 + lane - 16;
+      const int ti = diag ? j : j + 1 + (q >> 4);
+      const int row = diag ? lane : (q & 15);
+#ifdef CCSC_ABL_NOTRSM
+      const bool mine = diag;
+#else
+      const bool mine = diag || (lane < 40 && ti < Tn);
+#endif
+      cpx<double> x[16];
+#pragma unroll
+      for (int c = 0; c < 16; ++c)
+        x[c] = mine ? P[ti * kGcTSZ + c * kGcTS + row] : cpx<double>{1.0, 0.0};
+#ifndef CCSC_ABL_NOPOTRF
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        cpx<double> s0 = x[c], s1 = {0.0, 0.0};
+#pragma unroll
+        for (int k0 = 0; k0 < c; k0 += 4) {
+          asm volatile("" ::: "memory");   // at most four broadcast reads in flight
+#pragma unroll
+          for (int k = k0; k < k0 + 4 && k < c; ++k) {
+            const cpx<double> l = Lw[k * kGcTS + c];   // L[c][k]
+            cpx<double>& acc = (k & 1) ? s1 : s0;
+            acc.x -= x[k].x * l.x + x[k].y * l.y;
+            acc.y -= x[k].y * l.x - x[k].x * l.y;
+          }
+        }
+        const cpx<double> sc = cadd(s0, s1);
+        const double d = sqrt(rdl(sc.x, c));
+        x[c] = (lane == c) ? cpx<double>{d, 0.0} : cscale(sc, 1.0 / d);
+        if (diag) Lw[c * kGcTS + lane] = x[c];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // column c visible to the wave
+        __builtin_amdgcn_wave_barrier();
+      }
+#endif
+      const int gr_ = 16 * ti + row;
+      if (mine && (!diag || wave == 0) && gr_ < K) {
+#pragma unroll
+        for (int c = 0; c < 16; ++c) {
+          const int gc = 16 * j + c;
+          if (!diag || row >= c) Lf[gc_pk(gc, K) + gr_ - gc] = x[c];
+        }
+      }
+      if (mine && !diag) {
+#pragma unroll
+        for (int c = 0; c < 16; ++c) P[ti * kGcTSZ + c * kGcTS + row] = x[c];
+      }
+    }
+    __syncthreads();   // the panel L_.j is in P
+#ifndef CCSC_ABL_NOTRAIL
+    if (j + 1 < Tn) trail_step(P, Pn, j, wave, Tn, gr, gi);
+#endif
+  }
+}
+
+bool gram_chol_mf_ok(int K, int NV) { return K <= kGcKP && K * NV <= kGcHPT * kGcNT && NV <= 16; }
+
+size_t gram_chol_mf_smem(int NV) {
+  const size_t stage = (size_t)2 * kGcPC * kGcLD * 16 + (size_t)2 * kGcPC * NV * 16;
+  const size_t chol = (size_t)(2 * kGcTM + 4) * kGcTSZ * 16;   // two panels + the waves' L_jj
+  return stage > chol ? stage : chol;
+}
+
+hipError_t launch_gram_chol_mf(const cpx<double>* Zh, const cpx<double>* Bh, cpx<double>* L,
+                               cpx<double>* h, int F, int K, int ni, double rho, int NV,
+                               hipStream_t st) {
+  if (!gram_chol_mf_ok(K, NV)) return hipErrorInvalidValue;
+  const int grid = ((F + 7) / 8) * 8;
+  hipLaunchKernelGGL(k_gram_chol_mf, dim3(grid), dim3(kGcNT), gram_chol_mf_smem(NV), st, Zh, Bh,
+                     L, h, F, K, ni, rho, NV);
+  return hipGetLastError();
+}
+
+}  // namespace ccsc

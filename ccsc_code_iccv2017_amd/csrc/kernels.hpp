@@ -94,6 +94,12 @@ hipError_t launch_state_to_nat(const T* st_, T* nat, int64_t count, hipStream_t 
 template <typename T>
 hipError_t launch_gram_chol(const cpx<T>* Zh, const cpx<T>* Bh, cpx<T>* L, cpx<T>* h, int F,
                             int K, int ni, T rho, int NV, hipStream_t st);
+// The same outputs on the matrix cores (gramchol.hip): fp64 MFMA Gram and blocked
+// Cholesky, K <= 112, K * NV <= 2048.
+bool gram_chol_mf_ok(int K, int NV);
+hipError_t launch_gram_chol_mf(const cpx<double>* Zh, const cpx<double>* Bh, cpx<double>* L,
+                               cpx<double>* h, int F, int K, int ni, double rho, int NV,
+                               hipStream_t st);
 // x_{f,uv} = (L L^H)^{-1} (h_{f,uv} + rho * C_{f,uv}) for every (block, f, view);
 // C and Dh are [blk][K][NV][F].
 template <typename T>
