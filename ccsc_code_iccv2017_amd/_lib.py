@@ -20,7 +20,7 @@ CCSC_E_UNSUPPORTED = -5
 CCSC_E_STATE = -6
 
 CCSC_DPAR, CCSC_DZPAR, CCSC_L3D, CCSC_L4D, CCSC_HS23 = 0, 1, 2, 3, 4
-ABI_VERSION = 4
+ABI_VERSION = 5
 VERBOSE = {"none": 0, "brief": 1, "all": 2}
 CCSC_FP64, CCSC_FP32 = 0, 1
 DFACTOR = {"auto": 0, "cholesky": 1, "woodbury": 2}
@@ -78,6 +78,41 @@ class IterLog(C.Structure):
     ]
 
 
+# reconstruction solvers (ccsc_solve)
+CCSC_SOLVE_INPAINT2D, CCSC_SOLVE_POISSON2D, CCSC_SOLVE_MULTICH, CCSC_SOLVE_VIDEO3D = 0, 1, 2, 3
+
+
+class SolveProblem(C.Structure):
+    _fields_ = [
+        ("variant", C.c_int32),
+        ("sb", C.c_int64 * 3),
+        ("nch", C.c_int32),
+        ("n", C.c_int64),
+        ("K", C.c_int32),
+        ("ksize", C.c_int32 * 3),
+        ("psf_size", C.c_int32 * 3),
+        ("lambda_residual", C.c_double),
+        ("lambda_prior", C.c_double),
+        ("max_it", C.c_int32),
+        ("tol", C.c_double),
+        ("verbose", C.c_int32),
+    ]
+
+
+class SolveInputs(C.Structure):
+    _fields_ = [("b", _dp), ("kernels", _dp), ("mask", _dp), ("smooth_init", _dp), ("psf", _dp),
+                ("x_orig", _dp)]
+
+
+class SolveOutputs(C.Structure):
+    _fields_ = [("z", _dp), ("res", _dp)]
+
+
+class SolveLog(C.Structure):
+    _fields_ = [("capacity", C.c_int32), ("iters", _ip), ("obj", _dp), ("psnr", _dp),
+                ("diff", _dp), ("seconds", _dp)]
+
+
 CB = C.CFUNCTYPE(None, C.c_void_p, C.c_int32, C.c_double, C.c_double, C.c_double)
 COMM_FN = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.c_int32, C.POINTER(C.c_double), C.c_int64)
 
@@ -119,6 +154,10 @@ SIGNATURES = {
     "ccsc_session_kernel_stats": (C.c_int32, [C.c_void_p, C.c_int32, C.POINTER(C.c_int64),
                                               _dp, _dp, C.c_char_p, C.c_size_t]),
     "ccsc_session_destroy": (None, [C.c_void_p]),
+    "ccsc_solve_supported": (C.c_int32, [C.POINTER(SolveProblem), C.c_char_p, C.c_size_t]),
+    "ccsc_solve": (C.c_int32, [C.c_void_p, C.POINTER(SolveProblem), C.POINTER(SolveInputs),
+                               C.POINTER(SolveOutputs), C.POINTER(SolveLog), C.c_char_p,
+                               C.c_size_t]),
     "ccsc_test_fft2d": (C.c_int32, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, _dp, _dp, _dp,
                                     C.c_char_p, C.c_size_t]),
 }

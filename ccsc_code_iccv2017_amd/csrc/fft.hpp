@@ -186,12 +186,13 @@ struct LineGeom {
   int imoff;    // offset of the imaginary part from the real part
 };
 
-constexpr int kMaxPass = 3;
+constexpr int kMaxPass = 3;    // pass slots of the slice kernels' fft_dir
+constexpr int kPlanSlots = 4;  // plan capacity (the global line kernels of recon.hip use 4)
 struct Plan1D {
   int n;
   int npass;
-  int rad[kMaxPass];
-  int twoff[kMaxPass];  // offset (complex units) of pass s's twiddle table,
+  int rad[kPlanSlots];
+  int twoff[kPlanSlots];  // offset (complex units) of pass s's twiddle table,
                         // entries (r-1)*Ns + k = exp(-2 pi i r k / (Ns R)); a
                         // generic-radix pass appends its R roots exp(-2 pi i m/R)
 };
@@ -458,14 +459,15 @@ __device__ __forceinline__ void fft_pass_dispatch(int R, T* lds, int mode, const
 // the fused kernels) LICM would otherwise hoist every pass's loop-invariant
 // index math out of the loop and keep it live in registers (256 VGPRs + 5 KB
 // of scratch per lane).
-template <typename T, int MAXB, int SIGN>
+template <typename T, int MAXB, int SIGN, int NSLOT = kMaxPass>
 __device__ __forceinline__ void fft_dir(T* lds, int mode0, const LineGeom& gfirst,
                                         const LineGeom& g, const Grid2D& G, const Plan1D& p,
                                         const cpx<T>* tw) {
+  static_assert(NSLOT <= kPlanSlots, "plan capacity");
   int Ns = 1;
   int n = p.n;
   asm volatile("" : "+s"(n));
-  sfor<kMaxPass>([&](auto si) {
+  sfor<NSLOT>([&](auto si) {
     constexpr int s = decltype(si)::value;
     if (s < p.npass) {
       const int R = p.rad[s];

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define CCSC_ABI_VERSION 4
+#define CCSC_ABI_VERSION 5
 
 /* status codes */
 #define CCSC_OK 0
@@ -226,6 +226,79 @@ int32_t ccsc_session_kernel_stats(ccsc_session* s, int32_t kernel_id, int64_t* l
                                   double* total_ms, double* alg_bytes_per_launch, char* err,
                                   size_t errlen);
 void ccsc_session_destroy(ccsc_session* s);
+
+/* ---- reconstruction solvers ------------------------
+ * Sparse-coding reconstruction of images from learned filters; each variant is the
+ * drop-in for one reference function (paths relative to the reference root):
+ *   CCSC_SOLVE_INPAINT2D  [z, res] = admm_solve_conv2D_weighted_sampling(b, kernels, mask,
+ *                         lambda_residual, lambda_prior, smooth_init, max_it, tol, x_orig,
+ *                         verbose)          2D/Inpainting/admm_solve_conv2D_weighted_sampling.m:1-4
+ *   CCSC_SOLVE_POISSON2D  [z, res] = admm_solve_conv_poisson(b, kmat, mask, lambda_residual,
+ *                         lambda_prior, max_it, tol, x_orig, verbose)
+ *                                           2D/Poisson_deconv/admm_solve_conv_poisson.m:1-2
+ *   CCSC_SOLVE_MULTICH    [z, res] = admm_solve_conv23D_weighted_sampling(b, kmat, mask,
+ *                         lambda_residual, lambda_prior, max_it, tol, ~, verbose, smooth_init)
+ *                                           2-3D/Demosaicing/admm_solve_conv23D_weighted_sampling.m:1-2
+ *                         and admm_solve_conv_weighted_sampling_lf (the same text)
+ *                                           4D/ViewSynthesis/admm_solve_conv_weighted_sampling_lf.m:1-2
+ *   CCSC_SOLVE_VIDEO3D    [z, res] = admm_solve_video_weighted_sampling(b, kmat, mask,
+ *                         lambda_residual, lambda_prior, max_it, tol, verbose, psf, smooth_init)
+ *                                           3D/Deblurring/admm_solve_video_weighted_sampling.m:1-2
+ * One call solves n independent images of one shape (the reference's callers loop over
+ * images, e.g. reconstruct_poisson_noise.m:24); each image keeps its own gamma
+ * heuristic (c * lambda_prior / max(b(:))) and its own tol test.  Arrays are
+ * column-major float64 with the image index last. */
+#define CCSC_SOLVE_INPAINT2D 0
+#define CCSC_SOLVE_POISSON2D 1
+#define CCSC_SOLVE_MULTICH 2
+#define CCSC_SOLVE_VIDEO3D 3
+
+typedef struct ccsc_solve_problem {
+  int32_t variant;          /* CCSC_SOLVE_*                                                */
+  int64_t sb[3];            /* image extent x, y (, t for VIDEO3D)                         */
+  int32_t nch;              /* MULTICH: channels W = size(b, 3) (wavelengths / views); else 1 */
+  int64_t n;                /* images solved by this call                                  */
+  int32_t K;                /* learned filters (kernel_size(end)), without the dirac that
+                               POISSON2D appends and VIDEO3D prepends                      */
+  int32_t ksize[3];         /* filter extent x, y (, t); odd                                 */
+  int32_t psf_size[3];      /* VIDEO3D: extent of the blur psf                             */
+  double lambda_residual;
+  double lambda_prior;
+  int32_t max_it;
+  double tol;               /* relative change ||z - z_old|| / ||z||; <= 0: never stops early */
+  int32_t verbose;          /* CCSC_VERBOSE_*: BRIEF/ALL fill the objective / PSNR trace   */
+} ccsc_solve_problem;
+
+typedef struct ccsc_solve_inputs {
+  const double* b;           /* [sx, sy, (st | W), n]                                       */
+  const double* kernels;     /* INPAINT2D/POISSON2D [k,k,K]; MULTICH [k,k,W,K]; VIDEO3D [k,k,k,K] */
+  const double* mask;        /* same shape as b                                              */
+  const double* smooth_init; /* same shape as b; NULL for POISSON2D (it has none)            */
+  const double* psf;         /* VIDEO3D: blur kernel [psf_size]; else NULL                   */
+  const double* x_orig;      /* INPAINT2D/POISSON2D: [sx, sy, n] for the PSNR trace; nullable */
+} ccsc_solve_inputs;
+
+typedef struct ccsc_solve_outputs {
+  double* z;    /* [X, Y, (T), K', n] codes on the padded grid (K' includes the dirac:
+                   POISSON2D last, VIDEO3D first; MULTICH: X, Y = sx, sy); nullable       */
+  double* res;  /* INPAINT2D/POISSON2D [sx, sy, n]; MULTICH [sx, sy, W, n];
+                   VIDEO3D [sx, sy, st, n]; nullable                                       */
+} ccsc_solve_outputs;
+
+typedef struct ccsc_solvelog {
+  int32_t capacity;   /* entries per image in the arrays below (>= max_it + 1)            */
+  int32_t* iters;     /* [n] ADMM iterations run per image (tol may stop an image early)  */
+  double* obj;        /* [n][capacity] objective of iterate 0..iters (verbose BRIEF/ALL)  */
+  double* psnr;       /* [n][capacity] PSNR vs x_orig (INPAINT2D/POISSON2D)               */
+  double* diff;       /* [n][capacity] ||z - z_old|| / ||z|| (0 for iterate 0)            */
+  double* seconds;    /* [1] device time of the ADMM iterations (setup and output excluded) */
+} ccsc_solvelog;
+
+/* CCSC_OK if this build runs the (valid) problem, else CCSC_E_INVALID /
+ * CCSC_E_UNSUPPORTED with the reason (e.g. a grid length with no FFT plan). */
+int32_t ccsc_solve_supported(const ccsc_solve_problem* p, char* err, size_t errlen);
+int32_t ccsc_solve(ccsc_ctx* ctx, const ccsc_solve_problem* p, const ccsc_solve_inputs* in,
+                   ccsc_solve_outputs* out, ccsc_solvelog* log, char* err, size_t errlen);
 
 /* ---- kernel-level entry points (parity tests of single stages) ---------- */
 /* 2D R2C of `count` real slices [X,Y] -> half spectra [Y][X/2+1] (re,im). */

@@ -78,8 +78,24 @@ def reference_norms():
     return out
 
 
+def solver_fixture(name):
+    """Reconstruction-solver fixture: the oracle (oracle/ccsc_solvers.py) on the seeded
+    case of tests/solver_cases.py -> z, res and the per-iterate objective trace."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from solver_cases import solver_case
+    z, res, log = solver_case(name)
+    np.savez_compressed(os.path.join(GOLD, f"{name}.npz"), z=z, res=res,
+                        obj=np.array(log["obj"]), iters=np.array(log["iters"]),
+                        meta=np.array(json.dumps({"generator": "tools/make_golden.py "
+                                                  "(oracle/ccsc_solvers.py, float64)"})))
+
+
 if __name__ == "__main__":
     os.makedirs(GOLD, exist_ok=True)
+    for nm in ("solve_inpaint", "solve_poisson", "solve_multich", "solve_video"):
+        solver_fixture(nm)
+    if "--solvers" in sys.argv:
+        sys.exit(0)
     learner_fixture("dp_small", "dp", (12, 12), 5, 3, 4, 2, 2, 101)
     learner_fixture("dz_small", "dz", (12, 12), 5, 3, 4, 2, 2, 102)
     learner_fixture("dp_odd", "dp", (11, 10), 5, 3, 6, 3, 2, 103)
