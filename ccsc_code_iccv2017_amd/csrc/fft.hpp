@@ -279,7 +279,7 @@ __device__ __forceinline__ cpx<T> load_elem(const T* lds, const LineGeom& g, con
 // (x direction, estride 1) consecutive lanes take consecutive butterflies of
 // one line; when they are strided (y direction) consecutive lanes take the
 // same butterfly of consecutive lines, so every access is lane-contiguous.
-template <typename T, int R, int MAXB, int SIGN>
+template <typename T, int R, int MAXB, int SIGN, int NT = kNT>
 __device__ __forceinline__ void fft_pass(T* lds, int mode, const LineGeom& gin,
                                          const LineGeom& gout, const Grid2D& G, int n, int Ns,
                                          const cpx<T>* __restrict__ tw) {
@@ -292,7 +292,7 @@ __device__ __forceinline__ void fft_pass(T* lds, int mode, const LineGeom& gin,
   // read phase: load, twiddle (so no twiddle stays live across the barrier)
 #pragma unroll
   for (int b = 0; b < MAXB; ++b) {
-    const int bf = (int)threadIdx.x + b * kNT;
+    const int bf = (int)threadIdx.x + b * NT;
     outbase[b] = -1;
     if (bf < total) {
       int line, j;
@@ -345,10 +345,12 @@ __device__ __forceinline__ void fft_pass(T* lds, int mode, const LineGeom& gin,
 // DC term): ~(2R + 3h)/(2 kGenericQP) LDS reads per output instead of the
 // 3(R-1) of an output-per-thread R-term sum.  The host plan keeps the task
 // count within one per thread (generic_tasks() in engine.cpp).
-template <typename T, int SIGN>
+template <typename T, int SIGN, int NT = kNT, int GT = 1>
 __device__ __forceinline__ void fft_pass_generic(T* lds, int R, int mode, const LineGeom& gin,
                                               const LineGeom& gout, const Grid2D& G, int n,
                                               int Ns, const cpx<T>* __restrict__ tw) {
+  // GT tasks per thread (the slice kernels use 1; the global line kernels of recon.hip
+  // hold up to GT tasks' accumulators across the pass barrier)
   constexpr int QP = kGenericQP;
   const int nb = n / R;
   const int nl = gin.nlines;
@@ -357,97 +359,110 @@ __device__ __forceinline__ void fft_pass_generic(T* lds, int R, int mode, const 
   const int total = nl * nb * ng;
   const bool along = gin.estride == 1;
   const cpx<T>* roots = tw + (R - 1) * Ns;   // (cos, -sin)(2 pi m / R)
-  const int o = (int)threadIdx.x;
-  int dst = -1, q0 = 0;
-  cpx<T> dc = {(T)0, (T)0}, A[QP], B[QP];
-  if (o < total) {
-    int line, j, g;
-    if (along) {   // lanes contiguous in j (contiguous LDS addresses)
-      j = o % nb;
-      const int rest = o / nb;
-      g = rest % ng;
-      line = rest / ng;
-    } else {       // lanes contiguous in line (strided lines: one address per line)
-      line = o % nl;
-      const int rest = o / nl;
-      j = rest % nb;
-      g = rest / nb;
-    }
-    const int k = j % Ns;
-    q0 = 1 + g * QP;
-    int m[QP];
+  int dst[GT], q0[GT];
+  cpx<T> dc[GT], A[GT][QP], B[GT][QP];
 #pragma unroll
-    for (int i = 0; i < QP; ++i) {
-      A[i] = {(T)0, (T)0};
-      B[i] = {(T)0, (T)0};
-      m[i] = 0;
-    }
-    const cpx<T> x0 = load_elem<T>(lds, gin, G, mode, line, j);
-    cpx<T> sdc = {(T)0, (T)0};
-    for (int r = 1; r <= h; ++r) {
-      cpx<T> xa = load_elem<T>(lds, gin, G, mode, line, j + r * nb);
-      cpx<T> xb = load_elem<T>(lds, gin, G, mode, line, j + (R - r) * nb);
-      if (Ns > 1) {
-        cpx<T> wa = tw[(r - 1) * Ns + k], wb = tw[(R - r - 1) * Ns + k];
-        if (SIGN > 0) {
-          wa.y = -wa.y;
-          wb.y = -wb.y;
-        }
-        xa = cmul(xa, wa);
-        xb = cmul(xb, wb);
+  for (int t = 0; t < GT; ++t) {
+    const int o = (int)threadIdx.x + t * NT;
+    dst[t] = -1;
+    q0[t] = 0;
+    if (o < total) {
+      int line, j, g;
+      if (along) {   // lanes contiguous in j (contiguous LDS addresses)
+        j = o % nb;
+        const int rest = o / nb;
+        g = rest % ng;
+        line = rest / ng;
+      } else {       // lanes contiguous in line (strided lines: one address per line)
+        line = o % nl;
+        const int rest = o / nl;
+        j = rest % nb;
+        g = rest / nb;
       }
-      const cpx<T> sr = cadd(xa, xb), dr = csub(xa, xb);
-      sdc = cadd(sdc, sr);
+      const int k = j % Ns;
+      q0[t] = 1 + g * QP;
+      int m[QP];
 #pragma unroll
       for (int i = 0; i < QP; ++i) {
-        m[i] += q0 + i;
-        if (m[i] >= R) m[i] -= R;
-        const cpx<T> rt = roots[m[i]];   // (cos theta, -sin theta)
-        A[i].x += sr.x * rt.x;
-        A[i].y += sr.y * rt.x;
-        B[i].x += dr.x * rt.y;
-        B[i].y += dr.y * rt.y;
+        A[t][i] = {(T)0, (T)0};
+        B[t][i] = {(T)0, (T)0};
+        m[i] = 0;
       }
-    }
-    dc = cadd(x0, sdc);
+      const cpx<T> x0 = load_elem<T>(lds, gin, G, mode, line, j);
+      cpx<T> sdc = {(T)0, (T)0};
+      for (int r = 1; r <= h; ++r) {
+        cpx<T> xa = load_elem<T>(lds, gin, G, mode, line, j + r * nb);
+        cpx<T> xb = load_elem<T>(lds, gin, G, mode, line, j + (R - r) * nb);
+        if (Ns > 1) {
+          cpx<T> wa = tw[(r - 1) * Ns + k], wb = tw[(R - r - 1) * Ns + k];
+          if (SIGN > 0) {
+            wa.y = -wa.y;
+            wb.y = -wb.y;
+          }
+          xa = cmul(xa, wa);
+          xb = cmul(xb, wb);
+        }
+        const cpx<T> sr = cadd(xa, xb), dr = csub(xa, xb);
+        sdc = cadd(sdc, sr);
 #pragma unroll
-    for (int i = 0; i < QP; ++i) A[i] = cadd(A[i], x0);
-    dst = line * gout.lstride + ((j - k) * R + k) * gout.estride;
+        for (int i = 0; i < QP; ++i) {
+          m[i] += q0[t] + i;
+          if (m[i] >= R) m[i] -= R;
+          const cpx<T> rt = roots[m[i]];   // (cos theta, -sin theta)
+          A[t][i].x += sr.x * rt.x;
+          A[t][i].y += sr.y * rt.x;
+          B[t][i].x += dr.x * rt.y;
+          B[t][i].y += dr.y * rt.y;
+        }
+      }
+      dc[t] = cadd(x0, sdc);
+#pragma unroll
+      for (int i = 0; i < QP; ++i) A[t][i] = cadd(A[t][i], x0);
+      dst[t] = line * gout.lstride + ((j - k) * R + k) * gout.estride;
+    }
   }
   lds_sync();
-  if (dst >= 0) {
-    // forward (SIGN < 0): X_q = A + i B, X_{R-q} = A - i B; inverse: the opposite
-    const int ostride = Ns * gout.estride;
-    if (q0 == 1) lds_cpx_store(lds + dst, gout.imoff, dc);
+  const int ostride = Ns * gout.estride;
 #pragma unroll
-    for (int i = 0; i < QP; ++i) {
-      const int q = q0 + i;
-      if (q <= h) {
-        const cpx<T> iB = {-B[i].y, B[i].x};
-        const cpx<T> xq = SIGN < 0 ? cadd(A[i], iB) : csub(A[i], iB);
-        const cpx<T> xr = SIGN < 0 ? csub(A[i], iB) : cadd(A[i], iB);
-        lds_cpx_store(lds + dst + q * ostride, gout.imoff, xq);
-        lds_cpx_store(lds + dst + (R - q) * ostride, gout.imoff, xr);
+  for (int t = 0; t < GT; ++t) {
+    if (dst[t] >= 0) {
+      // forward (SIGN < 0): X_q = A + i B, X_{R-q} = A - i B; inverse: the opposite
+      if (q0[t] == 1) lds_cpx_store(lds + dst[t], gout.imoff, dc[t]);
+#pragma unroll
+      for (int i = 0; i < QP; ++i) {
+        const int q = q0[t] + i;
+        if (q <= h) {
+          const cpx<T> iB = {-B[t][i].y, B[t][i].x};
+          const cpx<T> xq = SIGN < 0 ? cadd(A[t][i], iB) : csub(A[t][i], iB);
+          const cpx<T> xr = SIGN < 0 ? csub(A[t][i], iB) : cadd(A[t][i], iB);
+          lds_cpx_store(lds + dst[t] + q * ostride, gout.imoff, xq);
+          lds_cpx_store(lds + dst[t] + (R - q) * ostride, gout.imoff, xr);
+        }
       }
     }
   }
   lds_sync();
 }
 
-template <typename T, int MAXB, int SIGN>
+template <typename T, int MAXB, int SIGN, int NT = kNT, int GT = 1>
 __device__ __forceinline__ void fft_pass_dispatch(int R, T* lds, int mode, const LineGeom& gin,
                                                   const LineGeom& gout, const Grid2D& G, int n,
                                                   int Ns, const cpx<T>* tw) {
   switch (R) {
-    case 2: fft_pass<T, 2, maxb_for_radix(2), SIGN>(lds, mode, gin, gout, G, n, Ns, tw); break;
-    case 3: fft_pass<T, 3, maxb_for_radix(3), SIGN>(lds, mode, gin, gout, G, n, Ns, tw); break;
-    case 4: fft_pass<T, 4, maxb_for_radix(4), SIGN>(lds, mode, gin, gout, G, n, Ns, tw); break;
-    case 5: fft_pass<T, 5, maxb_for_radix(5), SIGN>(lds, mode, gin, gout, G, n, Ns, tw); break;
-    case 7: fft_pass<T, 7, maxb_for_radix(7), SIGN>(lds, mode, gin, gout, G, n, Ns, tw); break;
-    case 8: fft_pass<T, 8, maxb_for_radix(8), SIGN>(lds, mode, gin, gout, G, n, Ns, tw); break;
-    case 10: fft_pass<T, 10, maxb_for_radix(10), SIGN>(lds, mode, gin, gout, G, n, Ns, tw); break;
-    case 11: fft_pass<T, 11, maxb_for_radix(11), SIGN>(lds, mode, gin, gout, G, n, Ns, tw); break;
-    default: fft_pass_generic<T, SIGN>(lds, R, mode, gin, gout, G, n, Ns, tw); break;
+#define CCSC_NATIVE_PASS(RR)                                                                   \
+    case RR:                                                                                   \
+      fft_pass<T, RR, maxb_for_radix(RR), SIGN, NT>(lds, mode, gin, gout, G, n, Ns, tw);       \
+      break;
+    CCSC_NATIVE_PASS(2)
+    CCSC_NATIVE_PASS(3)
+    CCSC_NATIVE_PASS(4)
+    CCSC_NATIVE_PASS(5)
+    CCSC_NATIVE_PASS(7)
+    CCSC_NATIVE_PASS(8)
+    CCSC_NATIVE_PASS(10)
+    CCSC_NATIVE_PASS(11)
+#undef CCSC_NATIVE_PASS
+    default: fft_pass_generic<T, SIGN, NT, GT>(lds, R, mode, gin, gout, G, n, Ns, tw); break;
   }
 }
 
@@ -459,7 +474,7 @@ __device__ __forceinline__ void fft_pass_dispatch(int R, T* lds, int mode, const
 // the fused kernels) LICM would otherwise hoist every pass's loop-invariant
 // index math out of the loop and keep it live in registers (256 VGPRs + 5 KB
 // of scratch per lane).
-template <typename T, int MAXB, int SIGN, int NSLOT = kMaxPass>
+template <typename T, int MAXB, int SIGN, int NSLOT = kMaxPass, int NT = kNT, int GT = 1>
 __device__ __forceinline__ void fft_dir(T* lds, int mode0, const LineGeom& gfirst,
                                         const LineGeom& g, const Grid2D& G, const Plan1D& p,
                                         const cpx<T>* tw) {
@@ -472,8 +487,10 @@ __device__ __forceinline__ void fft_dir(T* lds, int mode0, const LineGeom& gfirs
     if (s < p.npass) {
       const int R = p.rad[s];
       const cpx<T>* tws = tw + p.twoff[s];
-      if constexpr (s == 0) fft_pass_dispatch<T, MAXB, SIGN>(R, lds, mode0, gfirst, g, G, n, Ns, tws);
-      else fft_pass_dispatch<T, MAXB, SIGN>(R, lds, kModePlain, g, g, G, n, Ns, tws);
+      if constexpr (s == 0)
+        fft_pass_dispatch<T, MAXB, SIGN, NT, GT>(R, lds, mode0, gfirst, g, G, n, Ns, tws);
+      else
+        fft_pass_dispatch<T, MAXB, SIGN, NT, GT>(R, lds, kModePlain, g, g, G, n, Ns, tws);
       Ns *= R;
     }
   });

@@ -24,11 +24,26 @@ __device__ __forceinline__ T soft_thr(T a, T th) {
   return a > th ? a - th : (a < -th ? a + th : (T)0);
 }
 
+// block-level sum over the kLineNT threads (scratch: kLineNT / 64 elements)
+template <typename T>
+__device__ __forceinline__ T line_block_sum(T v, T* scratch) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) scratch[w] = v;
+  __syncthreads();
+  T s = 0;
+#pragma unroll
+  for (int i = 0; i < kLineNT / 64; ++i) s += scratch[i];
+  __syncthreads();
+  return s;
+}
+
 // ---------------------------------------------------------------------------
 // Row pass: 2L rows (L row pairs) of one slice per workgroup.  LDS rows of RS T.
 // ---------------------------------------------------------------------------
 template <typename T, int MODE>
-__global__ __launch_bounds__(kNT) void k_rows(RowArgs<T> a, RowGeom rg,
+__global__ __launch_bounds__(kLineNT) void k_rows(RowArgs<T> a, RowGeom rg,
                                               const cpx<T>* __restrict__ tw) {
   extern __shared__ __align__(16) unsigned char smem_raw[];
   T* lds = reinterpret_cast<T*>(smem_raw);
@@ -45,27 +60,30 @@ __global__ __launch_bounds__(kNT) void k_rows(RowArgs<T> a, RowGeom rg,
   const int sl = (int)(slice - img * a.per_img);
   const int64_t rbase = (slice * rg.rows + row0) * (int64_t)X;     // real arrays
   const int64_t sbase = (slice * rg.rows + row0) * (int64_t)Xh;    // spectra
+  // twiddle tables in LDS (every pass reads them per butterfly)
+  cpx<T>* s_tw = reinterpret_cast<cpx<T>*>(lds + rows_tw_off(rg));
+  for (int i = threadIdx.x; i < rg.ntw; i += kLineNT) s_tw[i] = tw[i];
 
   // ---- load ---------------------------------------------------------------
   if (MODE == kRowFwd) {
-    for (int i = threadIdx.x; i < G.Yp * X; i += kNT) {
+    for (int i = threadIdx.x; i < G.Yp * X; i += kLineNT) {
       const int ry = i / X, x = i - ry * X;
       lds[ry * RS + x] = ry < nrows ? a.src[rbase + (int64_t)ry * X + x] : (T)0;
     }
   } else if (a.first) {
-    for (int i = threadIdx.x; i < G.Yp * X; i += kNT) {
+    for (int i = threadIdx.x; i < G.Yp * X; i += kLineNT) {
       const int ry = i / X, x = i - ry * X;
       lds[ry * RS + x] = (T)0;
     }
   } else {
-    for (int i = threadIdx.x; i < nrows * Xh; i += kNT) {
+    for (int i = threadIdx.x; i < nrows * Xh; i += kLineNT) {
       const int ry = i / Xh, xp = i - ry * Xh;
       const cpx<T> c = a.S[sbase + (int64_t)ry * Xh + xp];
       lds[ry * RS + 2 * xp] = c.x;
       lds[ry * RS + 2 * xp + 1] = c.y;
     }
     lds_sync();
-    fft_dir<T, kMaxB, +1, kPlanSlots>(lds, kModeHermPair, gx, gx, G, G.px, tw);
+    fft_dir<T, kMaxB, +1, kPlanSlots, kLineNT, kLineGT>(lds, kModeHermPair, gx, gx, G, G.px, s_tw);
   }
   lds_sync();
 
@@ -75,7 +93,7 @@ __global__ __launch_bounds__(kNT) void k_rows(RowArgs<T> a, RowGeom rg,
     const bool act = !a.active || a.active[img] != 0;
     const T th = a.theta ? a.theta[img] : (T)0;
     const bool ident = a.prox == 1 && sl == 0;
-    for (int i = threadIdx.x; i < nrows * X; i += kNT) {
+    for (int i = threadIdx.x; i < nrows * X; i += kLineNT) {
       const int ry = i / X, x = i - ry * X;
       const int64_t gi = rbase + (int64_t)ry * X + x;
       const T z = lds[ry * RS + x];
@@ -97,7 +115,7 @@ __global__ __launch_bounds__(kNT) void k_rows(RowArgs<T> a, RowGeom rg,
   } else if (MODE == kRowIterX) {
     const T th = a.theta[img];
     const T ith = (T)1 / th;
-    for (int i = threadIdx.x; i < nrows * X; i += kNT) {
+    for (int i = threadIdx.x; i < nrows * X; i += kLineNT) {
       const int ry = i / X, x = i - ry * X;
       const int64_t gi = rbase + (int64_t)ry * X + x;
       const T v = lds[ry * RS + x];
@@ -131,7 +149,7 @@ __global__ __launch_bounds__(kNT) void k_rows(RowArgs<T> a, RowGeom rg,
       lds[ry * RS + x] = u + dn;                          // xi1
     }
   } else if (MODE == kRowRes) {
-    for (int i = threadIdx.x; i < nrows * X; i += kNT) {
+    for (int i = threadIdx.x; i < nrows * X; i += kLineNT) {
       const int ry = i / X, x = i - ry * X;
       const int row = row0 + ry;
       const int y = row % a.Y, t = row / a.Y;
@@ -145,9 +163,9 @@ __global__ __launch_bounds__(kNT) void k_rows(RowArgs<T> a, RowGeom rg,
   }
   if (MODE != kRowFwd && MODE != kRowRes && a.part) {
     T* scratch = lds + (size_t)G.Yp * RS + 16;   // past the slice (rows_smem_bytes)
-    const T s0 = block_sum(p0, scratch);
-    const T s1 = block_sum(p1, scratch);
-    const T s2 = block_sum(p2, scratch);
+    const T s0 = line_block_sum(p0, scratch);
+    const T s1 = line_block_sum(p1, scratch);
+    const T s2 = line_block_sum(p2, scratch);
     if (threadIdx.x == 0) {
       const int off = (MODE == kRowIterX) ? 3 : 0;   // codes: dz^2, z^2, |z|; data: obj, psnr
       T* pp = a.part + (((img * a.part_slices + a.part_off + sl) * rg.groups) + g) * kRowParts;
@@ -161,12 +179,12 @@ __global__ __launch_bounds__(kNT) void k_rows(RowArgs<T> a, RowGeom rg,
 
   // ---- forward x lines and two-for-one separation -------------------------------
   if (G.Yp != nrows)
-    for (int x = threadIdx.x; x < X; x += kNT) lds[nrows * RS + x] = (T)0;
+    for (int x = threadIdx.x; x < X; x += kLineNT) lds[nrows * RS + x] = (T)0;
   lds_sync();
-  fft_dir<T, kMaxB, -1, kPlanSlots>(lds, kModePlain, gx, gx, G, G.px, tw);
+  fft_dir<T, kMaxB, -1, kPlanSlots, kLineNT, kLineGT>(lds, kModePlain, gx, gx, G, G.px, s_tw);
   lds_sync();
   const int np = G.Yp / 2;
-  for (int i = threadIdx.x; i < np * Xh; i += kNT) {
+  for (int i = threadIdx.x; i < np * Xh; i += kLineNT) {
     const int j = i / Xh, xp = i - j * Xh;
     const int x2 = xp == 0 ? 0 : X - xp;
     const T* r0 = lds + (2 * j) * RS;
@@ -184,7 +202,7 @@ __global__ __launch_bounds__(kNT) void k_rows(RowArgs<T> a, RowGeom rg,
 // Column pass: TC consecutive x' columns of one line set, LDS [e][c] complex.
 // ---------------------------------------------------------------------------
 template <typename T, int SIGN>
-__global__ __launch_bounds__(kNT) void k_cols(cpx<T>* __restrict__ S, ColGeom cg,
+__global__ __launch_bounds__(kLineNT) void k_cols(cpx<T>* __restrict__ S, ColGeom cg,
                                               const cpx<T>* __restrict__ tw) {
   extern __shared__ __align__(16) unsigned char smem_raw[];
   T* lds = reinterpret_cast<T*>(smem_raw);
@@ -194,7 +212,9 @@ __global__ __launch_bounds__(kNT) void k_cols(cpx<T>* __restrict__ S, ColGeom cg
   const int c0 = tile * TC;
   const int nc = min(TC, cg.Xh - c0);
   cpx<T>* base = S + (o % cg.ninner) * cg.sin + (o / cg.ninner) * cg.sout + c0;
-  for (int i = threadIdx.x; i < n * TC; i += kNT) {
+  cpx<T>* s_tw = reinterpret_cast<cpx<T>*>(lds + (size_t)2 * n * TC);
+  for (int i = threadIdx.x; i < cg.ntw; i += kLineNT) s_tw[i] = tw[i];
+  for (int i = threadIdx.x; i < n * TC; i += kLineNT) {
     const int e = i / TC, c = i - e * TC;
     cpx<T> v = {(T)0, (T)0};
     if (c < nc) v = base[(int64_t)e * cg.es + c];
@@ -204,9 +224,9 @@ __global__ __launch_bounds__(kNT) void k_cols(cpx<T>* __restrict__ S, ColGeom cg
   const LineGeom g = {TC, 2, 2 * TC, 1};
   Grid2D Gd{};
   lds_sync();
-  fft_dir<T, kMaxB, SIGN, kPlanSlots>(lds, kModePlain, g, g, Gd, cg.p, tw);
+  fft_dir<T, kMaxB, SIGN, kPlanSlots, kLineNT, kLineGT>(lds, kModePlain, g, g, Gd, cg.p, s_tw);
   lds_sync();
-  for (int i = threadIdx.x; i < n * TC; i += kNT) {
+  for (int i = threadIdx.x; i < n * TC; i += kLineNT) {
     const int e = i / TC, c = i - e * TC;
     if (c < nc) base[(int64_t)e * cg.es + c] = {lds[2 * i], lds[2 * i + 1]};
   }
@@ -355,10 +375,10 @@ __global__ __launch_bounds__(256) void k_reduce_parts(const T* __restrict__ part
 // launchers
 // ---------------------------------------------------------------------------
 size_t rows_smem_bytes(const RowGeom& rg, size_t tsize) {
-  return ((size_t)(2 * rg.L) * rg.G.RS + 16 + kNT / 64) * tsize;
+  return (rows_tw_off(rg) + 2 * (size_t)rg.ntw) * tsize;
 }
 size_t cols_smem_bytes(const ColGeom& cg, size_t tsize) {
-  return (size_t)cg.n * cg.TC * 2 * tsize;
+  return ((size_t)cg.n * cg.TC * 2 + 2 * (size_t)cg.ntw) * tsize;
 }
 
 template <typename T>
@@ -368,11 +388,11 @@ hipError_t launch_rows(int mode, const RowArgs<T>& a, int64_t nslices, const Row
   const dim3 grid((unsigned)nslices, (unsigned)rg.groups);
   const size_t sm = rows_smem_bytes(rg, sizeof(T));
   switch (mode) {
-    case kRowFwd: hipLaunchKernelGGL((k_rows<T, kRowFwd>), grid, dim3(kNT), sm, st, a, rg, tw); break;
-    case kRowIterZ: hipLaunchKernelGGL((k_rows<T, kRowIterZ>), grid, dim3(kNT), sm, st, a, rg, tw); break;
-    case kRowIterX: hipLaunchKernelGGL((k_rows<T, kRowIterX>), grid, dim3(kNT), sm, st, a, rg, tw); break;
-    case kRowFinalZ: hipLaunchKernelGGL((k_rows<T, kRowFinalZ>), grid, dim3(kNT), sm, st, a, rg, tw); break;
-    case kRowRes: hipLaunchKernelGGL((k_rows<T, kRowRes>), grid, dim3(kNT), sm, st, a, rg, tw); break;
+    case kRowFwd: hipLaunchKernelGGL((k_rows<T, kRowFwd>), grid, dim3(kLineNT), sm, st, a, rg, tw); break;
+    case kRowIterZ: hipLaunchKernelGGL((k_rows<T, kRowIterZ>), grid, dim3(kLineNT), sm, st, a, rg, tw); break;
+    case kRowIterX: hipLaunchKernelGGL((k_rows<T, kRowIterX>), grid, dim3(kLineNT), sm, st, a, rg, tw); break;
+    case kRowFinalZ: hipLaunchKernelGGL((k_rows<T, kRowFinalZ>), grid, dim3(kLineNT), sm, st, a, rg, tw); break;
+    case kRowRes: hipLaunchKernelGGL((k_rows<T, kRowRes>), grid, dim3(kLineNT), sm, st, a, rg, tw); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -384,8 +404,8 @@ hipError_t launch_cols(cpx<T>* S, int sign, int64_t nouter, const ColGeom& cg, c
   if (nouter <= 0) return hipSuccess;
   const dim3 grid((unsigned)nouter, (unsigned)cg.xtiles);
   const size_t sm = cols_smem_bytes(cg, sizeof(T));
-  if (sign < 0) hipLaunchKernelGGL((k_cols<T, -1>), grid, dim3(kNT), sm, st, S, cg, tw);
-  else hipLaunchKernelGGL((k_cols<T, +1>), grid, dim3(kNT), sm, st, S, cg, tw);
+  if (sign < 0) hipLaunchKernelGGL((k_cols<T, -1>), grid, dim3(kLineNT), sm, st, S, cg, tw);
+  else hipLaunchKernelGGL((k_cols<T, +1>), grid, dim3(kLineNT), sm, st, S, cg, tw);
   return hipGetLastError();
 }
 

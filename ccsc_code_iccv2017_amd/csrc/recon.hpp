@@ -24,6 +24,7 @@ struct RowGeom {
   int rows;
   int L;
   int groups;
+  int ntw;     // twiddle table length (complex), staged into LDS
 };
 
 // Column-pass geometry: lines of length n with element stride es (complex units),
@@ -32,8 +33,14 @@ struct RowGeom {
 struct ColGeom {
   Plan1D p;
   int n, TC, Xh, xtiles, ninner;
+  int ntw;     // twiddle table length (complex), staged into LDS
   int64_t es, sin, sout;
 };
+
+// Line kernels run 256-thread workgroups (several per CU: their LDS tiles are small) and
+// hold up to kLineGT generic-radix tasks per thread across a pass barrier.
+constexpr int kLineNT = 256;
+constexpr int kLineGT = 4;
 
 constexpr int kRowParts = 5;   // partial sums per row workgroup (see RowArgs)
 
@@ -76,6 +83,11 @@ struct RowArgs {
   T scale;              // kRowRes: C2R scale
 };
 
+// LDS offset (units of T, 16-B aligned) of the row kernel's twiddle table: past the
+// 2L rows of the slice and the reduction scratch
+__host__ __device__ inline size_t rows_tw_off(const RowGeom& rg) {
+  return ((size_t)(2 * rg.L) * rg.G.RS + 16 + kLineNT / 64 + 1) & ~(size_t)1;
+}
 size_t rows_smem_bytes(const RowGeom& rg, size_t tsize);
 size_t cols_smem_bytes(const ColGeom& cg, size_t tsize);
 

@@ -65,14 +65,14 @@ static bool plan_line(int n, int nlines, Plan1D& out) {
     if ((int)cur.size() >= kPlanSlots || (int)cur.size() + 1 > best_np) return;
     for (int R : kNativeRad) {
       if (rem % R) continue;
-      if ((int64_t)(n / R) * nlines > (int64_t)maxb_for_radix(R) * kNT) continue;
+      if ((int64_t)(n / R) * nlines > (int64_t)maxb_for_radix(R) * kLineNT) continue;
       cur.push_back(R);
       dfs(rem / R, ng);
       cur.pop_back();
     }
     for (int R = 3; R <= rem; R += 2) {
       if (rem % R || native_rad(R)) continue;
-      if (gen_tasks(n, nlines, R) > kNT) continue;
+      if (gen_tasks(n, nlines, R) > (int64_t)kLineGT * kLineNT) continue;
       cur.push_back(R);
       dfs(rem / R, ng + 1);
       cur.pop_back();
@@ -105,7 +105,16 @@ static void add_twiddles(Plan1D& p, std::vector<cpx<double>>& t) {
   }
 }
 
-constexpr size_t kLineLds = 64 * 1024;   // two workgroups per CU
+constexpr size_t kLineLds = 40 * 1024;   // four or more workgroups per CU
+
+static int twiddle_count(const Plan1D& p) {
+  int n = 0, Ns = 1;
+  for (int s = 0; s < p.npass; ++s) {
+    n += (p.rad[s] - 1) * Ns + (native_rad(p.rad[s]) ? 0 : p.rad[s]);
+    Ns *= p.rad[s];
+  }
+  return std::max(n, 1);
+}
 
 static bool plan_rows(int X, int rows, RowGeom& rg) {
   rg = RowGeom{};
@@ -117,8 +126,9 @@ static bool plan_rows(int X, int rows, RowGeom& rg) {
   rg.rows = rows;
   for (int L = (rows + 1) / 2; L >= 1; --L) {
     rg.L = L;
-    if (rows_smem_bytes(rg, sizeof(double)) > kLineLds) continue;
     if (!plan_line(X, L, G.px)) continue;
+    rg.ntw = twiddle_count(G.px);
+    if (rows_smem_bytes(rg, sizeof(double)) > kLineLds) continue;
     rg.groups = (rows + 2 * L - 1) / (2 * L);
     return true;
   }
@@ -131,8 +141,9 @@ static bool plan_cols(int n, int Xh, ColGeom& cg) {
   cg.Xh = Xh;
   for (int TC = std::min(32, Xh); TC >= 1; --TC) {
     cg.TC = TC;
-    if (cols_smem_bytes(cg, sizeof(double)) > kLineLds) continue;
     if (!plan_line(n, TC, cg.p)) continue;
+    cg.ntw = twiddle_count(cg.p);
+    if (cols_smem_bytes(cg, sizeof(double)) > kLineLds) continue;
     cg.xtiles = (Xh + TC - 1) / TC;
     return true;
   }
