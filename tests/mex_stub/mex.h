@@ -1,6 +1,6 @@
 /*
  * mex.h -- TEST-ONLY stand-in for MATLAB's MEX API (no MATLAB in this image).
- * It declares exactly the subset matlab/ccsc_mex.c uses, with MATLAB's
+ * It declares exactly the subset matlab/ccsc_mex.c and matlab/ccsc_solve_mex.c use, with MATLAB's
  * signatures (R2018a interleaved-complex API), so the gateway compiles with
  * -Wall -Werror here and runs under tests/mex_stub/mexstub.c, a minimal
  * column-major mxArray implementation driven from Python (tests/test_mex.py).
@@ -38,6 +38,8 @@ mxArray* mxCreateStructMatrix(mwSize m, mwSize n, int nfields, const char** name
 void mxSetField(mxArray* s, size_t i, const char* name, mxArray* v);
 void mxSetN(mxArray* a, mwSize n);
 void mxDestroyArray(mxArray* a);
+void* mxCalloc(size_t n, size_t size);
+void mxFree(void* ptr);
 void mexErrMsgIdAndTxt(const char* id, const char* fmt, ...);
 int mexPrintf(const char* fmt, ...);
 int mexEvalString(const char* cmd);

@@ -138,6 +138,8 @@ mxArray* hx_field(const mxArray* s, const char* name) {
     if (!strcmp(s->fnames[f], name)) return s->fvals[f];
   return NULL;
 }
+void* mxCalloc(size_t n, size_t size) { return calloc(n ? n : 1, size); }
+void mxFree(void* ptr) { free(ptr); }
 void hx_free(mxArray* a) { mxDestroyArray(a); }
 /* 0 on success; else the mexErrMsgIdAndTxt message in err */
 int hx_call(int nlhs, mxArray** plhs, int nrhs, mxArray** prhs, char* err, size_t errlen) {

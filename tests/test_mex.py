@@ -16,21 +16,44 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 STUB = os.path.join(ROOT, "tests", "mex_stub")
 HARNESS = os.path.join(STUB, "_build", "libccsc_mexharness.so")
+SOLVE_HARNESS = os.path.join(STUB, "_build", "libccsc_solvemexharness.so")
 
 
-def test_gateway_compiles_warning_free():
+@pytest.mark.parametrize("gateway", ["ccsc_mex.c", "ccsc_solve_mex.c"])
+def test_gateway_compiles_warning_free(gateway):
     r = subprocess.run(["gcc", "-std=c11", "-Wall", "-Wextra", "-Werror", "-Wno-unused-parameter",
                         "-fsyntax-only", "-I", STUB, "-I", os.path.join(ROOT, "include"),
-                        os.path.join(ROOT, "matlab", "ccsc_mex.c")], capture_output=True, text=True)
+                        os.path.join(ROOT, "matlab", gateway)], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
 
 
-def _harness():
+def test_solver_wrappers_keep_the_reference_signatures():
+    """Each .m wrapper's function line names the reference function with its arguments."""
+    sigs = {
+        "admm_solve_conv2D_weighted_sampling": "b, kernels, mask, lambda_residual, lambda_prior, "
+                                               "smooth_init, max_it, tol, x_orig, verbose",
+        "admm_solve_conv_poisson": "b, kmat, mask, lambda_residual, lambda_prior, max_it, tol, "
+                                   "x_orig, verbose",
+        "admm_solve_conv23D_weighted_sampling": "b, kmat, mask, lambda_residual, lambda_prior, "
+                                                "max_it, tol, ~, verbose, smooth_init",
+        "admm_solve_conv_weighted_sampling_lf": "b, kmat, mask, lambda_residual, lambda_prior, "
+                                                "max_it, tol, ~, verbose, smooth_init",
+        "admm_solve_video_weighted_sampling": "b, kmat, mask, lambda_residual, lambda_prior, "
+                                              "max_it, tol, verbose, psf, smooth_init",
+    }
+    for name, args in sigs.items():
+        txt = open(os.path.join(ROOT, "matlab", name + ".m")).read()
+        head = " ".join(txt.split(")")[0].replace("...", " ").split())
+        assert f"[ z, res ] = {name}(" in head, head
+        assert " ".join(args.split()) in head, head
+
+
+def _harness(path=HARNESS):
     from ccsc_code_iccv2017_amd import _lib as L
     L.lib()                       # libccsc first (one HIP runtime per process, _lib.lib)
-    if not os.path.exists(HARNESS):
-        pytest.fail(f"{HARNESS} missing: run tests/mex_stub/build.sh")
-    h = C.CDLL(HARNESS)
+    if not os.path.exists(path):
+        pytest.fail(f"{path} missing: run tests/mex_stub/build.sh")
+    h = C.CDLL(path)
     P = C.c_void_p
     h.hx_double.restype = P
     h.hx_double.argtypes = [C.POINTER(C.c_double), C.c_int, C.POINTER(C.c_int64)]
@@ -107,6 +130,50 @@ def test_mexfunction_matches_engine(gpu_ctx, devices):
         rc, err, _ = _call(h, 1, bad)
         assert rc == 1 and "ccsc:" in err
         h.hx_free(bad[1])
+    finally:
+        for a in args:
+            h.hx_free(a)
+        h.hx_exit()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["solve_inpaint", "solve_video"])
+def test_solve_mexfunction_matches_engine(gpu_ctx, name):
+    """matlab/ccsc_solve_mex.c as the .m wrappers call it == ccsc_code_iccv2017_amd.solvers."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from solver_cases import solver_inputs
+    from ccsc_code_iccv2017_amd import solvers as SV
+    h = _harness(SOLVE_HARNESS)
+    inp = solver_inputs(name)
+    variant = 0 if name == "solve_inpaint" else 3
+    z_e, res_e, _ = SV.solve(variant, inp["b"], inp["kernels"], inp["mask"], inp["lambda_residual"],
+                             inp["lambda_prior"], inp["max_it"], 0.0, "none",
+                             smooth_init=inp.get("smooth_init"), psf=inp.get("psf"),
+                             x_orig=inp.get("x_orig"), ctx=gpu_ctx)
+    empty = np.zeros((0,))
+    args = [_mx(h, variant), _mx(h, inp["b"]), _mx(h, inp["kernels"]), _mx(h, inp["mask"]),
+            _mx(h, inp["lambda_residual"]), _mx(h, inp["lambda_prior"]), _mx(h, inp["max_it"]),
+            _mx(h, 0.0), h.hx_string(b"brief"), _mx(h, inp["smooth_init"]),
+            _mx(h, inp["psf"]) if "psf" in inp else _mx(h, empty),
+            _mx(h, inp["x_orig"]) if "x_orig" in inp else _mx(h, empty), _mx(h, 0)]
+    try:
+        rc, err, out = _call(h, 2, args)            # [z, res]
+        assert rc == 0, err
+        z_m, res_m = _np(h, out[0]), _np(h, out[1])
+        for m in out:
+            h.hx_free(m)
+        np.testing.assert_allclose(z_m.reshape(z_e.shape), z_e, rtol=0, atol=1e-12 * np.abs(z_e).max())
+        np.testing.assert_allclose(res_m.reshape(res_e.shape), res_e, rtol=0,
+                                   atol=1e-12 * np.abs(res_e).max())
+        rc, err, out = _call(h, 1, args)            # nargout = 1: z only
+        assert rc == 0, err
+        h.hx_free(out[0])
+        bad = list(args)
+        bad[3] = _mx(h, inp["mask"][:-1])           # mask of the wrong size: a MATLAB error
+        rc, err, _ = _call(h, 1, bad)
+        assert rc == 1 and "ccsc:" in err
+        h.hx_free(bad[3])
     finally:
         for a in args:
             h.hx_free(a)
