@@ -421,6 +421,7 @@ struct Session2D {
   // in state order, W the last w in bin-slot order solved with dws (dhs or dhws);
   // Bhs / dhs / sdens: B^, the current filter spectrum and sden in bin-slot order.
   bool zl_on = false;
+  bool zhat_line = true;   // D-precompute spectra on the lanes (CCSC_ZHAT_LINE=0: k_zhat_split)
   DevBuf Bhs, dhs, dhws, sdens;
   const cpx<double>* dws = nullptr;
   // tol > 0 with the register-line z-step: what `yz` holds (state order) while the
@@ -565,6 +566,10 @@ struct Session2D {
     if (m.W) W.alloc(m.W);
     if (m.dhw) dhatw.alloc(m.dhw);
     zl_on = m.zl != 0;
+    {
+      const char* ev = std::getenv("CCSC_ZHAT_LINE");
+      zhat_line = !(ev && ev[0] == '0');
+    }
     if (zl_on) {
       Bhs.alloc((size_t)np * F * 16);
       dhs.alloc((size_t)K * F * 16);
@@ -889,7 +894,11 @@ struct Session2D {
 
     // ---- D precompute (dP:95-99) ----
     for (int64_t jl = 0; jl < nbl; ++jl) {
-      if (zmode)  // fft2(z) of the state a: fft2(u - y) + XY conj(dw) w, u = soft(a)
+      if (zmode == 2 && zhat_line)   // the same on the lanes (zline.hip)
+        HIPCHK(launch_zhat_line<double>(z.as<double>() + (size_t)jl * ni * K * P,
+                                        W.as<cpx<double>>() + (size_t)jl * ni * F, dws,
+                                        Zh.as<cpx<double>>(), ni, K, theta, st));
+      else if (zmode)  // fft2(z) of the state a: fft2(u - y) + XY conj(dw) w, u = soft(a)
         HIPCHK(launch_zhat_split<double>(z.as<double>() + (size_t)jl * ni * K * P,
                                          W.as<cpx<double>>() + (size_t)jl * ni * F,
                                          zmode == 2 ? dws : dw, Zh.as<cpx<double>>(), ni,

@@ -80,6 +80,11 @@ hipError_t launch_zline(const T* A, T* Ao, const T* Zn, const T* Yn, cpx<T>* W, 
                         T* zpart = nullptr);
 template <typename T>
 hipError_t launch_state_to_nat_inplace(T* a, int64_t count, hipStream_t st);
+// fft2(z) of the register-line state for the D-precompute (k_zhat_split's result in
+// natural order, the transforms on the lanes): dst [npatch][K][F]
+template <typename T>
+hipError_t launch_zhat_line(const T* A, const cpx<T>* W, const cpx<T>* dcorr, cpx<T>* dst,
+                            int64_t npatch, int K, T theta, hipStream_t st);
 template <typename T>
 hipError_t launch_to_slots(const cpx<T>* src, cpx<T>* dst, int64_t count, hipStream_t st);
 template <typename T>

@@ -350,6 +350,88 @@ __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn
   }
 }
 
+// D-precompute spectra of the register-line state (dP:95-99, the fft2(z) of
+// precompute_H_hat_D's input): for the KB filter slices k0..k0+KB-1 of patch p,
+//   zhat = fft2(u - y) + XY conj(dcorr_k) w,   u = soft(a), y = a - u,
+// i.e. the R2C half of k_zline (P4 elementwise, P5 x-R2C, P7 separation, P9 y-R2C)
+// with the correction term added as each bin forms.  Out: natural-order half spectra
+// dst[(p K + k) F + y Xh + c] (the layout the Gram kernels read).  One workgroup per
+// (patch, KB slices), three barriers per slice; the stores of a wave cover 5 columns x
+// 11 rows per register, merged in L2.
+template <typename T, int KB>
+__global__ __launch_bounds__(zl::NT) void k_zhat_line(const T* __restrict__ A,
+                                                      const cpx<T>* __restrict__ W,
+                                                      const cpx<T>* __restrict__ dcorr,
+                                                      cpx<T>* __restrict__ dst, int K, int kgroups,
+                                                      T theta) {
+  using V2 = typename vec2_t<T>::type;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  cpx<T>* sT = reinterpret_cast<cpx<T>*>(smem);
+  const int64_t p = blockIdx.x / kgroups;
+  const int k0 = (int)(blockIdx.x - p * kgroups) * KB;
+  const cpx<T>* Wp = W + p * zl::F;
+  const bool xwave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6) < 11;
+  const T sc = (T)zl::P;
+  for (int kk = 0; kk < KB; ++kk) {
+    const int k = k0 + kk;
+    if (k >= K) break;   // uniform
+    const int tid = fresh((int)threadIdx.x);
+    const int wave = tid >> 6, lane = tid & 63;
+    const int l = min(lane / 11, 4);
+    const int s = lane - 11 * l;
+    const int sb = min(s, 10), sa = min(s, 9);
+    const int c = min(5 * wave + l, 55);
+    const int j = min(5 * wave + l, 54);
+    cpx<T>* Ey = sT + c;
+    cpx<T>* Ex = sT + 10 * min(wave, 10) * zl::RS + l * 110;
+    const int64_t sl = (p * K + k) * zl::P;
+    if (xwave) {
+      // ---- P4/P5: c = u - y of row pair j (layout A) -> x-R2C -> rows 2j, 2j+1 of T ----
+      const uint32_t po = (uint32_t)(j * 10 + fresh(sa)) * 16u;
+      cpx<T> zc[11];
+#pragma unroll
+      for (int n2 = 0; n2 < 11; ++n2) {
+        const V2 a = zld<V2>(A + sl, po + n2 * 550 * 16);
+        const T ux = soft_l(a.x, theta), uy = soft_l(a.y, theta);
+        zc[n2] = {ux - (a.x - ux), uy - (a.y - uy)};
+      }
+      const int s5 = fresh(sb);
+      cpx<T>* r0 = sT + 2 * j * zl::RS;
+      fwd_line<T, 1>(zc, Ex, s5, [&](int k1, cpx<T> val) { r0[k1 * 11 + s5] = val; });
+    }
+    lds_sync();
+    // ---- P7: column c, rows y = n1 + 10 n2: two-for-one separation ----
+    cpx<T> col[11];
+    {
+      const int n1 = fresh(sa);
+      const int zc1 = zslot(c), zc2 = zslot((c == 0) ? 0 : zl::X - c);
+      const bool odd = n1 & 1;
+#pragma unroll
+      for (int n2 = 0; n2 < 11; ++n2) {
+        const int y = mod110(11 * n1 + 10 * n2);
+        const cpx<T>* r0 = sT + (y >> 1) * (2 * zl::RS);
+        const cpx<T> z1 = r0[zc1], z2 = r0[zc2];
+        const T ex = (T)0.5 * (z1.x + z2.x), ey = (T)0.5 * (z1.y - z2.y);
+        const T ox = (T)0.5 * (z1.y + z2.y), oy = (T)-0.5 * (z1.x - z2.x);
+        col[n2] = {odd ? ox : ex, odd ? oy : ey};
+      }
+    }
+    lds_sync();
+    // ---- P9: y-R2C of column c -> bins (x' = c, y = elem_b(k2, k1)) + XY conj(dcorr) w ----
+    {
+      const int s9 = fresh(sb);
+      const cpx<T>* dk = dcorr + (int64_t)k * zl::F;
+      const uint32_t bo = (uint32_t)(c * 11 + s9) * 16u;
+      cpx<T>* out = dst + (p * K + k) * (int64_t)zl::F + c;
+      fwd_line<T, zl::RS>(col, Ey, s9, [&](int k1, cpx<T> cb) {
+        const cpx<T> q = cmulc(zld<cpx<T>>(dk, bo + k1 * 616 * 16), zld<cpx<T>>(Wp, bo + k1 * 616 * 16));
+        out[zl::elem_b(s9, k1) * zl::Xh] = {cb.x + sc * q.x, cb.y + sc * q.y};
+      });
+    }
+    lds_sync();   // the next slice's P5 rewrites the rows of T
+  }
+}
+
 // dst[b][bin_slot(f)] = src[b][f]  (complex spectra, `count` of them)
 template <typename T>
 __global__ void k_to_slots(const cpx<T>* __restrict__ src, cpx<T>* __restrict__ dst,
@@ -446,10 +528,25 @@ hipError_t launch_state_to_nat_inplace(T* a, int64_t count, hipStream_t st) {
 
 size_t zline_smem_bytes() { return zl::kSmem; }
 
+constexpr int kZhKB = 4;   // filter slices per workgroup of k_zhat_line
+
+template <typename T>
+hipError_t launch_zhat_line(const T* A, const cpx<T>* W, const cpx<T>* dcorr, cpx<T>* dst,
+                            int64_t npatch, int K, T theta, hipStream_t st) {
+  if (npatch <= 0) return hipSuccess;
+  const int kg = (K + kZhKB - 1) / kZhKB;
+  hipLaunchKernelGGL((k_zhat_line<T, kZhKB>), dim3((unsigned)(npatch * kg)), dim3(zl::NT),
+                     zl::kSmem, st, A, W, dcorr, dst, K, kg, theta);
+  return hipGetLastError();
+}
+
 template hipError_t launch_zline<double>(const double*, double*, const double*, const double*,
                                          cpx<double>*, const cpx<double>*, const cpx<double>*,
                                          const cpx<double>*, const double*, int64_t, int, double,
                                          int, hipStream_t, int, double*, double*);
+template hipError_t launch_zhat_line<double>(const double*, const cpx<double>*,
+                                             const cpx<double>*, cpx<double>*, int64_t, int,
+                                             double, hipStream_t);
 template hipError_t launch_to_slots<double>(const cpx<double>*, cpx<double>*, int64_t, hipStream_t);
 template hipError_t launch_to_slots_real<double>(const double*, double*, hipStream_t);
 template hipError_t launch_state_to_nat<double>(const double*, double*, int64_t, hipStream_t);
