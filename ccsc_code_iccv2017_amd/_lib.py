@@ -158,6 +158,10 @@ SIGNATURES = {
     "ccsc_solve": (C.c_int32, [C.c_void_p, C.POINTER(SolveProblem), C.POINTER(SolveInputs),
                                C.POINTER(SolveOutputs), C.POINTER(SolveLog), C.c_char_p,
                                C.c_size_t]),
+    "ccsc_local_cn": (C.c_int32, [C.c_void_p, _dp, _dp, C.c_int64, C.c_int32, C.c_int32,
+                                  C.c_char_p, C.c_size_t]),
+    "ccsc_local_cn_dev": (C.c_int32, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int32,
+                                      C.c_int32, C.c_char_p, C.c_size_t]),
     "ccsc_test_fft2d": (C.c_int32, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, _dp, _dp, _dp,
                                     C.c_char_p, C.c_size_t]),
 }

@@ -195,6 +195,12 @@ hipError_t launch_norms(const T* a, const T* b, int64_t count, T* part, T* out2,
 template <typename T>
 hipError_t launch_max(const T* a, int64_t count, T* part, T* out, hipStream_t st);
 
+// ---- localcn.hip: CreateImages.m:299-369 'local_cn' + ZERO_MEAN (:652-657) ---------
+// n column-major [H, W] fp64 images (device pointers), one workgroup per image.
+bool local_cn_ok(int H, int W);
+hipError_t launch_local_cn(const double* in, double* out, int64_t n, int H, int W,
+                           hipStream_t st);
+
 // ---- util.hip ---------------------------------------------------------------
 template <typename T>
 hipError_t launch_randn(T* out, int64_t count, uint64_t seed, uint64_t offset, hipStream_t st);

@@ -621,4 +621,40 @@ int32_t ccsc_solve(ccsc_ctx* ctx, const ccsc_solve_problem* p, const ccsc_solve_
   });
 }
 
+int32_t ccsc_local_cn_dev(ccsc_ctx* ctx, const double* in, double* out, int64_t n, int32_t H,
+                          int32_t W, char* err, size_t errlen) {
+  return guarded(err, errlen, [&] {
+    if (!ctx || !in || !out || n < 0) throw Err(CCSC_E_INVALID, "bad arguments");
+    if (!local_cn_ok(H, W))
+      throw Err(CCSC_E_UNSUPPORTED, "local_cn: images must be 7x7 .. 12288 pixels and fit the LDS");
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(launch_local_cn(in, out, n, H, W, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+  });
+}
+
+int32_t ccsc_local_cn(ccsc_ctx* ctx, const double* in, double* out, int64_t n, int32_t H,
+                      int32_t W, char* err, size_t errlen) {
+  return guarded(err, errlen, [&] {
+    if (!ctx || !in || !out || n < 0) throw Err(CCSC_E_INVALID, "bad arguments");
+    if (!local_cn_ok(H, W))
+      throw Err(CCSC_E_UNSUPPORTED, "local_cn: images must be 7x7 .. 12288 pixels and fit the LDS");
+    HIPCHK(hipSetDevice(ctx->device));
+    const int64_t per = (int64_t)H * W;
+    const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(n, (256LL << 20) / (per * 8)));
+    DevBuf a, b;
+    a.alloc((size_t)(chunk * per) * 8);
+    b.alloc(a.bytes);
+    for (int64_t i0 = 0; i0 < n; i0 += chunk) {
+      const int64_t m = std::min(chunk, n - i0);
+      HIPCHK(hipMemcpyAsync(a.p, in + i0 * per, (size_t)(m * per) * 8, hipMemcpyHostToDevice,
+                            ctx->stream));
+      HIPCHK(launch_local_cn(a.as<double>(), b.as<double>(), m, H, W, ctx->stream));
+      HIPCHK(hipMemcpyAsync(out + i0 * per, b.p, (size_t)(m * per) * 8, hipMemcpyDeviceToHost,
+                            ctx->stream));
+    }
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+  });
+}
+
 }  // extern "C"

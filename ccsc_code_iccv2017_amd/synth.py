@@ -12,8 +12,10 @@ tests use seeded synthetic data of the same shapes:
     reference, the normalised image is stored as single then widened to double
     (CreateImages.m:367, :711).
 
-PyTorch is used only as an array library here (CPU for tests, the GPU for the
-10^4-patch bench config); it is data preparation, not the learner.
+On a GPU the local contrast normalisation runs in libccsc's hand-written kernel
+(ccsc_local_cn_dev, csrc/localcn.hip: one workgroup per image, LDS-resident 13x13
+convolutions, radix-select median); the torch restatement below serves CPU tensors
+(tests, the CPU baseline).  PyTorch draws the synthetic codes and noise.
 """
 from __future__ import annotations
 
@@ -44,12 +46,36 @@ def rconv2(large: torch.Tensor, small: np.ndarray) -> torch.Tensor:
     return Fnn.conv2d(t, k[None, None])[:, 0]
 
 
+_CTX = {}
+
+
+def local_cn_gpu(imgs: torch.Tensor) -> torch.Tensor:
+    """local_cn on the GPU through the C-ABI (ccsc_local_cn_dev); imgs [n, H, W] on a
+    CUDA device.  No fallback: a missing libccsc raises."""
+    from . import _lib as L
+    from .learners import Context
+    n, H, W = imgs.shape
+    x = imgs.to(torch.float64).transpose(1, 2).contiguous()   # [n, W, H] = column-major [H, W]
+    out = torch.empty_like(x)
+    dev = imgs.device.index if imgs.device.index is not None else torch.cuda.current_device()
+    if dev not in _CTX:
+        _CTX[dev] = Context(dev)
+    torch.cuda.synchronize(imgs.device)
+    eb = L.errbuf()
+    L.check(L.lib().ccsc_local_cn_dev(_CTX[dev].ptr, x.data_ptr(), out.data_ptr(), n, H, W, eb,
+                                      len(eb)), eb)
+    return out.transpose(1, 2)
+
+
 def local_cn(imgs: torch.Tensor) -> torch.Tensor:
     """CreateImages.m:299-369 ('local_cn') then :652-657 (ZERO_MEAN) per image.
 
     imgs: [n, H, W] float64 (rows = MATLAB dim 1).  Returns float64 values that
-    went through the reference's single-precision storage.
+    went through the reference's single-precision storage.  CUDA tensors go through
+    the HIP kernel (local_cn_gpu); this torch restatement serves CPU tensors.
     """
+    if imgs.is_cuda:
+        return local_cn_gpu(imgs)
     k = fspecial_gaussian(13, 3 * 1.591)
     lmn = rconv2(imgs, k)
     lmnsq = rconv2(imgs * imgs, k)

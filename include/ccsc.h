@@ -300,6 +300,19 @@ int32_t ccsc_solve_supported(const ccsc_solve_problem* p, char* err, size_t errl
 int32_t ccsc_solve(ccsc_ctx* ctx, const ccsc_solve_problem* p, const ccsc_solve_inputs* in,
                    ccsc_solve_outputs* out, ccsc_solvelog* log, char* err, size_t errlen);
 
+/* ---- input preprocessing ----------------------------
+ * Local contrast normalisation of the learners' input images: the 'local_cn' and
+ * ZERO_MEAN branches of image_helpers/CreateImages.m:299-369, :652-657 (13x13 Gaussian,
+ * sigma 3*1.591, reflection padding of image_helpers/rconv2.m:22-58, std floored at
+ * its median, single-precision result), one GPU workgroup per image.
+ * in/out: n column-major [H, W] float64 images (out = double(single(...)), may alias in).
+ * ccsc_local_cn takes host arrays; ccsc_local_cn_dev device arrays on the context's
+ * device (e.g. torch tensors), ordered on the context's stream, synchronised on return. */
+int32_t ccsc_local_cn(ccsc_ctx* ctx, const double* in, double* out, int64_t n, int32_t H,
+                      int32_t W, char* err, size_t errlen);
+int32_t ccsc_local_cn_dev(ccsc_ctx* ctx, const double* in, double* out, int64_t n, int32_t H,
+                          int32_t W, char* err, size_t errlen);
+
 /* ---- kernel-level entry points (parity tests of single stages) ---------- */
 /* 2D R2C of `count` real slices [X,Y] -> half spectra [Y][X/2+1] (re,im). */
 int32_t ccsc_test_fft2d(ccsc_ctx* ctx, int32_t X, int32_t Y, int32_t count, const double* in,

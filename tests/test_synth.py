@@ -147,3 +147,32 @@ def test_images_2d_shape_layout_and_sharding():
     raw = synth.images_2d(2, size=(20, 20), K=4, psf=5, chunk=2, seed=11, local_cn_on=False)
     np.testing.assert_allclose(synth.local_cn(torch.as_tensor(np.moveaxis(raw, 2, 0)))
                                .numpy(), np.moveaxis(full[:, :, :2], 2, 0), rtol=0, atol=2e-7)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(100, 100), (17, 23), (24, 9)])
+def test_local_cn_gpu_kernel_matches_loop(shape):
+    """csrc/localcn.hip (through ccsc_local_cn_dev) == the loop restatement of
+    CreateImages.m:306-369 + :652-657; single-precision output, so agreement to the
+    float32 rounding of the last step (the mean's summation order is not MATLAB's)."""
+    rng = np.random.default_rng(5)
+    imgs = [rng.standard_normal(shape), np.ones(shape) * 3.0,            # constant: zero-median branch
+            np.where(rng.uniform(size=shape) < 0.7, 0.0, rng.standard_normal(shape))]
+    t = torch.as_tensor(np.stack(imgs), dtype=torch.float64, device="cuda")
+    got = synth.local_cn(t).cpu().numpy()
+    for i, im in enumerate(imgs):
+        ref = local_cn_loop(im)
+        np.testing.assert_allclose(got[i], ref, rtol=0, atol=2e-6 * max(1.0, np.abs(ref).max()))
+
+
+@pytest.mark.gpu
+def test_local_cn_host_entry_point(gpu_ctx):
+    """ccsc_local_cn (host arrays, column-major [H, W, n]) == the device entry point."""
+    from ccsc_code_iccv2017_amd import _lib as L
+    rng = np.random.default_rng(6)
+    b = np.asfortranarray(rng.standard_normal((30, 28, 5)))
+    out = np.zeros_like(b, order="F")
+    eb = L.errbuf()
+    L.check(L.lib().ccsc_local_cn(gpu_ctx.ptr, L.dptr(b), L.dptr(out), 5, 30, 28, eb, len(eb)), eb)
+    for i in range(5):
+        np.testing.assert_allclose(out[:, :, i], local_cn_loop(b[:, :, i]), rtol=0, atol=2e-6)
