@@ -46,9 +46,6 @@ def rconv2(large: torch.Tensor, small: np.ndarray) -> torch.Tensor:
     return Fnn.conv2d(t, k[None, None])[:, 0]
 
 
-_CTX = {}
-
-
 def local_cn_gpu(imgs: torch.Tensor) -> torch.Tensor:
     """local_cn on the GPU through the C-ABI (ccsc_local_cn_dev); imgs [n, H, W] on a
     CUDA device.  No fallback: a missing libccsc raises."""
@@ -58,12 +55,11 @@ def local_cn_gpu(imgs: torch.Tensor) -> torch.Tensor:
     x = imgs.to(torch.float64).transpose(1, 2).contiguous()   # [n, W, H] = column-major [H, W]
     out = torch.empty_like(x)
     dev = imgs.device.index if imgs.device.index is not None else torch.cuda.current_device()
-    if dev not in _CTX:
-        _CTX[dev] = Context(dev)
     torch.cuda.synchronize(imgs.device)
-    eb = L.errbuf()
-    L.check(L.lib().ccsc_local_cn_dev(_CTX[dev].ptr, x.data_ptr(), out.data_ptr(), n, H, W, eb,
-                                      len(eb)), eb)
+    with Context(dev) as ctx:   # one stream for this call (no context outlives it)
+        eb = L.errbuf()
+        L.check(L.lib().ccsc_local_cn_dev(ctx.ptr, x.data_ptr(), out.data_ptr(), n, H, W, eb,
+                                          len(eb)), eb)
     return out.transpose(1, 2)
 
 
