@@ -43,13 +43,10 @@ __device__ __forceinline__ T line_block_sum(T v, T* scratch) {
 // Row pass: 2L rows (L row pairs) of one slice per workgroup.  LDS rows of RS T.
 // ---------------------------------------------------------------------------
 template <typename T, int MODE>
-__global__ __launch_bounds__(kLineNT) void k_rows(RowArgs<T> a, RowGeom rg,
-                                              const cpx<T>* __restrict__ tw) {
-  extern __shared__ __align__(16) unsigned char smem_raw[];
-  T* lds = reinterpret_cast<T*>(smem_raw);
+__device__ __forceinline__ void rows_body(const RowArgs<T>& a, const RowGeom& rg,
+                                          const cpx<T>* __restrict__ tw, int64_t slice, T* lds) {
   Grid2D G = rg.G;
   const int X = G.X, Xh = G.Xh, RS = G.RS;
-  const int64_t slice = blockIdx.x;
   const int g = blockIdx.y;
   const int row0 = g * 2 * rg.L;
   const int nrows = min(2 * rg.L, rg.rows - row0);
@@ -198,15 +195,41 @@ __global__ __launch_bounds__(kLineNT) void k_rows(RowArgs<T> a, RowGeom rg,
   }
 }
 
+template <typename T, int MODE>
+__global__ __launch_bounds__(kLineNT) void k_rows(RowArgs<T> a, RowGeom rg,
+                                              const cpx<T>* __restrict__ tw) {
+  extern __shared__ __align__(16) unsigned char smem_raw[];
+  rows_body<T, MODE>(a, rg, tw, (int64_t)blockIdx.x, reinterpret_cast<T*>(smem_raw));
+}
+
+// One launch for both slice sets of an iteration: workgroups [0, nz) run the code
+// slices (MZ = kRowIterZ or kRowFinalZ) with args a, the rest the data slices
+// (kRowIterX) with args b -- the single-image data launch alone would leave the GPU
+// nearly idle for its whole latency.
+template <typename T, int MZ>
+__global__ __launch_bounds__(kLineNT) void k_rows_pair(RowArgs<T> a, RowArgs<T> b, int64_t nz,
+                                                   RowGeom rg, const cpx<T>* __restrict__ tw) {
+  extern __shared__ __align__(16) unsigned char smem_raw[];
+  T* lds = reinterpret_cast<T*>(smem_raw);
+  const int64_t s = blockIdx.x;
+  if (s < nz) rows_body<T, MZ>(a, rg, tw, s, lds);
+  else rows_body<T, kRowIterX>(b, rg, tw, s - nz, lds);
+}
+
 // ---------------------------------------------------------------------------
 // Column pass: TC consecutive x' columns of one line set, LDS [e][c] complex.
 // ---------------------------------------------------------------------------
 template <typename T, int SIGN>
-__global__ __launch_bounds__(kLineNT) void k_cols(cpx<T>* __restrict__ S, ColGeom cg,
+__global__ __launch_bounds__(kLineNT) void k_cols(cpx<T>* __restrict__ S, cpx<T>* __restrict__ S2,
+                                              int64_t n1, ColGeom cg,
                                               const cpx<T>* __restrict__ tw) {
   extern __shared__ __align__(16) unsigned char smem_raw[];
   T* lds = reinterpret_cast<T*>(smem_raw);
-  const int64_t o = blockIdx.x;
+  int64_t o = blockIdx.x;
+  if (o >= n1) {   // workgroups past the first set's n1 line sets run the second set
+    S = S2;
+    o -= n1;
+  }
   const int tile = blockIdx.y;
   const int TC = cg.TC, n = cg.n;
   const int c0 = tile * TC;
@@ -400,12 +423,29 @@ hipError_t launch_rows(int mode, const RowArgs<T>& a, int64_t nslices, const Row
 
 template <typename T>
 hipError_t launch_cols(cpx<T>* S, int sign, int64_t nouter, const ColGeom& cg, const cpx<T>* tw,
-                       hipStream_t st) {
-  if (nouter <= 0) return hipSuccess;
-  const dim3 grid((unsigned)nouter, (unsigned)cg.xtiles);
+                       hipStream_t st, cpx<T>* S2, int64_t nouter2) {
+  if (nouter + nouter2 <= 0) return hipSuccess;
+  const dim3 grid((unsigned)(nouter + nouter2), (unsigned)cg.xtiles);
   const size_t sm = cols_smem_bytes(cg, sizeof(T));
-  if (sign < 0) hipLaunchKernelGGL((k_cols<T, -1>), grid, dim3(kLineNT), sm, st, S, cg, tw);
-  else hipLaunchKernelGGL((k_cols<T, +1>), grid, dim3(kLineNT), sm, st, S, cg, tw);
+  if (sign < 0)
+    hipLaunchKernelGGL((k_cols<T, -1>), grid, dim3(kLineNT), sm, st, S, S2, nouter, cg, tw);
+  else
+    hipLaunchKernelGGL((k_cols<T, +1>), grid, dim3(kLineNT), sm, st, S, S2, nouter, cg, tw);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_rows_pair(int code_mode, const RowArgs<T>& a, int64_t nz, const RowArgs<T>& b,
+                            int64_t nx, const RowGeom& rg, const cpx<T>* tw, hipStream_t st) {
+  if (nz + nx <= 0) return hipSuccess;
+  const dim3 grid((unsigned)(nz + nx), (unsigned)rg.groups);
+  const size_t sm = rows_smem_bytes(rg, sizeof(T));
+  if (code_mode == kRowIterZ)
+    hipLaunchKernelGGL((k_rows_pair<T, kRowIterZ>), grid, dim3(kLineNT), sm, st, a, b, nz, rg, tw);
+  else if (code_mode == kRowFinalZ)
+    hipLaunchKernelGGL((k_rows_pair<T, kRowFinalZ>), grid, dim3(kLineNT), sm, st, a, b, nz, rg, tw);
+  else
+    return hipErrorInvalidValue;
   return hipGetLastError();
 }
 
@@ -470,7 +510,10 @@ hipError_t launch_reduce_parts(const T* part, T* out, int64_t n, int per_img, in
 template hipError_t launch_rows<double>(int, const RowArgs<double>&, int64_t, const RowGeom&,
                                         const cpx<double>*, hipStream_t);
 template hipError_t launch_cols<double>(cpx<double>*, int, int64_t, const ColGeom&,
-                                        const cpx<double>*, hipStream_t);
+                                        const cpx<double>*, hipStream_t, cpx<double>*, int64_t);
+template hipError_t launch_rows_pair<double>(int, const RowArgs<double>&, int64_t,
+                                             const RowArgs<double>&, int64_t, const RowGeom&,
+                                             const cpx<double>*, hipStream_t);
 template hipError_t launch_solve_sm<double>(cpx<double>*, cpx<double>*, const cpx<double>*,
                                             const double*, double, double, int, int, int64_t, int,
                                             int, int, int, hipStream_t);

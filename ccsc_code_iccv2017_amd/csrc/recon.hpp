@@ -94,9 +94,14 @@ size_t cols_smem_bytes(const ColGeom& cg, size_t tsize);
 template <typename T>
 hipError_t launch_rows(int mode, const RowArgs<T>& a, int64_t nslices, const RowGeom& rg,
                        const cpx<T>* tw, hipStream_t st);
+// code slices (a, code_mode kRowIterZ / kRowFinalZ) and data slices (b, kRowIterX) in one launch
+template <typename T>
+hipError_t launch_rows_pair(int code_mode, const RowArgs<T>& a, int64_t nz, const RowArgs<T>& b,
+                            int64_t nx, const RowGeom& rg, const cpx<T>* tw, hipStream_t st);
+// nouter line sets of S, then (optionally) nouter2 of S2, in one launch
 template <typename T>
 hipError_t launch_cols(cpx<T>* S, int sign, int64_t nouter, const ColGeom& cg, const cpx<T>* tw,
-                       hipStream_t st);
+                       hipStream_t st, cpx<T>* S2 = nullptr, int64_t nouter2 = 0);
 
 // Sherman-Morrison z-solve of SI / SP per (image, bin), in place:
 //   xi2 [n][K][F] -> zhat * invP, xi1 [n][F] -> sum_k dhat_k zhat_k (the next v1);

@@ -295,6 +295,19 @@ struct Solver {
     }
   }
 
+  // both spectrum sets (codes, data) in one launch per line direction
+  void cols2(int sign, int64_t nz, int64_t nx) {
+    cpx<double>* a = Sz.as<cpx<double>>();
+    cpx<double>* b = Sx.as<cpx<double>>();
+    if (sign < 0) {
+      HIPCHK(launch_cols<double>(a, -1, nz * S.Tn, S.cy, tw(tw_y), st, b, nx * S.Tn));
+      if (S.nd == 3) HIPCHK(launch_cols<double>(a, -1, nz * S.Y, S.ct, tw(tw_t), st, b, nx * S.Y));
+    } else {
+      if (S.nd == 3) HIPCHK(launch_cols<double>(a, +1, nz * S.Y, S.ct, tw(tw_t), st, b, nx * S.Y));
+      HIPCHK(launch_cols<double>(a, +1, nz * S.Tn, S.cy, tw(tw_y), st, b, nx * S.Tn));
+    }
+  }
+
   void setup(const ccsc_solve_inputs& in) {
     const ccsc_solve_problem& p = S.p;
     if (!in.b || !in.kernels || !in.mask) throw Err(CCSC_E_INVALID, "b, kernels and mask are required");
@@ -506,9 +519,8 @@ struct Solver {
     int live = (int)n;
     for (int i = 0; i <= max_it && live > 0; ++i) {
       const bool last = i == max_it;
-      HIPCHK(launch_rows<double>(last ? kRowFinalZ : kRowIterZ, code_args(i == 0), nz, S.rg,
-                                 tw(tw_r), st));
-      HIPCHK(launch_rows<double>(kRowIterX, data_args(i == 0), nx, S.rg, tw(tw_r), st));
+      HIPCHK(launch_rows_pair<double>(last ? kRowFinalZ : kRowIterZ, code_args(i == 0), nz,
+                                      data_args(i == 0), nx, S.rg, tw(tw_r), st));
       if (need_sums) {
         HIPCHK(launch_reduce_parts<double>(part.as<double>(), sums.as<double>(), n, S.Kc + S.W,
                                            S.rg.groups, st));
@@ -544,11 +556,9 @@ struct Solver {
         for (auto& it : iters) it = i;
       }
       if (last || live == 0) break;
-      cols(Sz.as<cpx<double>>(), -1, nz);
-      cols(Sx.as<cpx<double>>(), -1, nx);
+      cols2(-1, nz, nx);
       solve_bins();
-      cols(Sz.as<cpx<double>>(), +1, nz);
-      cols(Sx.as<cpx<double>>(), +1, nx);
+      cols2(+1, nz, nx);
     }
     HIPCHK(hipEventRecord(e1, st));
     HIPCHK(hipEventSynchronize(e1));
