@@ -121,12 +121,12 @@ static bool make_grid2d(int X, int Y, Grid2D& G, std::string& why) {
   G.F = G.Xh * Y;
   if (!plan1d(X, G.Yp / 2, G.px)) {
     why = "grid length " + std::to_string(X) +
-          " has no radix plan (factors 2,3,5,7,11 plus at most one prime <= 64, within the register budget)";
+          " has no radix plan (factors 2,3,5,7,11 plus at most one prime <= 127, within the register budget)";
     return false;
   }
   if (!plan1d(Y, G.Xh, G.py)) {
     why = "grid length " + std::to_string(Y) +
-          " has no radix plan (factors 2,3,5,7,11 plus at most one prime <= 64, within the register budget)";
+          " has no radix plan (factors 2,3,5,7,11 plus at most one prime <= 127, within the register budget)";
     return false;
   }
   // per-pass twiddle tables, x passes then y passes

@@ -197,9 +197,10 @@ struct Plan1D {
                         // generic-radix pass appends its R roots exp(-2 pi i m/R)
 };
 // Radices with an unrolled in-register butterfly; any other prime factor (up
-// to kMaxGenericRadix, e.g. 37 for the 74-point grids of the 3D/4D configs)
-// runs through fft_pass_generic.
-constexpr int kMaxGenericRadix = 64;
+// to kMaxGenericRadix, e.g. 37 for the 74-point grids of the 3D/4D configs, or a
+// prime grid length such as 71 = 61 + 2*5) runs through fft_pass_generic, within
+// one task per thread (generic_tasks, engine.cpp).
+constexpr int kMaxGenericRadix = 127;
 constexpr int kGenericQP = 3;      // conjugate output pairs per generic-pass task
 
 // Per-slice description of the 2D grid (all in units of T unless noted).

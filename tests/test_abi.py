@@ -81,7 +81,7 @@ def test_supported_reports_reasons(L):
     eb = L.errbuf()
     p = _problem(L, 1)
     assert L.lib().ccsc_supported(C.byref(p), eb, len(eb)) == 0
-    p = _problem(L, 1, sb=(100, 124))       # grid 110 x 134 = 2*67: prime 67 > kMaxGenericRadix
+    p = _problem(L, 1, sb=(100, 124))       # grid 110 x 134 = 2*67: the radix-67 pass exceeds one task per thread
     rc = L.lib().ccsc_supported(C.byref(p), eb, len(eb))
     assert rc == L.CCSC_E_UNSUPPORTED and b"radix" in eb.value
 

@@ -48,6 +48,8 @@ def _case(variant, sb, psf, K, n, ni, seed):
 @pytest.mark.parametrize("variant", ["dp", "dz"])
 @pytest.mark.parametrize("sb,psf,K,n,ni", [((12, 12), 5, 3, 4, 2), ((100, 100), 11, 4, 4, 2),
                                            ((11, 10), 5, 3, 6, 3),
+                                           # prime grid lengths (71 x 73: generic passes)
+                                           ((61, 63), 11, 3, 4, 2),
                                            # Woodbury D-factor (ni << K): K <= 64, K > 64, ni = 8
                                            ((12, 12), 5, 8, 4, 2), ((12, 12), 5, 70, 4, 2),
                                            ((12, 12), 5, 32, 16, 8),
