@@ -431,6 +431,9 @@ struct Session2D {
   enum { ZT_NONE, ZT_PREV, ZT_CUR };
   int zt = ZT_NONE;
   DevBuf twt, oacc, odz;   // 3D: t-FFT twiddles, objective scratch
+  int tsolve_tc = 0;       // 3D: x' columns per k_tsolve3 workgroup (0: three-kernel z-solve)
+  Grid2D gt2{};            //     its t plan (K * tsolve_tc lines) and twiddles
+  DevBuf twt2;
 
   // host-side log
   int outer_done = 0;
@@ -556,6 +559,25 @@ struct Session2D {
       HIPCHK(hipMemcpy(twt.p, twts.data(), twt.bytes, hipMemcpyHostToDevice));
       oacc.alloc((size_t)F * 16);
       odz.alloc((size_t)P * 8);
+      // fused t-FFT + z-solve (k_tsolve3): TC x' columns per workgroup, the widest that
+      // plans and fits the LDS (CCSC_TSOLVE3=0 keeps the three-kernel form)
+      const char* ev = std::getenv("CCSC_TSOLVE3");
+      const char* etc = std::getenv("CCSC_TSOLVE3_TC");
+      if (!(ev && ev[0] == '0')) {
+        std::string why2;
+        for (int tc : {4, 2, 1}) {
+          if (etc && std::atoi(etc) > 0 && tc != std::atoi(etc)) continue;
+          Grid2D Gt2{};
+          if (!make_gridt(Tn, K * tc, Gt2, why2)) continue;
+          if (tsolve3_smem_bytes(Gt2, K, tc, sizeof(double)) > 160 * 1024) continue;
+          tsolve_tc = tc;
+          gt2 = Gt2;
+          auto t2 = make_twiddles(gt2);
+          twt2.alloc(t2.size() * sizeof(cpx<double>));
+          HIPCHK(hipMemcpy(twt2.p, t2.data(), twt2.bytes, hipMemcpyHostToDevice));
+          break;
+        }
+      }
     }
     const size_t KP = (size_t)K * P;
     bdev.alloc(m.b);
@@ -725,10 +747,16 @@ struct Session2D {
       const auto* twtc = twt.as<cpx<double>>();
       HIPCHK(launch_plane_fwd<double>(1, z.as<double>(), yz.as<double>(), nullptr, 0, 0, 0, 0,
                                       theta, 1, r, C, np * K, Tn, twc, G, st));
-      HIPCHK(launch_tfft<double>(C, C, np * K, G.Y, G.F, -1, twtc, g.Gt, st));
-      HIPCHK(launch_zsolve3<double>(C, Bhat.as<cpx<double>>(), dhat.as<cpx<double>>(),
-                                    sden.as<double>(), F, np, K, 1.0 / (double)P, st));
-      HIPCHK(launch_tfft<double>(C, C, np * K, G.Y, G.F, +1, twtc, g.Gt, st));
+      if (tsolve_tc) {
+        HIPCHK(launch_tsolve3<double>(C, Bhat.as<cpx<double>>(), dhat.as<cpx<double>>(),
+                                      sden.as<double>(), np, K, G.Y, G.Xh, G.F, tsolve_tc,
+                                      1.0 / (double)P, twt2.as<cpx<double>>(), gt2, st));
+      } else {
+        HIPCHK(launch_tfft<double>(C, C, np * K, G.Y, G.F, -1, twtc, g.Gt, st));
+        HIPCHK(launch_zsolve3<double>(C, Bhat.as<cpx<double>>(), dhat.as<cpx<double>>(),
+                                      sden.as<double>(), F, np, K, 1.0 / (double)P, st));
+        HIPCHK(launch_tfft<double>(C, C, np * K, G.Y, G.F, +1, twtc, g.Gt, st));
+      }
       HIPCHK(launch_plane_inv<double>(1, C, z.as<double>(), nullptr, nullptr,
                                       tol_on ? znorm.as<double>() : nullptr, 0, 1.0, r, np * K,
                                       Tn, twc, G, st));

@@ -145,6 +145,13 @@ template <typename T>
 hipError_t launch_plane_inv(int mode, const cpx<T>* src, T* dst, const T* yv, T* supp, T* norms,
                             int64_t nfirst, T scale, int r, int64_t nslices, int Tn,
                             const cpx<T>* tw, const Grid2D& G, hipStream_t stream);
+// fused t-FFT + z-solve + inverse t-FFT over (patch, y, TC x' columns) tiles; Gt2 plans
+// the t lines of K * TC columns (make_gridt with Xh = K * TC)
+size_t tsolve3_smem_bytes(const Grid2D& Gt2, int K, int TC, size_t tsize);
+template <typename T>
+hipError_t launch_tsolve3(cpx<T>* C, const cpx<T>* Bhat, const cpx<T>* dhat, const T* sden,
+                          int64_t npatch, int K, int Yn, int Xh, int F2, int TC, T invP3,
+                          const cpx<T>* tw, const Grid2D& Gt2, hipStream_t stream);
 template <typename T>
 hipError_t launch_zsolve3(cpx<T>* C, const cpx<T>* Bhat, const cpx<T>* dhat, const T* sden,
                           int64_t F3, int64_t npatch, int K, T invP3, hipStream_t stream);

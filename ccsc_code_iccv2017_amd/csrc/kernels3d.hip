@@ -173,6 +173,72 @@ __global__ void k_zsolve3(cpx<T>* __restrict__ C, const cpx<T>* __restrict__ Bha
   }
 }
 
+// ---- fused t-FFT + z-solve + inverse t-FFT (replaces k_tfft(-1), k_zsolve3,
+// k_tfft(+1) of the 3D z-step): one workgroup per (patch p, y row, tile of TC x'
+// columns) holds the K filters' T x TC plane-spectrum columns in LDS, layout
+// [t][k*TC + c] (K*TC complex lines of length T), so the spectra cross HBM once
+// each way per z-iteration instead of three times (L3:172-178, the closed form of
+// k_zsolve3).  Gt2: the t plan for K*TC lines.  Neighbouring x' tiles of one row are
+// consecutive workgroups (their 16*TC-byte column segments share cache lines).
+template <typename T>
+__global__ __launch_bounds__(kNT) void k_tsolve3(cpx<T>* __restrict__ C,
+                                                 const cpx<T>* __restrict__ Bhat,
+                                                 const cpx<T>* __restrict__ dhat,
+                                                 const T* __restrict__ sden, int K, int Yn,
+                                                 int Xh, int F2, int TC, int xtiles, T invP3,
+                                                 const cpx<T>* __restrict__ twg, Grid2D Gt) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  cpx<T>* s_tw = reinterpret_cast<cpx<T>*>(smem);
+  T* lds = reinterpret_cast<T*>(s_tw + Gt.ntw);
+  for (int i = threadIdx.x; i < Gt.ntw; i += kNT) s_tw[i] = twg[i];
+  const int tile = blockIdx.x % xtiles;
+  const int64_t rest = blockIdx.x / xtiles;
+  const int y = (int)(rest % Yn);
+  const int64_t p = rest / Yn;
+  const int Tn = Gt.Y;
+  const int x0 = tile * TC;
+  const int nc = min(TC, Xh - x0);
+  const int NL = K * TC;
+  const int64_t F3 = (int64_t)F2 * Tn;
+  const int64_t colbase = (int64_t)y * Xh + x0;
+  cpx<T>* Cp = C + p * K * F3;
+  for (int i = threadIdx.x; i < K * Tn * TC; i += kNT) {
+    const int c = i % TC;
+    const int r = i / TC;
+    const int t = r % Tn, k = r / Tn;
+    cpx<T> v = {(T)0, (T)0};
+    if (c < nc) v = Cp[(int64_t)k * F3 + (int64_t)t * F2 + colbase + c];
+    lds_cpx_store(lds + 2 * (t * NL + k * TC + c), 1, v);
+  }
+  lds_sync();
+  const LineGeom g = {NL, 2, 2 * NL, 1};
+  fft_dir<T, kMaxB, -1>(lds, kModePlain, g, g, Gt, Gt.py, s_tw);
+  // per bin (t, c): w = (B - sum_k d_k C_k) sden, C_k <- C_k / P3 + conj(d_k) w
+  for (int b = threadIdx.x; b < Tn * TC; b += kNT) {
+    const int t = b / TC, c = b - (b / TC) * TC;
+    if (c >= nc) continue;
+    const int64_t f3 = (int64_t)t * F2 + colbase + c;
+    T* row = lds + 2 * (t * NL + c);
+    cpx<T> acc = {(T)0, (T)0};
+    for (int k = 0; k < K; ++k)
+      acc = cadd(acc, cmul(dhat[(int64_t)k * F3 + f3], lds_cpx(row + 2 * k * TC, 1)));
+    const cpx<T> w = cscale(csub(Bhat[p * F3 + f3], acc), sden[f3]);
+    for (int k = 0; k < K; ++k) {
+      const cpx<T> d = dhat[(int64_t)k * F3 + f3];
+      const cpx<T> cv = lds_cpx(row + 2 * k * TC, 1);
+      lds_cpx_store(row + 2 * k * TC, 1, cadd(cscale(cv, invP3), cmulc(d, w)));
+    }
+  }
+  lds_sync();
+  fft_dir<T, kMaxB, +1>(lds, kModePlain, g, g, Gt, Gt.py, s_tw);
+  for (int i = threadIdx.x; i < K * Tn * TC; i += kNT) {
+    const int c = i % TC;
+    const int r = i / TC;
+    const int t = r % Tn, k = r / Tn;
+    if (c < nc) Cp[(int64_t)k * F3 + (int64_t)t * F2 + colbase + c] = lds_cpx(lds + 2 * (t * NL + k * TC + c), 1);
+  }
+}
+
 // ---- objective helper: acc[p][f] = sum_k Zhat[p][k][f] d[k][f] --------------
 template <typename T>
 __global__ void k_corr_sum(const cpx<T>* __restrict__ Zh, const cpx<T>* __restrict__ dhat,
@@ -243,6 +309,23 @@ hipError_t launch_tfft(const cpx<T>* src, cpx<T>* dst, int64_t nslices, int Yn, 
   return hipGetLastError();
 }
 
+size_t tsolve3_smem_bytes(const Grid2D& Gt2, int K, int TC, size_t tsize) {
+  return (size_t)Gt2.ntw * 2 * tsize + (size_t)Gt2.Y * K * TC * 2 * tsize;
+}
+
+template <typename T>
+hipError_t launch_tsolve3(cpx<T>* C, const cpx<T>* Bhat, const cpx<T>* dhat, const T* sden,
+                          int64_t npatch, int K, int Yn, int Xh, int F2, int TC, T invP3,
+                          const cpx<T>* tw, const Grid2D& Gt2, hipStream_t stream) {
+  if (npatch <= 0) return hipSuccess;
+  if (Gt2.Xh != K * TC) return hipErrorInvalidValue;   // the plan's line count
+  const int xtiles = (Xh + TC - 1) / TC;
+  const dim3 grid((unsigned)(npatch * Yn * xtiles));
+  hipLaunchKernelGGL(k_tsolve3<T>, grid, dim3(kNT), tsolve3_smem_bytes(Gt2, K, TC, sizeof(T)),
+                     stream, C, Bhat, dhat, sden, K, Yn, Xh, F2, TC, xtiles, invP3, tw, Gt2);
+  return hipGetLastError();
+}
+
 template <typename T>
 hipError_t launch_plane_inv(int mode, const cpx<T>* src, T* dst, const T* yv, T* supp, T* norms,
                             int64_t nfirst, T scale, int r, int64_t nslices, int Tn,
@@ -287,6 +370,10 @@ template hipError_t launch_tfft<double>(const cpx<double>*, cpx<double>*, int64_
 template hipError_t launch_plane_inv<double>(int, const cpx<double>*, double*, const double*,
                                              double*, double*, int64_t, double, int, int64_t, int,
                                              const cpx<double>*, const Grid2D&, hipStream_t);
+template hipError_t launch_tsolve3<double>(cpx<double>*, const cpx<double>*,
+                                           const cpx<double>*, const double*, int64_t, int, int,
+                                           int, int, int, double, const cpx<double>*,
+                                           const Grid2D&, hipStream_t);
 template hipError_t launch_zsolve3<double>(cpx<double>*, const cpx<double>*, const cpx<double>*,
                                            const double*, int64_t, int64_t, int, double,
                                            hipStream_t);
