@@ -568,7 +568,7 @@ struct Session2D {
         for (int tc : {4, 2, 1}) {
           if (etc && std::atoi(etc) > 0 && tc != std::atoi(etc)) continue;
           Grid2D Gt2{};
-          if (!make_gridt(Tn, K * tc, Gt2, why2)) continue;
+          if (!tsolve3_ok(Tn, K, tc) || !make_gridt(Tn, K * tc, Gt2, why2)) continue;
           if (tsolve3_smem_bytes(Gt2, K, tc, sizeof(double)) > 160 * 1024) continue;
           tsolve_tc = tc;
           gt2 = Gt2;

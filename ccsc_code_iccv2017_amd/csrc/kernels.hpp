@@ -147,6 +147,7 @@ hipError_t launch_plane_inv(int mode, const cpx<T>* src, T* dst, const T* yv, T*
                             const cpx<T>* tw, const Grid2D& G, hipStream_t stream);
 // fused t-FFT + z-solve + inverse t-FFT over (patch, y, TC x' columns) tiles; Gt2 plans
 // the t lines of K * TC columns (make_gridt with Xh = K * TC)
+bool tsolve3_ok(int Tn, int K, int TC);
 size_t tsolve3_smem_bytes(const Grid2D& Gt2, int K, int TC, size_t tsize);
 template <typename T>
 hipError_t launch_tsolve3(cpx<T>* C, const cpx<T>* Bhat, const cpx<T>* dhat, const T* sden,

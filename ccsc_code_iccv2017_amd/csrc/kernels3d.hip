@@ -180,6 +180,8 @@ __global__ void k_zsolve3(cpx<T>* __restrict__ C, const cpx<T>* __restrict__ Bha
 // each way per z-iteration instead of three times (L3:172-178, the closed form of
 // k_zsolve3).  Gt2: the t plan for K*TC lines.  Neighbouring x' tiles of one row are
 // consecutive workgroups (their 16*TC-byte column segments share cache lines).
+constexpr int kTsKmax = 16;   // k values per thread of k_tsolve3's solve phase
+
 template <typename T>
 __global__ __launch_bounds__(kNT) void k_tsolve3(cpx<T>* __restrict__ C,
                                                  const cpx<T>* __restrict__ Bhat,
@@ -213,20 +215,43 @@ __global__ __launch_bounds__(kNT) void k_tsolve3(cpx<T>* __restrict__ C,
   lds_sync();
   const LineGeom g = {NL, 2, 2 * NL, 1};
   fft_dir<T, kMaxB, -1>(lds, kModePlain, g, g, Gt, Gt.py, s_tw);
-  // per bin (t, c): w = (B - sum_k d_k C_k) sden, C_k <- C_k / P3 + conj(d_k) w
-  for (int b = threadIdx.x; b < Tn * TC; b += kNT) {
-    const int t = b / TC, c = b - (b / TC) * TC;
-    if (c >= nc) continue;
-    const int64_t f3 = (int64_t)t * F2 + colbase + c;
-    T* row = lds + 2 * (t * NL + c);
-    cpx<T> acc = {(T)0, (T)0};
-    for (int k = 0; k < K; ++k)
-      acc = cadd(acc, cmul(dhat[(int64_t)k * F3 + f3], lds_cpx(row + 2 * k * TC, 1)));
-    const cpx<T> w = cscale(csub(Bhat[p * F3 + f3], acc), sden[f3]);
-    for (int k = 0; k < K; ++k) {
-      const cpx<T> d = dhat[(int64_t)k * F3 + f3];
-      const cpx<T> cv = lds_cpx(row + 2 * k * TC, 1);
-      lds_cpx_store(row + 2 * k * TC, 1, cadd(cscale(cv, invP3), cmulc(d, w)));
+  // per bin (t, c): w = (B - sum_k d_k C_k) sden, C_k <- C_k / P3 + conj(d_k) w.
+  // G = kNT / (T TC) threads per bin split the k range (their d_k stay in registers
+  // between the two sweeps); partial sums meet in LDS past the spectra.
+  const int nb = Tn * TC;
+  const int G = max(1, kNT / nb);
+  const int kg = (K + G - 1) / G;
+  cpx<T>* part = reinterpret_cast<cpx<T>*>(lds + 2 * (size_t)Tn * NL);   // [G][nb]
+  const int b = threadIdx.x % nb, grp = threadIdx.x / nb;
+  const int t = b / TC, c = b - t * TC;
+  const bool on = grp < G && c < nc;
+  const int64_t f3 = (int64_t)t * F2 + colbase + c;
+  T* row = lds + 2 * (t * NL + c);
+  cpx<T> dv[kTsKmax];
+  cpx<T> acc = {(T)0, (T)0};
+#pragma unroll
+  for (int j = 0; j < kTsKmax; ++j) {
+    const int k = grp * kg + j;
+    dv[j] = (on && j < kg && k < K) ? dhat[(int64_t)k * F3 + f3] : cpx<T>{(T)0, (T)0};
+  }
+#pragma unroll
+  for (int j = 0; j < kTsKmax; ++j) {
+    const int k = grp * kg + j;
+    if (on && j < kg && k < K) acc = cadd(acc, cmul(dv[j], lds_cpx(row + 2 * k * TC, 1)));
+  }
+  if (grp < G) part[grp * nb + b] = acc;
+  lds_sync();
+  if (on) {
+    cpx<T> tot = {(T)0, (T)0};
+    for (int q = 0; q < G; ++q) tot = cadd(tot, part[q * nb + b]);
+    const cpx<T> w = cscale(csub(Bhat[p * F3 + f3], tot), sden[f3]);
+#pragma unroll
+    for (int j = 0; j < kTsKmax; ++j) {
+      const int k = grp * kg + j;
+      if (j < kg && k < K) {
+        const cpx<T> cv = lds_cpx(row + 2 * k * TC, 1);
+        lds_cpx_store(row + 2 * k * TC, 1, cadd(cscale(cv, invP3), cmulc(dv[j], w)));
+      }
     }
   }
   lds_sync();
@@ -309,8 +334,18 @@ hipError_t launch_tfft(const cpx<T>* src, cpx<T>* dst, int64_t nslices, int Yn, 
   return hipGetLastError();
 }
 
+bool tsolve3_ok(int Tn, int K, int TC) {
+  const int nb = Tn * TC;
+  if (nb > kNT) return false;
+  const int G = std::max(1, kNT / nb);
+  return (K + G - 1) / G <= kTsKmax;
+}
+
 size_t tsolve3_smem_bytes(const Grid2D& Gt2, int K, int TC, size_t tsize) {
-  return (size_t)Gt2.ntw * 2 * tsize + (size_t)Gt2.Y * K * TC * 2 * tsize;
+  const int nb = Gt2.Y * TC;
+  const int G = std::max(1, kNT / nb);
+  return (size_t)Gt2.ntw * 2 * tsize + (size_t)Gt2.Y * K * TC * 2 * tsize +
+         (size_t)G * nb * 2 * tsize;   // + the solve's partial sums
 }
 
 template <typename T>
@@ -319,6 +354,7 @@ hipError_t launch_tsolve3(cpx<T>* C, const cpx<T>* Bhat, const cpx<T>* dhat, con
                           const cpx<T>* tw, const Grid2D& Gt2, hipStream_t stream) {
   if (npatch <= 0) return hipSuccess;
   if (Gt2.Xh != K * TC) return hipErrorInvalidValue;   // the plan's line count
+  if (!tsolve3_ok(Gt2.Y, K, TC)) return hipErrorInvalidValue;   // <= kTsKmax k per thread
   const int xtiles = (Xh + TC - 1) / TC;
   const dim3 grid((unsigned)(npatch * Yn * xtiles));
   hipLaunchKernelGGL(k_tsolve3<T>, grid, dim3(kNT), tsolve3_smem_bytes(Gt2, K, TC, sizeof(T)),
