@@ -559,13 +559,14 @@ struct Session2D {
       HIPCHK(hipMemcpy(twt.p, twts.data(), twt.bytes, hipMemcpyHostToDevice));
       oacc.alloc((size_t)F * 16);
       odz.alloc((size_t)P * 8);
-      // fused t-FFT + z-solve (k_tsolve3): TC x' columns per workgroup, the widest that
-      // plans and fits the LDS (CCSC_TSOLVE3=0 keeps the three-kernel form)
+      // fused t-FFT + z-solve (k_tsolve3): TC x' columns per workgroup; C4 (74x74x42,
+      // K = 49) measured 0.432 s per outer iteration at TC = 2, 0.456 at TC = 4 and with
+      // the three-kernel form (CCSC_TSOLVE3=0), 0.587 at TC = 1
       const char* ev = std::getenv("CCSC_TSOLVE3");
       const char* etc = std::getenv("CCSC_TSOLVE3_TC");
       if (!(ev && ev[0] == '0')) {
         std::string why2;
-        for (int tc : {4, 2, 1}) {
+        for (int tc : {2, 4, 1}) {
           if (etc && std::atoi(etc) > 0 && tc != std::atoi(etc)) continue;
           Grid2D Gt2{};
           if (!tsolve3_ok(Tn, K, tc) || !make_gridt(Tn, K * tc, Gt2, why2)) continue;
