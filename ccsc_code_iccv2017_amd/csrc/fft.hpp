@@ -445,14 +445,14 @@ __device__ __forceinline__ void fft_pass_generic(T* lds, int R, int mode, const 
   lds_sync();
 }
 
-template <typename T, int MAXB, int SIGN, int NT = kNT, int GT = 1>
+template <typename T, int MAXB, int SIGN, int NT = kNT, int GT = 1, int BS = 1>
 __device__ __forceinline__ void fft_pass_dispatch(int R, T* lds, int mode, const LineGeom& gin,
                                                   const LineGeom& gout, const Grid2D& G, int n,
                                                   int Ns, const cpx<T>* tw) {
   switch (R) {
 #define CCSC_NATIVE_PASS(RR)                                                                   \
     case RR:                                                                                   \
-      fft_pass<T, RR, maxb_for_radix(RR), SIGN, NT>(lds, mode, gin, gout, G, n, Ns, tw);       \
+      fft_pass<T, RR, maxb_for_radix(RR) * BS, SIGN, NT>(lds, mode, gin, gout, G, n, Ns, tw);  \
       break;
     CCSC_NATIVE_PASS(2)
     CCSC_NATIVE_PASS(3)
@@ -475,7 +475,8 @@ __device__ __forceinline__ void fft_pass_dispatch(int R, T* lds, int mode, const
 // the fused kernels) LICM would otherwise hoist every pass's loop-invariant
 // index math out of the loop and keep it live in registers (256 VGPRs + 5 KB
 // of scratch per lane).
-template <typename T, int MAXB, int SIGN, int NSLOT = kMaxPass, int NT = kNT, int GT = 1>
+template <typename T, int MAXB, int SIGN, int NSLOT = kMaxPass, int NT = kNT, int GT = 1,
+          int BS = 1>
 __device__ __forceinline__ void fft_dir(T* lds, int mode0, const LineGeom& gfirst,
                                         const LineGeom& g, const Grid2D& G, const Plan1D& p,
                                         const cpx<T>* tw) {
@@ -489,9 +490,9 @@ __device__ __forceinline__ void fft_dir(T* lds, int mode0, const LineGeom& gfirs
       const int R = p.rad[s];
       const cpx<T>* tws = tw + p.twoff[s];
       if constexpr (s == 0)
-        fft_pass_dispatch<T, MAXB, SIGN, NT, GT>(R, lds, mode0, gfirst, g, G, n, Ns, tws);
+        fft_pass_dispatch<T, MAXB, SIGN, NT, GT, BS>(R, lds, mode0, gfirst, g, G, n, Ns, tws);
       else
-        fft_pass_dispatch<T, MAXB, SIGN, NT, GT>(R, lds, kModePlain, g, g, G, n, Ns, tws);
+        fft_pass_dispatch<T, MAXB, SIGN, NT, GT, BS>(R, lds, kModePlain, g, g, G, n, Ns, tws);
       Ns *= R;
     }
   });

@@ -75,7 +75,7 @@ struct DevBuf {
     bytes = b;
   }
   void release() {
-    if (p) hipFree(p);
+    if (p) (void)hipFree(p);
     p = nullptr;
     bytes = 0;
   }

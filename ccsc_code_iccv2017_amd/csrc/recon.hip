@@ -80,7 +80,7 @@ __device__ __forceinline__ void rows_body(const RowArgs<T>& a, const RowGeom& rg
       lds[ry * RS + 2 * xp + 1] = c.y;
     }
     lds_sync();
-    fft_dir<T, kMaxB, +1, kPlanSlots, kLineNT, kLineGT>(lds, kModeHermPair, gx, gx, G, G.px, s_tw);
+    fft_dir<T, kMaxB, +1, kPlanSlots, kLineNT, kLineGT, kLineBS>(lds, kModeHermPair, gx, gx, G, G.px, s_tw);
   }
   lds_sync();
 
@@ -178,7 +178,7 @@ __device__ __forceinline__ void rows_body(const RowArgs<T>& a, const RowGeom& rg
   if (G.Yp != nrows)
     for (int x = threadIdx.x; x < X; x += kLineNT) lds[nrows * RS + x] = (T)0;
   lds_sync();
-  fft_dir<T, kMaxB, -1, kPlanSlots, kLineNT, kLineGT>(lds, kModePlain, gx, gx, G, G.px, s_tw);
+  fft_dir<T, kMaxB, -1, kPlanSlots, kLineNT, kLineGT, kLineBS>(lds, kModePlain, gx, gx, G, G.px, s_tw);
   lds_sync();
   const int np = G.Yp / 2;
   for (int i = threadIdx.x; i < np * Xh; i += kLineNT) {
@@ -247,7 +247,7 @@ __global__ __launch_bounds__(kLineNT) void k_cols(cpx<T>* __restrict__ S, cpx<T>
   const LineGeom g = {TC, 2, 2 * TC, 1};
   Grid2D Gd{};
   lds_sync();
-  fft_dir<T, kMaxB, SIGN, kPlanSlots, kLineNT, kLineGT>(lds, kModePlain, g, g, Gd, cg.p, s_tw);
+  fft_dir<T, kMaxB, SIGN, kPlanSlots, kLineNT, kLineGT, kLineBS>(lds, kModePlain, g, g, Gd, cg.p, s_tw);
   lds_sync();
   for (int i = threadIdx.x; i < n * TC; i += kLineNT) {
     const int e = i / TC, c = i - e * TC;

@@ -65,7 +65,7 @@ static bool plan_line(int n, int nlines, Plan1D& out) {
     if ((int)cur.size() >= kPlanSlots || (int)cur.size() + 1 > best_np) return;
     for (int R : kNativeRad) {
       if (rem % R) continue;
-      if ((int64_t)(n / R) * nlines > (int64_t)maxb_for_radix(R) * kLineNT) continue;
+      if ((int64_t)(n / R) * nlines > (int64_t)maxb_for_radix(R) * kLineBS * kLineNT) continue;
       cur.push_back(R);
       dfs(rem / R, ng);
       cur.pop_back();
@@ -105,7 +105,11 @@ static void add_twiddles(Plan1D& p, std::vector<cpx<double>>& t) {
   }
 }
 
-constexpr size_t kLineLds = 40 * 1024;   // four or more workgroups per CU
+// LDS budget of one line-kernel workgroup (four or more per CU); CCSC_LINE_LDS_KB overrides
+static size_t line_lds() {
+  const char* e = std::getenv("CCSC_LINE_LDS_KB");
+  return (e && std::atoi(e) > 0) ? (size_t)std::atoi(e) * 1024 : (size_t)40 * 1024;
+}
 
 static int twiddle_count(const Plan1D& p) {
   int n = 0, Ns = 1;
@@ -128,7 +132,7 @@ static bool plan_rows(int X, int rows, RowGeom& rg) {
     rg.L = L;
     if (!plan_line(X, L, G.px)) continue;
     rg.ntw = twiddle_count(G.px);
-    if (rows_smem_bytes(rg, sizeof(double)) > kLineLds) continue;
+    if (rows_smem_bytes(rg, sizeof(double)) > line_lds()) continue;
     rg.groups = (rows + 2 * L - 1) / (2 * L);
     return true;
   }
@@ -143,7 +147,7 @@ static bool plan_cols(int n, int Xh, ColGeom& cg) {
     cg.TC = TC;
     if (!plan_line(n, TC, cg.p)) continue;
     cg.ntw = twiddle_count(cg.p);
-    if (cols_smem_bytes(cg, sizeof(double)) > kLineLds) continue;
+    if (cols_smem_bytes(cg, sizeof(double)) > line_lds()) continue;
     cg.xtiles = (Xh + TC - 1) / TC;
     return true;
   }
@@ -564,8 +568,8 @@ struct Solver {
     HIPCHK(hipEventSynchronize(e1));
     float ms = 0;
     HIPCHK(hipEventElapsedTime(&ms, e0, e1));
-    hipEventDestroy(e0);
-    hipEventDestroy(e1);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
     if (log) {
       if (log->iters)
         for (int64_t m = 0; m < n; ++m) log->iters[m] = iters[(size_t)m];
