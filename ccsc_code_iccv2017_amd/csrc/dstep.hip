@@ -10,6 +10,8 @@
 // complex); every d-iteration streams L_f once and does the two triangular
 // solves.  Only the half spectrum is solved: for real data S_{-f} = conj(S_f).
 #include "kernels.hpp"
+#include <algorithm>
+#include <cstdlib>
 
 namespace ccsc {
 
@@ -495,11 +497,23 @@ __global__ __launch_bounds__(256) void k_dsolve(const cpx<T>* __restrict__ L,
   }  // view groups
 }
 
+// A/B knob: CCSC_DS_LDS_KB reserves that much (unused) LDS per workgroup, capping the
+// workgroups per CU and so the factor bytes in flight between a (block, f)'s forward
+// and backward sweep (the reuse distance of the second read of L).
+static size_t dsolve_lds_bytes() {
+  static const size_t v = [] {
+    const char* e = std::getenv("CCSC_DS_LDS_KB");
+    const int kb = e ? std::atoi(e) : 0;
+    return (size_t)std::min(std::max(kb, 0), 160) * 1024;
+  }();
+  return v;
+}
+
 template <typename T, int RPL, int NVB>
 static void dsolve_go(dim3 grid, hipStream_t st, const cpx<T>* L, const cpx<T>* h,
                       const cpx<T>* Ch, cpx<T>* Dh, int F, int K, T rho, int fgroups, int NV) {
-  hipLaunchKernelGGL((k_dsolve<T, RPL, NVB>), grid, dim3(256), 0, st, L, h, Ch, Dh, F, K, rho,
-                     fgroups, NV);
+  hipLaunchKernelGGL((k_dsolve<T, RPL, NVB>), grid, dim3(256), dsolve_lds_bytes(), st, L, h, Ch,
+                     Dh, F, K, rho, fgroups, NV);
 }
 
 template <typename T>
