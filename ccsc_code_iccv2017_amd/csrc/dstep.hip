@@ -322,7 +322,10 @@ __device__ __forceinline__ cpx<T> shfl_c(cpx<T> v, int src) {
 // instead of NV times.  The factor's columns are read in blocks of kDsJB per
 // wave (one load batch per block, address-independent of the solve) so their
 // latency is paid once per block instead of once per column.
-constexpr int kDsJB = 8;
+#ifndef CCSC_DS_JB
+#define CCSC_DS_JB 8
+#endif
+constexpr int kDsJB = CCSC_DS_JB;
 #ifndef CCSC_DS_BWRED
 #define CCSC_DS_BWRED 0
 #endif

@@ -36,6 +36,9 @@ constexpr int kGcLD = kGcKP + 1;            // staged row stride (complex)
 constexpr int kGcTS = 17;                   // column stride (complex) of an LDS tile
 constexpr int kGcTSZ = 16 * kGcTS;          // complex per LDS tile
 constexpr int kGcHPT = 8;                   // right-hand-side entries of h per thread
+#ifndef CCSC_GC_RL
+#define CCSC_GC_RL 0
+#endif
 
 __device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
@@ -270,7 +273,27 @@ __global__ __launch_bounds__(kGcNT, 2) void k_gram_chol_mf(const cpx<double>* __
 #pragma unroll
       for (int c = 0; c < 16; ++c)
         x[c] = mine ? P[ti * kGcTSZ + c * kGcTS + row] : cpx<double>{1.0, 0.0};
-#ifndef CCSC_ABL_NOPOTRF
+#if !defined(CCSC_ABL_NOPOTRF) && CCSC_GC_RL
+      // right-looking in registers: once column c is final, every row r loses
+      // L[r][c] conj(L[c2][c]) from its column c2 > c, L[c2][c] broadcast from lane c2 by
+      // v_readlane -- no LDS round trip on the column-to-column chain; 1/sqrt of the
+      // pivot by v_rsq_f64 and two Newton steps instead of sqrt and a division
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        const double a = rdl(x[c].x, c);
+        double y = __builtin_amdgcn_rsq(a);
+        const double hh = 0.5 * a;
+        y = fma(y, fma(-hh * y, y, 0.5), y);
+        y = fma(y, fma(-hh * y, y, 0.5), y);
+        x[c] = (lane == c) ? cpx<double>{a * y, 0.0} : cscale(x[c], y);
+#pragma unroll
+        for (int c2 = c + 1; c2 < 16; ++c2) {
+          const double lx = rdl(x[c].x, c2), ly = rdl(x[c].y, c2);   // L[c2][c]
+          x[c2].x -= x[c].x * lx + x[c].y * ly;
+          x[c2].y -= x[c].y * lx - x[c].x * ly;
+        }
+      }
+#elif !defined(CCSC_ABL_NOPOTRF)
 #pragma unroll
       for (int c = 0; c < 16; ++c) {
         cpx<double> s0 = x[c], s1 = {0.0, 0.0};

@@ -49,8 +49,25 @@
 #include "zline.hpp"
 
 
+// Measured on the C2 slice (n = 1000, ms per launch): 7.98 plain, 7.75 nontemporal state,
+// 8.56 resident w alone, 7.17 both (tools/gpu_ab_zl.sh); a next-slice state prefetch by the
+// idle wave (LDS-DMA) and w held in registers (49 spills) were slower.  -D...=0 for A/B.
+#ifndef CCSC_ZL_NT
+#define CCSC_ZL_NT 1
+#endif
+#ifndef CCSC_ZL_WLDS
+#define CCSC_ZL_WLDS 1
+#endif
+
 namespace ccsc {
 
+#if CCSC_ZL_WLDS
+constexpr int kZlWL = 7;   // waves whose w bins stay in LDS (35 columns x 110 bins, 61.6 KB)
+constexpr size_t kZlSmem = zl::kSmem + (size_t)kZlWL * 5 * zl::Y * 16;
+#else
+constexpr size_t kZlSmem = zl::kSmem;
+#endif
+static_assert(kZlSmem <= 160 * 1024, "z-step LDS");
 
 template <typename T>
 __device__ __forceinline__ T soft_l(T a, T theta) {
@@ -109,6 +126,31 @@ template <typename V>
 __device__ __forceinline__ void zst(void* base, uint32_t boff, V v) {
   *reinterpret_cast<V*>(reinterpret_cast<char*>(base) + boff) = v;
 }
+// state stream (read once, written once per launch): CCSC_ZL_NT marks it nontemporal so it
+// does not evict the re-read spectra (w, dcorr, dhat) from L2
+typedef double nt_d2 __attribute__((ext_vector_type(2)));
+template <typename V>
+__device__ __forceinline__ V sld(const void* base, uint32_t boff) {
+#if CCSC_ZL_NT
+  const nt_d2 r = __builtin_nontemporal_load(
+      reinterpret_cast<const nt_d2*>(reinterpret_cast<const char*>(base) + boff));
+  V v;
+  v.x = r.x;
+  v.y = r.y;
+  return v;
+#else
+  return zld<V>(base, boff);
+#endif
+}
+template <typename V>
+__device__ __forceinline__ void sst(void* base, uint32_t boff, V v) {
+#if CCSC_ZL_NT
+  const nt_d2 r = {v.x, v.y};
+  __builtin_nontemporal_store(r, reinterpret_cast<nt_d2*>(reinterpret_cast<char*>(base) + boff));
+#else
+  zst<V>(base, boff, v);
+#endif
+}
 // an opaque copy of a lane index: per-lane address math is redone where it is used
 // instead of being hoisted out of the slice loop into (spilled) registers
 __device__ __forceinline__ int fresh(int v) {
@@ -154,6 +196,22 @@ __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn
   // the last wave owns one y-line and no x-line (55 row pairs = 11 waves of 5)
   const bool xwave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6) < 11;
   T nd = (T)0, nz = (T)0;   // TOL 2: ||z_cur - z_prev||^2, ||z_cur||^2 of the lanes' own elements
+#if CCSC_ZL_WLDS
+  // w is the same for every slice of the patch: the y-lines of waves 0..kZlWL-1 (columns
+  // 0..5 kZlWL - 1) keep their bins in the LDS left over beside T, each lane its own ten
+  // (slot k1 * 385 + c * 11 + k2; written and read back by the same lane, so no barrier)
+  cpx<T>* sW = sT + zl::TSZ;
+  if constexpr (MODE >= 2) {
+    if (__builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6) < kZlWL) {
+      const int lane = threadIdx.x & 63, l = min(lane / 11, 4), s = lane - 11 * l;
+      const int c = 5 * (int)(threadIdx.x >> 6) + l;
+      const int sb = min(s, 10);
+      const uint32_t bo = (uint32_t)(c * 11 + sb) * 16u;
+#pragma unroll
+      for (int k1 = 0; k1 < 10; ++k1) sW[k1 * 385 + c * 11 + sb] = zld<cpx<T>>(Wp, bo + k1 * 616 * 16);
+    }
+  }
+#endif
 
   for (int k = 0; k < K; ++k) {
     // lane roles, recomputed per slice from an opaque thread index (see fresh())
@@ -173,10 +231,18 @@ __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn
       // ---- P1: y-C2R of conj(dcorr_k) w from bins to T[y][c] ----
       const cpx<T>* dk = dcorr + (int64_t)k * zl::F;
       const uint32_t bo = (uint32_t)(c * 11 + sb) * 16u;
+#if CCSC_ZL_WLDS
+      const bool wl = __builtin_amdgcn_readfirstlane(wave) < kZlWL;
+#endif
       cpx<T> b[10];
 #pragma unroll
       for (int k1 = 0; k1 < 10; ++k1)
+#if CCSC_ZL_WLDS
+        b[k1] = cmulc(zld<cpx<T>>(dk, bo + k1 * 616 * 16),
+                      wl ? sW[k1 * 385 + c * 11 + sb] : zld<cpx<T>>(Wp, bo + k1 * 616 * 16));
+#else
         b[k1] = cmulc(zld<cpx<T>>(dk, bo + k1 * 616 * 16), zld<cpx<T>>(Wp, bo + k1 * 616 * 16));
+#endif
       inv_line<T, zl::RS>(b, Ey, sb, [&](int n2, cpx<T> val) {
         sT[mod110(11 * sa + 10 * n2) * zl::RS + c] = val;
       });
@@ -202,7 +268,7 @@ __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn
         // each corr value is consumed as the last inverse stage forms it ----
         V2 av[11];
 #pragma unroll
-        for (int n2 = 0; n2 < 11; ++n2) av[n2] = zld<V2>(A + sl, po + n2 * 550 * 16);
+        for (int n2 = 0; n2 < 11; ++n2) av[n2] = sld<V2>(A + sl, po + n2 * 550 * 16);
         V2 zo[TOL == 2 ? 11 : 1];
         if constexpr (TOL == 2) {
 #pragma unroll
@@ -227,7 +293,7 @@ __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn
           if constexpr (MODE == 2) {
             a.x = sx + corr.x;
             a.y = sy + corr.y;
-            zst<V2>(Ao + sl, po + n2 * 550 * 16, a);
+            sst<V2>(Ao + sl, po + n2 * 550 * 16, a);
             const T ux = soft_l(a.x, theta), uy = soft_l(a.y, theta);
             zc[n2] = {ux - (a.x - ux), uy - (a.y - uy)};
           }
@@ -474,7 +540,7 @@ template <typename T, int MODE, int TOL>
 static void zline_go(hipStream_t st, int64_t npatch, const T* A, T* Ao, const T* Zn, const T* Yn,
                      cpx<T>* W, const cpx<T>* Bs, const cpx<T>* dcorr, const cpx<T>* dhat,
                      const T* sden, int K, T theta, T* Zt, T* zpart) {
-  hipLaunchKernelGGL((k_zline<T, MODE, TOL>), dim3((unsigned)npatch), dim3(zl::NT), zl::kSmem, st,
+  hipLaunchKernelGGL((k_zline<T, MODE, TOL>), dim3((unsigned)npatch), dim3(zl::NT), kZlSmem, st,
                      A, Ao, Zn, Yn, W, Bs, dcorr, dhat, sden, K, theta, Zt, zpart);
 }
 
