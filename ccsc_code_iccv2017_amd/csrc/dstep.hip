@@ -323,7 +323,7 @@ __device__ __forceinline__ cpx<T> shfl_c(cpx<T> v, int src) {
 // wave (one load batch per block, address-independent of the solve) so their
 // latency is paid once per block instead of once per column.
 #ifndef CCSC_DS_JB
-#define CCSC_DS_JB 8
+#define CCSC_DS_JB 6
 #endif
 constexpr int kDsJB = CCSC_DS_JB;
 #ifndef CCSC_DS_BWRED

@@ -37,7 +37,7 @@ constexpr int kGcTS = 17;                   // column stride (complex) of an LDS
 constexpr int kGcTSZ = 16 * kGcTS;          // complex per LDS tile
 constexpr int kGcHPT = 8;                   // right-hand-side entries of h per thread
 #ifndef CCSC_GC_RL
-#define CCSC_GC_RL 0
+#define CCSC_GC_RL 1
 #endif
 
 __device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
