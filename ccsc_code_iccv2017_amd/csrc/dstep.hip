@@ -539,6 +539,223 @@ hipError_t launch_dsolve(const cpx<T>* L, const cpx<T>* h, const cpx<T>* Ch, cpx
 }
 
 // ---------------------------------------------------------------------------
+// Tile d-solve for the 2D headline block shape (NV = 1, 64 < K <= 112; C1/C2:
+// K = 100, dP:252-276).  The factor's diagonal 16 x 16 tiles hold M_JJ = L_JJ^-1
+// (k_invert_diag, once per precompute), so with r = h + rho C
+//   forward   y_J = M_JJ (r_J - sum_{J' < J} L_JJ' y_J')
+//   backward  x_J = M_JJ^H (y_J - sum_{I > J} L_IJ^H x_I)
+// are tile matrix-vector products with no serial chain inside a tile.  One
+// workgroup (4 waves) per (block, f) holds the T(T+1)/2 lower tiles in registers
+// (lane (row = l & 15, cg = l >> 4) holds L[row][4 cg + q], q < 4), reads them once
+// and runs both sweeps from registers: the factor crosses HBM once per solve where
+// k_dsolve streams it twice.  Tile ownership (kDtMap) puts (J+1, J) on the wave that
+// owns (J+1, J+1), so each sweep step is one phase between barriers:
+//   forward phase J:  owners of (I, J), I > J+1: r_I -= L_IJ y_J;  the owner of
+//                     (J+1, J): y_{J+1} = M (r_{J+1} - L_{J+1,J} y_J)
+//   backward phase J: the owner of (J, J): x_J = M^H (y_J - sum_I P_IJ), then
+//                     P_{J,J-1} = L_{J,J-1}^H x_J;  owners of (I, J-1), I > J: P_{I,J-1}
+// (P double-buffered by phase parity): T + 1 barriers per sweep pair instead of 4T.
+// ---------------------------------------------------------------------------
+constexpr int kDtT = 7;                          // tiles per dimension (K <= 112)
+constexpr int kDtTW = kDtT * (kDtT + 1) / 8;     // 7 tiles per wave
+// (I, J) of wave w's tile s, packed I * 8 + J (see above: pairs (J+1, J), (J+1, J+1)
+// share a wave; every column's off-diagonal tiles spread over the waves)
+__constant__ const unsigned char kDtMap[4][kDtTW] = {
+    {1 * 8 + 0, 1 * 8 + 1, 5 * 8 + 4, 5 * 8 + 5, 4 * 8 + 1, 4 * 8 + 2, 6 * 8 + 3},
+    {2 * 8 + 1, 2 * 8 + 2, 6 * 8 + 5, 6 * 8 + 6, 4 * 8 + 0, 5 * 8 + 3, 6 * 8 + 4},
+    {3 * 8 + 2, 3 * 8 + 3, 0 * 8 + 0, 2 * 8 + 0, 6 * 8 + 0, 5 * 8 + 1, 6 * 8 + 2},
+    {4 * 8 + 3, 4 * 8 + 4, 3 * 8 + 0, 5 * 8 + 0, 3 * 8 + 1, 6 * 8 + 1, 5 * 8 + 2}};
+
+// sum over the four 16-lane rows (lanes row, row + 16, row + 32, row + 48)
+__device__ __forceinline__ double xrow_sum(double v) {
+  v += __shfl_xor(v, 16, 64);
+  return v + __shfl_xor(v, 32, 64);
+}
+// sum within each 16-lane row (DPP; result in every lane of the row)
+__device__ __forceinline__ double row16_sum(double v) {
+  v += dpp_mov<0xB1>(v);    // quad_perm [1,0,3,2]
+  v += dpp_mov<0x4E>(v);    // quad_perm [2,3,0,1]
+  v += dpp_mov<0x141>(v);   // row_half_mirror
+  return v + dpp_mov<0x140>(v);   // row_mirror
+}
+__device__ __forceinline__ void wave_sync_lds() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
+bool dsolve_tile_ok(int K, int NV) { return NV == 1 && K > 64 && K <= 16 * kDtT; }
+
+__global__ __launch_bounds__(256) void k_dsolve_tile(const cpx<double>* __restrict__ L,
+                                                     const cpx<double>* __restrict__ h,
+                                                     const cpx<double>* __restrict__ Ch,
+                                                     cpx<double>* __restrict__ Dh, int F, int K,
+                                                     double rho) {
+  __shared__ cpx<double> sr[16 * kDtT], sy[16 * kDtT], sx[16 * kDtT], sp[2][kDtT][16];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int row = lane & 15, cg = lane >> 4;
+  const int blk = blockIdx.x / F, f = blockIdx.x - blk * F;
+  const int Tn = (K + 15) >> 4;
+  const cpx<double>* Lf = L + ((int64_t)blk * F + f) * (K * (K + 1) / 2);
+  const cpx<double> zero = {0.0, 0.0};
+  int tI[kDtTW], tJ[kDtTW];   // wave-uniform; tiles past the grid get I = -1
+#pragma unroll
+  for (int s = 0; s < kDtTW; ++s) {
+    const int m = kDtMap[wave][s];
+    tI[s] = (m >> 3) < Tn ? (m >> 3) : -1;
+    tJ[s] = m & 7;
+  }
+  cpx<double> Lt[kDtTW][4];
+#pragma unroll
+  for (int s = 0; s < kDtTW; ++s) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int R = 16 * tI[s] + row, C = 16 * tJ[s] + 4 * cg + q;
+      Lt[s][q] = (tI[s] >= 0 && R < K && C <= R) ? Lf[C * K - (C * (C - 1)) / 2 + R - C] : zero;
+    }
+  }
+  if (tid < 16 * Tn) {
+    cpx<double> v = zero;
+    if (tid < K) {
+      const cpx<double> c = Ch[((int64_t)blk * K + tid) * F + f];
+      const cpx<double> hh = h[((int64_t)blk * F + f) * K + tid];
+      v = {hh.x + rho * c.x, hh.y + rho * c.y};
+    }
+    sr[tid] = v;
+  }
+  __syncthreads();
+  // y = M v for the diagonal tile in slot s, v[i] in vbuf (LDS, this wave's own writes)
+  auto diag_fwd = [&](const cpx<double> (&Mt)[4], const cpx<double>* vbuf, cpx<double>* ybuf) {
+    cpx<double> v = zero;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v = cadd(v, cmul(Mt[q], vbuf[4 * cg + q]));
+    v = {xrow_sum(v.x), xrow_sum(v.y)};
+    if (cg == 0) ybuf[row] = v;
+  };
+  // ---- forward ----
+#pragma unroll
+  for (int s = 0; s < kDtTW; ++s)
+    if (tI[s] == 0 && tJ[s] == 0) diag_fwd(Lt[s], sr, sy);
+  __syncthreads();
+  for (int J = 0; J + 1 < Tn; ++J) {
+    const cpx<double>* yJ = sy + 16 * J;
+#pragma unroll
+    for (int s = 0; s < kDtTW; ++s) {
+      if (tJ[s] == J && tI[s] > J) {
+        cpx<double> v = zero;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v = cadd(v, cmul(Lt[s][q], yJ[4 * cg + q]));
+        v = {xrow_sum(v.x), xrow_sum(v.y)};
+        cpx<double>* rI = sr + 16 * tI[s];
+        if (cg == 0) rI[row] = csub(rI[row], v);
+        if (tI[s] == J + 1) {
+          // this wave also owns (J+1, J+1) (slot s + 1 by construction of kDtMap)
+          wave_sync_lds();
+          diag_fwd(Lt[s + 1 < kDtTW ? s + 1 : s], rI, sy + 16 * (J + 1));
+        }
+      }
+    }
+    __syncthreads();
+  }
+  // ---- backward ----
+  for (int J = Tn - 1; J >= 0; --J) {
+    const int pb = J & 1;   // partials P_IJ were written in the previous phase into sp[pb]
+#pragma unroll
+    for (int s = 0; s < kDtTW; ++s) {
+      if (tI[s] == J && tJ[s] == J) {
+        cpx<double> v = sy[16 * J + row];
+        for (int I = J + 1; I < Tn; ++I) v = csub(v, sp[pb][I][row]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const cpx<double> p = cmulc(Lt[s][q], v);   // conj(M[row][c]) v[row]
+          const cpx<double> ps = {row16_sum(p.x), row16_sum(p.y)};
+          if (row == 0) sx[16 * J + 4 * cg + q] = ps;
+        }
+        wave_sync_lds();
+      }
+    }
+    if (J == 0) break;
+    // partials for column block J - 1 (x_I known for I >= J after the step above)
+#pragma unroll
+    for (int s = 0; s < kDtTW; ++s) {
+      if (tJ[s] == J - 1 && tI[s] >= J) {
+        const cpx<double> xr = sx[16 * tI[s] + row];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const cpx<double> p = cmulc(Lt[s][q], xr);   // conj(L[row][c]) x[row]
+          const cpx<double> ps = {row16_sum(p.x), row16_sum(p.y)};
+          if (row == 0) sp[pb ^ 1][tI[s]][4 * cg + q] = ps;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  __syncthreads();
+  if (tid < K) Dh[((int64_t)blk * K + tid) * F + f] = sx[tid];
+}
+
+hipError_t launch_dsolve_tile(const cpx<double>* L, const cpx<double>* h, const cpx<double>* Ch,
+                              cpx<double>* Dh, int nblocks, int F, int K, double rho,
+                              hipStream_t st) {
+  if (nblocks <= 0) return hipSuccess;
+  if (!dsolve_tile_ok(K, 1)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_dsolve_tile, dim3((unsigned)(nblocks * F)), dim3(256), 0, st, L, h, Ch,
+                     Dh, F, K, rho);
+  return hipGetLastError();
+}
+
+// In place: the diagonal 16 x 16 tiles of one block's F packed factors <- their
+// inverses (the form k_dsolve_tile reads), once per precompute.  One wave per
+// (f, tile J) item: L_JJ staged in LDS, lane c & 15 forms column c of M = L_JJ^-1 by
+// forward substitution into the wave's LDS copy of M (each lane reads back only its
+// own column; the four lanes of a column write the same values):
+//   M[r][c] = (delta_rc - sum_{k<r} L[r][k] M[k][c]) / L[r][r],
+// a row's 2r broadcast reads issued together.
+__global__ __launch_bounds__(256) void k_invert_diag(cpx<double>* __restrict__ L, int F, int K,
+                                                     int Tn) {
+  __shared__ cpx<double> sL[4][16 * 17], sM[4][16 * 17];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15;
+  const int64_t item = (int64_t)blockIdx.x * 4 + wave;   // f * Tn + J
+  if (item >= (int64_t)F * Tn) return;                   // wave-uniform
+  const int f = (int)(item / Tn), J = (int)(item - (int64_t)f * Tn);
+  cpx<double>* Lf = L + (int64_t)f * (K * (K + 1) / 2);
+  cpx<double>* Lw = sL[wave];
+  cpx<double>* Mw = sM[wave];
+  for (int e = lane; e < 256; e += 64) {
+    const int r = e & 15, cc = e >> 4, R = 16 * J + r, C = 16 * J + cc;
+    Lw[cc * 17 + r] = (r >= cc && R < K) ? Lf[C * K - (C * (C - 1)) / 2 + R - C]
+                                         : cpx<double>{(r == cc) ? 1.0 : 0.0, 0.0};
+  }
+  wave_sync_lds();
+  for (int r = 0; r < 16; ++r) {
+    cpx<double> s0 = {(r == c) ? 1.0 : 0.0, 0.0}, s1 = {0.0, 0.0};
+#pragma unroll
+    for (int k = 0; k < 15; ++k) {
+      if (k < r) {
+        const cpx<double> p = cmul(Lw[k * 17 + r], Mw[k * 17 + c]);
+        if (k & 1) s1 = csub(s1, p);
+        else s0 = csub(s0, p);
+      }
+    }
+    Mw[r * 17 + c] = cscale(cadd(s0, s1), 1.0 / Lw[r * 17 + r].x);
+  }
+  if (lane < 16) {
+    const int C = 16 * J + c;
+    for (int r = c; r < 16 && 16 * J + r < K; ++r)
+      Lf[C * K - (C * (C - 1)) / 2 + 16 * J + r - C] = Mw[r * 17 + c];
+  }
+}
+
+hipError_t launch_invert_diag(cpx<double>* L, int F, int K, hipStream_t st) {
+  const int Tn = (K + 15) >> 4;
+  if (F <= 0 || Tn > kDtT) return hipErrorInvalidValue;
+  const int64_t items = (int64_t)F * Tn;
+  hipLaunchKernelGGL(k_invert_diag, dim3((unsigned)((items + 3) / 4)), dim3(256), 0, st, L, F, K,
+                     Tn);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // Woodbury form for blocks of ni << K patches (3D/4D: ni = sqrt(n) = 8, K = 49):
 // (A^H A + rho I)^{-1} = (I - A^H M^{-1} A) / rho, M = rho I + A A^H (ni x ni) --
 // the reference's own pinv(rho I + A A^H) form (dP:230-236, L3/L4 precompute),

@@ -403,6 +403,7 @@ struct Session2D {
   bool is4, is3;
   bool woodbury;   // D-factor in Woodbury form (p.dfactor; AUTO: woodbury_fits, ni << K)
   bool gram_mf;    // Gram + Cholesky on the matrix cores (gramchol.hip; CCSC_GRAM_MF=0: VALU form)
+  bool dtile = false;   // tile d-solve on a factor with inverted diagonal tiles (dstep.hip)
   int64_t N, nbl, b0, np;
   bool owner0;
   double theta;
@@ -533,6 +534,10 @@ struct Session2D {
     {
       const char* ev = std::getenv("CCSC_GRAM_MF");
       gram_mf = gram_chol_mf_ok(K, NV) && !(ev && ev[0] == '0');
+      // tile d-solve (one read of the factor per solve) on the MFMA factor with inverted
+      // diagonal tiles; CCSC_DS_TILE=0 keeps the two-sweep k_dsolve
+      const char* et = std::getenv("CCSC_DS_TILE");
+      dtile = gram_mf && !woodbury && dsolve_tile_ok(K, NV) && !(et && et[0] == '0');
     }
     is4 = p.variant == CCSC_L4D;
     is3 = p.variant == CCSC_L3D;
@@ -942,8 +947,10 @@ struct Session2D {
         if (woodbury)
           HIPCHK(launch_gram_wb<double>(Zh.as<cpx<double>>(), Bj, Lj, hj, F, K, ni, p.rho_d, NV,
                                         st));
-        else if (gram_mf)
+        else if (gram_mf) {
           HIPCHK(launch_gram_chol_mf(Zh.as<cpx<double>>(), Bj, Lj, hj, F, K, ni, p.rho_d, NV, st));
+          if (dtile) HIPCHK(launch_invert_diag(Lj, F, K, st));
+        }
         else
           HIPCHK(launch_gram_chol<double>(Zh.as<cpx<double>>(), Bj, Lj, hj, F, K, ni, p.rho_d,
                                           NV, st));
@@ -960,6 +967,10 @@ struct Session2D {
           HIPCHK(launch_dsolve_wb<double>(L.as<cpx<double>>(), h.as<cpx<double>>(),
                                           Ch.as<cpx<double>>(), Dh.as<cpx<double>>(), (int)nbl, F,
                                           K, ni, p.rho_d, NV, st));
+        else if (dtile)
+          HIPCHK(launch_dsolve_tile(L.as<cpx<double>>(), h.as<cpx<double>>(),
+                                    Ch.as<cpx<double>>(), Dh.as<cpx<double>>(), (int)nbl, F, K,
+                                    p.rho_d, st));
         else
           HIPCHK(launch_dsolve<double>(L.as<cpx<double>>(), h.as<cpx<double>>(),
                                        Ch.as<cpx<double>>(), Dh.as<cpx<double>>(), (int)nbl, F, K,

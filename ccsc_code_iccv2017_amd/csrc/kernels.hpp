@@ -110,6 +110,16 @@ hipError_t launch_gram_chol_mf(const cpx<double>* Zh, const cpx<double>* Bh, cpx
 template <typename T>
 hipError_t launch_dsolve(const cpx<T>* L, const cpx<T>* h, const cpx<T>* Ch, cpx<T>* Dh,
                          int nblocks, int F, int K, T rho, int NV, hipStream_t st);
+// The same solve (NV = 1, 64 < K <= 112) on a factor whose diagonal 16 x 16 tiles hold
+// L_jj^-1 (launch_invert_diag, in place after the Gram/Cholesky kernel): one workgroup
+// per (block, f) holds the factor's
+// 16 x 16 tiles in registers and both sweeps are tile matrix-vector products, so L is
+// read once per solve instead of twice.
+bool dsolve_tile_ok(int K, int NV);
+hipError_t launch_invert_diag(cpx<double>* L, int F, int K, hipStream_t st);
+hipError_t launch_dsolve_tile(const cpx<double>* L, const cpx<double>* h, const cpx<double>* Ch,
+                              cpx<double>* Dh, int nblocks, int F, int K, double rho,
+                              hipStream_t st);
 // Woodbury form for blocks of few patches (woodbury_fits): per f the slot of
 // Kp = K(K+1)/2 complex holds A (ni x K, row-major) and the Cholesky factor of
 // M = rho I + A A^H (ni x ni dense, row-major, zeros above the diagonal);
