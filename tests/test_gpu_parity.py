@@ -207,6 +207,30 @@ def test_dfactor_forms_agree(gpu_ctx, rho_d):
     assert _rel(outs["woodbury"][0], outs["cholesky"][0]) < 1e-8
 
 
+@pytest.mark.parametrize("K", [72, 100])
+def test_dsolve_tile_matches_two_sweep_and_oracle(gpu_ctx, K, monkeypatch):
+    """The tile d-solve (dstep.hip k_dsolve_tile on a factor whose diagonal tiles are
+    inverted by k_invert_diag; NV = 1, 64 < K <= 112 -- the C1/C2 block shape) and the
+    two-sweep k_dsolve (CCSC_DS_TILE=0) give the oracle's iterate (dP:252-276); K = 72
+    leaves a partial last tile (Tn = 5)."""
+    from ccsc_code_iccv2017_amd import learners as E
+    b, d0, z0 = _case("dz", (12, 12), 5, K, 2 * K, K, seed=41)
+    init = {"d": d0, "z": z0}
+    o = O.learn_2d_dzparallel(b, [5, 5, K], 1.0, 1.0, 2, 0.0, "brief", init, ni=K,
+                              trace_objective=True)
+    outs = {}
+    for tile in ("1", "0"):
+        monkeypatch.setenv("CCSC_DS_TILE", tile)
+        outs[tile] = E.admm_learn_conv2D_large_dzParallel(b, [5, 5, K], 1.0, 1.0, 2, 0.0,
+                                                          "brief", init, ni=K,
+                                                          trace_objective=True, ctx=gpu_ctx)
+    for tile, e in outs.items():
+        assert _rel(e[0], o[0]) < 1e-7, tile
+        assert _rel(e[1], o[1]) < 1e-7, tile
+        np.testing.assert_allclose(e[3]["trace"]["obj_z"], np.array(o[4]["obj_z"]), rtol=1e-9)
+    assert _rel(outs["1"][0], outs["0"][0]) < 1e-9
+
+
 def test_dfactor_woodbury_rejected_when_blocks_too_large(gpu_ctx):
     from ccsc_code_iccv2017_amd import _lib as L
     from ccsc_code_iccv2017_amd import learners as E
