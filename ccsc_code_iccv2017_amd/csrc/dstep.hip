@@ -594,7 +594,12 @@ __global__ __launch_bounds__(256) void k_dsolve_tile(const cpx<double>* __restri
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int row = lane & 15, cg = lane >> 4;
-  const int blk = blockIdx.x / F, f = blockIdx.x - blk * F;
+  // XCD-aware: workgroups i, i + 8, ... (one XCD) take neighbouring f, so the [blk][K][F]
+  // right-hand sides and solutions they read and write share 128-B lines in one L2
+  const int per = (F + 7) >> 3;
+  const int blk = blockIdx.x / (8 * per), r8 = blockIdx.x - blk * 8 * per;
+  const int f = (r8 & 7) * per + (r8 >> 3);
+  if (f >= F) return;
   const int Tn = (K + 15) >> 4;
   const cpx<double>* Lf = L + ((int64_t)blk * F + f) * (K * (K + 1) / 2);
   const cpx<double> zero = {0.0, 0.0};
@@ -699,8 +704,8 @@ hipError_t launch_dsolve_tile(const cpx<double>* L, const cpx<double>* h, const 
                               hipStream_t st) {
   if (nblocks <= 0) return hipSuccess;
   if (!dsolve_tile_ok(K, 1)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_dsolve_tile, dim3((unsigned)(nblocks * F)), dim3(256), 0, st, L, h, Ch,
-                     Dh, F, K, rho);
+  hipLaunchKernelGGL(k_dsolve_tile, dim3((unsigned)(nblocks * 8 * ((F + 7) / 8))), dim3(256), 0,
+                     st, L, h, Ch, Dh, F, K, rho);
   return hipGetLastError();
 }
 
