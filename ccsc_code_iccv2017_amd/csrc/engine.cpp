@@ -376,6 +376,8 @@ static Plan2D plan2d(const ccsc_problem& p, const Geom& g, int rank, int nranks)
   // register-line z-step (zline.hip, 110 grid): B^ and the two filter spectra in
   // bin-slot order, sden in bin-slot order
   m.zl = zline ? m.np * F * 16 + 2 * K * F * 16 + F * 8 : 0;
+  // + the second precompute workspace (the R2C of block j+1 beside the Gram of block j)
+  if (zline) m.zl += m.Zh;
   m.misc = (2 * K * NV * F) * 16 + F * 8 + (m.nbl + 2) * K * NV * SS * 8 * 2 +
            (4 * m.np * NV * g.Tn + 4 * K * NV * g.Tn + 64) * 8 + (size_t)(G.ntw + g.Gt.ntw) * 16 +
            (is3 ? F * 16 + P * 8 : 0);
@@ -404,6 +406,14 @@ struct Session2D {
   bool woodbury;   // D-factor in Woodbury form (p.dfactor; AUTO: woodbury_fits, ni << K)
   bool gram_mf;    // Gram + Cholesky on the matrix cores (gramchol.hip; CCSC_GRAM_MF=0: VALU form)
   bool dtile = false;   // tile d-solve on a factor with inverted diagonal tiles (dstep.hip)
+  // the diagonal-tile inversion of block j runs on st2 beside block j+1's precompute R2C
+  hipStream_t st2 = nullptr;
+  hipEvent_t ev_g = nullptr, ev_i = nullptr;
+  // 110 grid: block j+1's precompute R2C (k_zhat_line, into the other of Zh / Zh2) runs on
+  // st3 beside block j's Gram/Cholesky, filling that kernel's last partial round
+  hipStream_t st3 = nullptr;
+  hipEvent_t ev_s = nullptr, ev_z = nullptr, ev_gz[2] = {nullptr, nullptr};
+  DevBuf Zh2;
   int64_t N, nbl, b0, np;
   bool owner0;
   double theta;
@@ -491,6 +501,18 @@ struct Session2D {
 
   ~Session2D() {
     if (st) hipStreamSynchronize(st);
+    if (st2) {
+      hipStreamSynchronize(st2);
+      hipStreamDestroy(st2);
+    }
+    if (ev_g) hipEventDestroy(ev_g);
+    if (ev_i) hipEventDestroy(ev_i);
+    if (st3) {
+      hipStreamSynchronize(st3);
+      hipStreamDestroy(st3);
+    }
+    for (hipEvent_t e : {ev_s, ev_z, ev_gz[0], ev_gz[1]})
+      if (e) hipEventDestroy(e);
     for (auto& rc : recs) {
       hipEventDestroy(rc.a);
       hipEventDestroy(rc.b);
@@ -538,6 +560,11 @@ struct Session2D {
       // diagonal tiles; CCSC_DS_TILE=0 keeps the two-sweep k_dsolve
       const char* et = std::getenv("CCSC_DS_TILE");
       dtile = gram_mf && !woodbury && dsolve_tile_ok(K, NV) && !(et && et[0] == '0');
+      if (dtile) {
+        HIPCHK(hipStreamCreateWithFlags(&st2, hipStreamNonBlocking));
+        HIPCHK(hipEventCreateWithFlags(&ev_g, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&ev_i, hipEventDisableTiming));
+      }
     }
     is4 = p.variant == CCSC_L4D;
     is3 = p.variant == CCSC_L3D;
@@ -599,6 +626,10 @@ struct Session2D {
       zhat_line = !(ev && ev[0] == '0');
     }
     if (zl_on) {
+      Zh2.alloc(m.Zh);
+      HIPCHK(hipStreamCreateWithFlags(&st3, hipStreamNonBlocking));
+      for (hipEvent_t* e : {&ev_s, &ev_z, &ev_gz[0], &ev_gz[1]})
+        HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
       Bhs.alloc((size_t)np * F * 16);
       dhs.alloc((size_t)K * F * 16);
       dhws.alloc((size_t)K * F * 16);
@@ -927,8 +958,21 @@ struct Session2D {
     HIPCHK(hipEventRecord(e0, st));
 
     // ---- D precompute (dP:95-99) ----
+    const bool ovz = zmode == 2 && zhat_line && st3;
+    if (ovz) {   // st3's R2C passes read the state the z-phase left on st
+      HIPCHK(hipEventRecord(ev_s, st));
+      HIPCHK(hipStreamWaitEvent(st3, ev_s, 0));
+    }
     for (int64_t jl = 0; jl < nbl; ++jl) {
-      if (zmode == 2 && zhat_line)   // the same on the lanes (zline.hip)
+      cpx<double>* Zc = (ovz && (jl & 1)) ? Zh2.as<cpx<double>>() : Zh.as<cpx<double>>();
+      if (ovz) {   // the same on the lanes (zline.hip), on st3 (see st3)
+        if (jl >= 2) HIPCHK(hipStreamWaitEvent(st3, ev_gz[jl & 1], 0));   // Gram(jl-2) read Zc
+        HIPCHK(launch_zhat_line<double>(z.as<double>() + (size_t)jl * ni * K * P,
+                                        W.as<cpx<double>>() + (size_t)jl * ni * F, dws, Zc, ni,
+                                        K, theta, st3));
+        HIPCHK(hipEventRecord(ev_z, st3));
+        HIPCHK(hipStreamWaitEvent(st, ev_z, 0));
+      } else if (zmode == 2 && zhat_line)
         HIPCHK(launch_zhat_line<double>(z.as<double>() + (size_t)jl * ni * K * P,
                                         W.as<cpx<double>>() + (size_t)jl * ni * F, dws,
                                         Zh.as<cpx<double>>(), ni, K, theta, st));
@@ -945,16 +989,23 @@ struct Session2D {
         cpx<double>* Lj = L.as<cpx<double>>() + (size_t)jl * F * Kp;
         cpx<double>* hj = h.as<cpx<double>>() + (size_t)jl * F * NV * K;
         if (woodbury)
-          HIPCHK(launch_gram_wb<double>(Zh.as<cpx<double>>(), Bj, Lj, hj, F, K, ni, p.rho_d, NV,
-                                        st));
+          HIPCHK(launch_gram_wb<double>(Zc, Bj, Lj, hj, F, K, ni, p.rho_d, NV, st));
         else if (gram_mf) {
-          HIPCHK(launch_gram_chol_mf(Zh.as<cpx<double>>(), Bj, Lj, hj, F, K, ni, p.rho_d, NV, st));
-          if (dtile) HIPCHK(launch_invert_diag(Lj, F, K, st));
+          HIPCHK(launch_gram_chol_mf(Zc, Bj, Lj, hj, F, K, ni, p.rho_d, NV, st));
+          if (dtile) {
+            HIPCHK(hipEventRecord(ev_g, st));
+            HIPCHK(hipStreamWaitEvent(st2, ev_g, 0));
+            HIPCHK(launch_invert_diag(Lj, F, K, st2));
+          }
         }
         else
-          HIPCHK(launch_gram_chol<double>(Zh.as<cpx<double>>(), Bj, Lj, hj, F, K, ni, p.rho_d,
-                                          NV, st));
+          HIPCHK(launch_gram_chol<double>(Zc, Bj, Lj, hj, F, K, ni, p.rho_d, NV, st));
       });
+      if (ovz) HIPCHK(hipEventRecord(ev_gz[jl & 1], st));
+    }
+    if (dtile) {   // every block's inverted diagonal tiles before the first d-solve
+      HIPCHK(hipEventRecord(ev_i, st2));
+      HIPCHK(hipStreamWaitEvent(st, ev_i, 0));
     }
     // ---- D iterations (dP:103-134) ----
     const bool tol_on = p.tol > 0;
