@@ -272,7 +272,7 @@ __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn
         V2 zo[TOL == 2 ? 11 : 1];
         if constexpr (TOL == 2) {
 #pragma unroll
-          for (int n2 = 0; n2 < 11; ++n2) zo[n2] = zld<V2>(Zt + sl, po + n2 * 550 * 16);
+          for (int n2 = 0; n2 < 11; ++n2) zo[n2] = sld<V2>(Zt + sl, po + n2 * 550 * 16);
         }
         // lanes that own their elements (not a clamped duplicate) count in the norms
         const T own = (s < 10 && lane < 55) ? (T)1 : (T)0;
@@ -288,7 +288,7 @@ __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn
               nd += own * (ex * ex + ey * ey);
               nz += own * (zn.x * zn.x + zn.y * zn.y);
             }
-            zst<V2>(Zt + sl, po + n2 * 550 * 16, zn);
+            sst<V2>(Zt + sl, po + n2 * 550 * 16, zn);
           }
           if constexpr (MODE == 2) {
             a.x = sx + corr.x;
