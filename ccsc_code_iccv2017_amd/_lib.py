@@ -20,10 +20,11 @@ CCSC_E_UNSUPPORTED = -5
 CCSC_E_STATE = -6
 
 CCSC_DPAR, CCSC_DZPAR, CCSC_L3D, CCSC_L4D, CCSC_HS23 = 0, 1, 2, 3, 4
-ABI_VERSION = 5
+ABI_VERSION = 6
 VERBOSE = {"none": 0, "brief": 1, "all": 2}
 CCSC_FP64, CCSC_FP32 = 0, 1
 DFACTOR = {"auto": 0, "cholesky": 1, "woodbury": 2}
+TRANSPORT = {0: "none", 1: "rccl", 2: "host"}
 
 
 class Problem(C.Structure):
@@ -133,6 +134,7 @@ SIGNATURES = {
                                           C.c_char_p, C.c_size_t]),
     "ccsc_create_multi": (C.c_void_p, [C.POINTER(C.c_int32), C.c_int32, C.c_char_p, C.c_size_t]),
     "ccsc_destroy": (None, [C.c_void_p]),
+    "ccsc_comm_ranks": (C.c_int32, [C.c_void_p, _ip, _ip, C.c_char_p, C.c_size_t]),
     "ccsc_learn": (C.c_int32, [C.c_void_p, C.POINTER(Problem), _dp, _dp, _dp,
                                C.POINTER(Outputs), C.POINTER(IterLog), CB, C.c_void_p,
                                C.c_char_p, C.c_size_t]),

@@ -710,15 +710,38 @@ struct Session2D {
     HIPCHK(hipMemcpyAsync(buf, ctx->stage.data(), count * 8, hipMemcpyHostToDevice, st));
     HIPCHK(hipStreamSynchronize(st));
   }
-  void allreduce(double* buf, size_t count) {
+  // The transport is chosen by what the context was created with (a host callback or
+  // an RCCL communicator), never by a communicator pointer an abort may have cleared;
+  // in a multi-device group every collective first checks that no rank has failed.
+  template <typename Fn>
+  void collective(int op, double* buf, size_t count, Fn&& rccl) {
     if (ctx->nranks <= 1) return;
-    if (ctx->comm) NCCLCHK(ncclAllReduce(buf, buf, count, ncclDouble, ncclSum, ctx->comm, st));
-    else host_exchange(CCSC_COMM_ALLREDUCE_SUM, buf, count);
+    if (ctx->hostfn) {   // the exchange itself returns an error once the group aborted
+      host_exchange(op, buf, count);
+      return;
+    }
+    CommGroup* g = ctx->grp.get();
+    if (g) g->inflight.fetch_add(1);
+    struct Leave {
+      CommGroup* g;
+      ~Leave() {
+        if (g) g->inflight.fetch_sub(1);
+      }
+    } leave{g};
+    if (g && g->aborted.load())
+      throw Err(CCSC_E_RCCL, "host communicator aborted: another rank of this context failed");
+    if (!ctx->comm) throw Err(CCSC_E_STATE, "multi-rank context without a communicator");
+    rccl();
+  }
+  void allreduce(double* buf, size_t count) {
+    collective(CCSC_COMM_ALLREDUCE_SUM, buf, count, [&] {
+      NCCLCHK(ncclAllReduce(buf, buf, count, ncclDouble, ncclSum, ctx->comm, st));
+    });
   }
   void bcast0(double* buf, size_t count) {
-    if (ctx->nranks <= 1) return;
-    if (ctx->comm) NCCLCHK(ncclBroadcast(buf, buf, count, ncclDouble, 0, ctx->comm, st));
-    else host_exchange(CCSC_COMM_BCAST0, buf, count);
+    collective(CCSC_COMM_BCAST0, buf, count, [&] {
+      NCCLCHK(ncclBroadcast(buf, buf, count, ncclDouble, 0, ctx->comm, st));
+    });
   }
   void pair_to_host(double* out2) {
     HIPCHK(hipMemcpyAsync(out2, pair.p, 2 * sizeof(double), hipMemcpyDeviceToHost, st));
@@ -1625,6 +1648,53 @@ struct ccsc_session {
 };
 
 namespace ccsc {
+// One rank of a multi-device context failed: mark the group aborted (once, whichever
+// threads fail), wake the in-process exchange, let collectives already past their
+// abort check finish enqueueing, then abort every RCCL communicator so the other
+// ranks' collectives waiting on the failed rank return (see CommGroup).
+static void abort_group(ccsc_ctx* ctx) {
+  CommGroup* g = ctx->grp.get();
+  std::lock_guard<std::mutex> lk(g->mu);
+  if (g->aborted.exchange(true)) return;
+  if (ctx->hg) ctx->hg->abort();
+  for (int i = 0; i < 2000 && g->inflight.load() > 0; ++i)
+    std::this_thread::sleep_for(std::chrono::microseconds(50));
+  for (ccsc_ctx* u : ctx->subs)
+    if (u->comm) {
+      ncclCommAbort(u->comm);
+      u->comm = nullptr;
+    }
+}
+
+// Before a learn on a multi-device context whose previous learn failed: fresh
+// communicators (RCCL: ncclCommInitAll over the device list; repeated devices: a new
+// in-process exchange), so a failure does not leave the (MEX-cached) context unusable.
+static void reset_group(ccsc_ctx* ctx) {
+  CommGroup* g = ctx->grp.get();
+  if (!g || !g->aborted.load()) return;
+  std::lock_guard<std::mutex> lk(g->mu);
+  const int nd = (int)ctx->subs.size();
+  if (ctx->hg) {
+    ctx->hg.reset(new HostGroup(nd));
+    for (int i = 0; i < nd; ++i) ctx->hg_ranks[i] = HostGroupRank{ctx->hg.get(), i};
+  } else {
+    std::vector<ncclComm_t> comms(nd, nullptr);
+    NCCLCHK(ncclCommInitAll(comms.data(), nd, ctx->devices.data()));
+    for (int i = 0; i < nd; ++i) ctx->subs[i]->comm = comms[i];
+    HIPCHK(hipSetDevice(ctx->device));
+  }
+  g->aborted.store(false);
+}
+
+// Test-only fault injection (failure detection): CCSC_TEST_FAIL_RANK =
+// "rank:outer" makes that rank of a multi-device learn throw before outer iteration
+// `outer`, while the other ranks run into their next collective.
+static bool injected_fault(int rank, int outer) {
+  const char* ev = std::getenv("CCSC_TEST_FAIL_RANK");
+  int r = -1, o = -1;
+  return ev && std::sscanf(ev, "%d:%d", &r, &o) == 2 && r == rank && o == outer;
+}
+
 // ccsc_learn on a multi-device context: the caller's whole problem (b, z0, outputs
 // over all n patches) is split at the block boundaries of ccsc_shard; rank i runs
 // on sub-context i in its own host thread, the calling thread drives rank 0 and is
@@ -1633,6 +1703,7 @@ namespace ccsc {
 static void learn_group(ccsc_ctx* ctx, const ccsc_problem& pin, const double* b, const double* d0,
                         const double* z0, ccsc_outputs* out, ccsc_iterlog* log, ccsc_cb cb,
                         void* user) {
+  reset_group(ctx);
   ccsc_problem q = pin;
   resolve_problem(q);
   Geom g;
@@ -1648,12 +1719,10 @@ static void learn_group(ccsc_ctx* ctx, const ccsc_problem& pin, const double* b,
   std::vector<std::vector<double>> dscr(nd), oscr(nd);
   std::vector<std::string> errs(nd);
   std::vector<int> codes(nd, CCSC_OK);
-  auto fail_all = [&] {
-    if (ctx->hg) ctx->hg->abort();
-    for (ccsc_ctx* u : ctx->subs)
-      if (u->comm) ncclCommAbort(u->comm), u->comm = nullptr;
-  };
   auto run = [&](int i) {
+    // the session outlives the catch: a failed rank aborts the group BEFORE its stream is
+    // drained, so no rank waits on a collective whose peer has stopped
+    std::unique_ptr<Session2D> Sp;
     try {
       ccsc_ctx* u = ctx->subs[i];
       HIPCHK(hipSetDevice(u->device));
@@ -1661,9 +1730,13 @@ static void learn_group(ccsc_ctx* ctx, const ccsc_problem& pin, const double* b,
       shard(q, i, nd, b0, nb);
       const int64_t p0 = b0 * q.ni;
       const double* zi = z0 ? (q.variant == CCSC_DZPAR ? z0 : z0 + p0 * zpatch) : nullptr;
-      Session2D S(u, q, b + p0 * bpatch, d0, zi);
+      Sp.reset(new Session2D(u, q, b + p0 * bpatch, d0, zi));
+      Session2D& S = *Sp;
       S.ensure_trace_capacity(S.p.max_it);
       for (int it = 0; it < S.p.max_it && !S.finished; ++it) {
+        if (injected_fault(i, it))
+          throw Err(CCSC_E_INVALID, "injected fault (CCSC_TEST_FAIL_RANK) before outer iteration " +
+                                        std::to_string(it));
         S.outer_iteration();
         if (i == 0 && cb) cb(user, S.outer_done, S.v_obj_d.back(), S.v_obj_z.back(), S.v_tim.back());
       }
@@ -1686,11 +1759,15 @@ static void learn_group(ccsc_ctx* ctx, const ccsc_problem& pin, const double* b,
     } catch (const Err& e) {
       errs[i] = e.what();
       codes[i] = e.code;
-      fail_all();
+      abort_group(ctx);
     } catch (const std::exception& e) {
       errs[i] = e.what();
       codes[i] = CCSC_E_INVALID;
-      fail_all();
+      abort_group(ctx);
+    }
+    try {
+      Sp.reset();
+    } catch (...) {
     }
   };
   std::vector<std::thread> th;
@@ -1825,42 +1902,79 @@ ccsc_ctx* ccsc_create_multi(const int32_t* devices, int32_t ndev, char* err, siz
       if (devices[i] < 0 || devices[i] >= count)
         throw Err(CCSC_E_INVALID, "device " + std::to_string(devices[i]) + " out of range (" +
                                       std::to_string(count) + " visible)");
-    std::unique_ptr<ccsc_ctx> c(new ccsc_ctx());
+    // every object is owned by `c` (subs, their streams and communicators) the moment it
+    // exists, so an error at any step releases all of it through ccsc_destroy
+    struct Guard {
+      ccsc_ctx* c;
+      ~Guard() {
+        if (c) ccsc_destroy(c);
+      }
+    } guard{new ccsc_ctx()};
+    ccsc_ctx* c = guard.c;
     c->device = devices[0];
     c->nranks = ndev;
+    c->devices.assign(devices, devices + ndev);
     HIPCHK(hipSetDevice(devices[0]));
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     if (ndev > 1) {
       bool distinct = true;
       for (int i = 0; i < ndev; ++i)
         for (int j = 0; j < i; ++j) distinct = distinct && devices[i] != devices[j];
-      std::vector<ncclComm_t> comms(ndev, nullptr);
-      if (distinct) {
-        NCCLCHK(ncclCommInitAll(comms.data(), ndev, devices));
-      } else {
+      c->grp = std::make_shared<CommGroup>();
+      if (!distinct) {
         c->hg.reset(new HostGroup(ndev));
         c->hg_ranks.resize(ndev);
       }
       for (int i = 0; i < ndev; ++i) {
-        std::unique_ptr<ccsc_ctx> u(new ccsc_ctx());
+        c->subs.push_back(new ccsc_ctx());
+        ccsc_ctx* u = c->subs.back();
         u->device = devices[i];
         u->rank = i;
         u->nranks = ndev;
-        u->comm = comms[i];
+        u->grp = c->grp;
         if (c->hg) {
           c->hg_ranks[i] = HostGroupRank{c->hg.get(), i};
           u->hostfn = host_group_fn;
           u->hostuser = &c->hg_ranks[i];
         }
+      }
+      if (distinct) {
+        std::vector<ncclComm_t> comms(ndev, nullptr);
+        NCCLCHK(ncclCommInitAll(comms.data(), ndev, devices));
+        for (int i = 0; i < ndev; ++i) c->subs[i]->comm = comms[i];
+      }
+      for (int i = 0; i < ndev; ++i) {
         HIPCHK(hipSetDevice(devices[i]));
-        HIPCHK(hipStreamCreateWithFlags(&u->stream, hipStreamNonBlocking));
-        c->subs.push_back(u.release());
+        HIPCHK(hipStreamCreateWithFlags(&c->subs[i]->stream, hipStreamNonBlocking));
       }
       HIPCHK(hipSetDevice(devices[0]));
     }
-    ctx = c.release();
+    ctx = c;
+    guard.c = nullptr;
   });
   return rc == CCSC_OK ? ctx : nullptr;
+}
+
+int32_t ccsc_comm_ranks(ccsc_ctx* ctx, int32_t* ranks, int32_t* transport, char* err,
+                        size_t errlen) {
+  return guarded(err, errlen, [&] {
+    if (!ctx || !ranks) throw Err(CCSC_E_INVALID, "NULL argument");
+    // a multi-device context reports the communicator of its rank 0
+    const ccsc_ctx* u = ctx->subs.empty() ? ctx : ctx->subs[0];
+    int32_t t = CCSC_TRANSPORT_NONE, n = 1;
+    if (u->nranks > 1 && u->hostfn) {
+      t = CCSC_TRANSPORT_HOST;
+      n = u->nranks;
+    } else if (u->nranks > 1) {
+      if (!u->comm) throw Err(CCSC_E_STATE, "the communicator was aborted (a rank failed)");
+      int c = 0;
+      NCCLCHK(ncclCommCount(u->comm, &c));
+      t = CCSC_TRANSPORT_RCCL;
+      n = c;
+    }
+    *ranks = n;
+    if (transport) *transport = t;
+  });
 }
 
 void ccsc_destroy(ccsc_ctx* ctx) {

@@ -7,6 +7,7 @@
 
 #include <rccl/rccl.h>
 
+#include <atomic>
 #include <condition_variable>
 #include <cstdio>
 #include <memory>
@@ -138,6 +139,19 @@ static int32_t host_group_fn(void* user, int32_t op, double* buf, int64_t count)
   auto* u = static_cast<HostGroupRank*>(user);
   return u->g->exchange(u->rank, op, buf, count);
 }
+
+// Failure state shared by the ranks of a multi-device context.  When one rank's
+// thread fails, abort_group() (engine.cpp) marks the group aborted ONCE, wakes the
+// in-process exchange and aborts every RCCL communicator, so the other ranks' blocked
+// collectives return; every later collective of the group throws instead of touching
+// a communicator.  `inflight` counts collectives between that check and their
+// enqueue, so the abort does not free a communicator under them.  The next
+// ccsc_learn on the context re-creates the communicators (reset_group).
+struct CommGroup {
+  std::mutex mu;
+  std::atomic<bool> aborted{false};
+  std::atomic<int> inflight{0};
+};
 }  // namespace ccsc
 
 struct ccsc_ctx {
@@ -154,4 +168,6 @@ struct ccsc_ctx {
   std::vector<ccsc_ctx*> subs;
   std::unique_ptr<ccsc::HostGroup> hg;           // repeated devices: in-process exchange
   std::vector<ccsc::HostGroupRank> hg_ranks;
+  std::vector<int32_t> devices;                  // the device list (ranks 0..ndev-1)
+  std::shared_ptr<ccsc::CommGroup> grp;          // parent and subs of a multi-device context
 };

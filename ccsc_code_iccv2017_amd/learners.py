@@ -85,6 +85,14 @@ class Context:
     def group(self):
         return len(getattr(self, "devices", ())) > 1
 
+    def comm_ranks(self):
+        """(ranks, transport) of the context's communicator (ccsc_comm_ranks): RCCL
+        reports ncclCommCount, "host" the host-staged transport, "none" one rank."""
+        eb = L.errbuf()
+        n, t = C.c_int32(0), C.c_int32(0)
+        L.check(self._lib.ccsc_comm_ranks(self.ptr, C.byref(n), C.byref(t), eb, len(eb)), eb)
+        return n.value, L.TRANSPORT[t.value]
+
     def close(self):
         if self.ptr:
             self._lib.ccsc_destroy(self.ptr)

@@ -73,6 +73,8 @@ def solve(variant, b, kernels, mask, lambda_residual, lambda_prior, max_it, tol,
         if multi and kernels.shape[2] != p.nch:
             raise ValueError("kernels must be [k, k, W, K] with W = size(b, 3)")
         if v3:
+            if psf is None:
+                raise ValueError("the video solver needs the blur psf")
             psf = _f64(psf)
             ps = list(psf.shape) + [1] * (3 - psf.ndim)
             for i in range(3):
@@ -89,6 +91,12 @@ def solve(variant, b, kernels, mask, lambda_residual, lambda_prior, max_it, tol,
         inp = L.SolveInputs()
         smooth_init = _f64(smooth_init)
         x_orig = _f64(x_orig)
+        # the library copies exactly b.size doubles of smooth_init and b.size / W of x_orig
+        if smooth_init is not None and smooth_init.size != b.size:
+            raise ValueError("smooth_init must have the size of b")
+        if x_orig is not None and x_orig.size != b.size // p.nch:
+            raise ValueError("x_orig must have the size of one channel of b")
+
         keep = [b, kernels, mask, smooth_init, psf, x_orig]
         inp.b, inp.kernels, inp.mask = L.dptr(b), L.dptr(kernels), L.dptr(mask)
         inp.smooth_init, inp.psf, inp.x_orig = L.dptr(smooth_init), L.dptr(psf), L.dptr(x_orig)

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define CCSC_ABI_VERSION 5
+#define CCSC_ABI_VERSION 6
 
 /* status codes */
 #define CCSC_OK 0
@@ -179,6 +179,15 @@ ccsc_ctx* ccsc_create_hostcomm(int32_t device, int32_t rank, int32_t nranks, ccs
  * (CCSC_E_UNSUPPORTED here).  ndev == 1 is ccsc_create(devices[0], 0, 1, NULL). */
 ccsc_ctx* ccsc_create_multi(const int32_t* devices, int32_t ndev, char* err, size_t errlen);
 void ccsc_destroy(ccsc_ctx* ctx);
+/* Ranks the context's communicator spans and its transport: RCCL reports
+ * ncclCommCount (of rank 0's communicator for a multi-device context), the host
+ * transport its nranks; a one-rank context reports 1 and NONE.  Evidence that a
+ * multi-GPU run exchanged over RCCL across the ranks it claims (bench.py). */
+#define CCSC_TRANSPORT_NONE 0
+#define CCSC_TRANSPORT_RCCL 1
+#define CCSC_TRANSPORT_HOST 2
+int32_t ccsc_comm_ranks(ccsc_ctx* ctx, int32_t* ranks, int32_t* transport, char* err,
+                        size_t errlen);
 
 /* ---- one-shot learner: the literal drop-in for the .m functions --------- */
 /* b: this rank's patches, [sb..., (U,V), n_local] column-major float64.

@@ -37,8 +37,8 @@ static void cleanup(void) {
 }
 
 /* the cached context when it serves the same device list, else a new one */
-static ccsc_ctx* context_for(const mxArray* a, char* err, size_t errlen) {
-  const mwSize nd = mxGetNumberOfElements(a);
+static ccsc_ctx* context_for(const mxArray* a, int first_only, char* err, size_t errlen) {
+  const mwSize nd = first_only && mxGetNumberOfElements(a) > 0 ? 1 : mxGetNumberOfElements(a);
   if (nd < 1 || nd > CCSC_MEX_MAXDEV)
     mexErrMsgIdAndTxt("ccsc:devices", "devices must list 1..%d GPU indices", CCSC_MEX_MAXDEV);
   int32_t devs[CCSC_MEX_MAXDEV];
@@ -109,7 +109,6 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
   }
 
   if (!mxIsDouble(prhs[10])) mexErrMsgIdAndTxt("ccsc:devices", "devices must be double");
-  ccsc_ctx* ctx = context_for(prhs[10], err, sizeof err);
   const double* d0 = mxIsEmpty(prhs[8]) ? NULL : mxGetDoubles(prhs[8]);
   const double* z0 = mxIsEmpty(prhs[9]) ? NULL : mxGetDoubles(prhs[9]);
 
@@ -119,6 +118,21 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
   const mwSize X = (mwSize)(p.sb[0] + 2 * r), Y = (mwSize)(p.sb[1] + 2 * r);
   const mwSize T = (mwSize)(p.ndim == 3 ? p.sb[2] + 2 * r : 1);
   const mwSize U = (mwSize)p.views[0], V = (mwSize)p.views[1];
+  /* the library copies exactly these many doubles from init.d / init.z: a wrong size
+   * is an error here, as MATLAB's own size checks would raise in the reference */
+  {
+    const mwSize nd0 = s * s * (p.ndim == 3 ? s : 1) * (variant == CCSC_L4D ? U * V : 1) * K;
+    const mwSize nz0 = X * Y * T * K * (variant == CCSC_DZPAR ? (mwSize)p.ni : n);
+    if (d0 && mxGetNumberOfElements(prhs[8]) != nd0)
+      mexErrMsgIdAndTxt("ccsc:args", "init.d must have %d elements", (int)nd0);
+    if (z0 && mxGetNumberOfElements(prhs[9]) != nz0)
+      mexErrMsgIdAndTxt("ccsc:args", "init.z must have %.0f elements", (double)nz0);
+    if ((d0 && (!mxIsDouble(prhs[8]) || mxIsComplex(prhs[8]))) ||
+        (z0 && (!mxIsDouble(prhs[9]) || mxIsComplex(prhs[9]))))
+      mexErrMsgIdAndTxt("ccsc:args", "init.d / init.z must be real double");
+  }
+  /* the 2-3D learner runs on one GPU (its d-solve couples every image per frequency) */
+  ccsc_ctx* ctx = context_for(prhs[10], variant == CCSC_HS23, err, sizeof err);
   mwSize dd[5], zd[6], xd[5];
   mwSize ndd, nzd, nxd;
   switch (variant) {

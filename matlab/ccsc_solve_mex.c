@@ -87,8 +87,18 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     p.verbose = !strcmp(v, "all") ? CCSC_VERBOSE_ALL : !strcmp(v, "brief") ? CCSC_VERBOSE_BRIEF
                                                                            : CCSC_VERBOSE_NONE;
   }
+  /* the library copies exactly numel(b) doubles of mask and smooth_init, numel(b)/W of
+   * x_orig and prod(size(psf)) of psf: a wrong size is an error here, as MATLAB's own
+   * size checks would raise in the reference */
   if (mxGetNumberOfElements(prhs[3]) != mxGetNumberOfElements(b))
     mexErrMsgIdAndTxt("ccsc:args", "mask must have the size of b");
+  if (!mxIsEmpty(prhs[9]) && mxGetNumberOfElements(prhs[9]) != mxGetNumberOfElements(b))
+    mexErrMsgIdAndTxt("ccsc:args", "smooth_init must have the size of b");
+  if (!mxIsEmpty(prhs[11]) &&
+      mxGetNumberOfElements(prhs[11]) != mxGetNumberOfElements(b) / (mwSize)p.nch)
+    mexErrMsgIdAndTxt("ccsc:args", "x_orig must have the size of one channel of b");
+  if (v3 && mxIsEmpty(prhs[10]))
+    mexErrMsgIdAndTxt("ccsc:args", "the video solver needs the blur psf");
   if (ccsc_solve_supported(&p, err, sizeof err)) mexErrMsgIdAndTxt("ccsc:invalid", "%s", err);
   ccsc_ctx* ctx = solve_context((int32_t)mxGetScalar(prhs[12]), err, sizeof err);
 

@@ -29,7 +29,7 @@ def test_every_header_symbol_is_exported(L):
     missing = [s for s in header_symbols() if not hasattr(lib, s)]
     assert not missing, missing
     assert set(header_symbols()) == set(L.SIGNATURES), "ctypes table out of sync with ccsc.h"
-    assert L.lib().ccsc_abi_version() == L.ABI_VERSION == 5
+    assert L.lib().ccsc_abi_version() == L.ABI_VERSION == 6
 
 
 def _problem(L, variant, sb=(100, 100), n=10000, K=100, psf=11, **kw):

@@ -131,3 +131,82 @@ def test_multi_device_context_rejects_sessions(gpu_ctx):
         assert "one-device context" in str(ei.value)
     finally:
         mctx.close()
+
+
+def _small_dz(seed=31, nblk=3):
+    rng = np.random.default_rng(seed)
+    ni, K, psf = 2, 3, 5
+    n = ni * nblk
+    b = rng.standard_normal((12, 11, n))
+    d0 = rng.standard_normal((psf, psf, K))
+    z0 = rng.standard_normal((16, 15, K, ni))
+    return (b, [psf, psf, K], 1.0, 1.0, 3, 0.0, "brief", {"d": d0, "z": z0}), ni
+
+
+@pytest.mark.parametrize("fail", ["1:1", "0:0", "1:0"])
+def test_failing_rank_aborts_group_and_context_recovers(gpu_ctx, monkeypatch, fail):
+    """One rank of a multi-device learn fails (test fault injection, CCSC_TEST_FAIL_RANK
+    = rank:outer) while the other is blocked in its next exchange: the call returns that
+    rank's error (no hang, no crash), and the SAME context then learns again and
+    matches the one-device result -- the MEX keeps its context cached across calls."""
+    from ccsc_code_iccv2017_amd import _lib as L
+    from ccsc_code_iccv2017_amd import learners as E
+    args, ni = _small_dz()
+    d1, z1, DZ1, it1 = E.admm_learn_conv2D_large_dzParallel(*args, ni=ni, ctx=gpu_ctx)
+    mctx = E.Context.multi([0, 0])
+    try:
+        assert mctx.comm_ranks() == (2, "host")
+        monkeypatch.setenv("CCSC_TEST_FAIL_RANK", fail)
+        with pytest.raises(L.CCSCError) as ei:
+            E.admm_learn_conv2D_large_dzParallel(*args, ni=ni, ctx=mctx)
+        assert "injected fault" in str(ei.value) and f"rank {fail.split(':')[0]}" in str(ei.value)
+        monkeypatch.delenv("CCSC_TEST_FAIL_RANK")
+        d2, z2, DZ2, it2 = E.admm_learn_conv2D_large_dzParallel(*args, ni=ni, ctx=mctx)
+    finally:
+        mctx.close()
+    np.testing.assert_allclose(d2, d1, rtol=0, atol=1e-10 * np.abs(d1).max())
+    np.testing.assert_allclose(z2, z1, rtol=0, atol=1e-10 * np.abs(z1).max())
+    np.testing.assert_allclose(it2["obj_vals_z"], it1["obj_vals_z"], rtol=1e-10)
+
+
+def test_one_rank_context_reports_no_transport(gpu_ctx):
+    assert gpu_ctx.comm_ranks() == (1, "none")
+
+
+def _visible_gpus():
+    import torch
+    return torch.cuda.device_count()
+
+
+@pytest.mark.skipif("_visible_gpus() < 2", reason="needs >= 2 GPUs (runs on the driver's 8-GPU node)")
+def test_distinct_devices_over_rccl_equal_one_device(gpu_ctx):
+    """ccsc_create_multi over distinct GPUs: ncclCommInitAll, RCCL all-reduce per
+    d-iteration and broadcast per outer iteration (dP:114-121, :143) -- the MATLAB
+    drop-in over a node.  ncclCommCount must report every device; the result equals
+    the one-device learn; an injected failure on the last rank aborts the
+    communicators and the context recovers with fresh ones."""
+    from ccsc_code_iccv2017_amd import _lib as L
+    from ccsc_code_iccv2017_amd import learners as E
+    ndev = min(_visible_gpus(), 8)
+    args, ni = _small_dz(nblk=ndev + 1)
+    d1, z1, DZ1, it1 = E.admm_learn_conv2D_large_dzParallel(*args, ni=ni, ctx=gpu_ctx)
+    mctx = E.Context.multi(list(range(ndev)))
+    try:
+        assert mctx.comm_ranks() == (ndev, "rccl")
+        d2, z2, DZ2, it2 = E.admm_learn_conv2D_large_dzParallel(*args, ni=ni, ctx=mctx)
+        np.testing.assert_allclose(d2, d1, rtol=0, atol=1e-10 * np.abs(d1).max())
+        np.testing.assert_allclose(z2, z1, rtol=0, atol=1e-10 * np.abs(z1).max())
+        np.testing.assert_allclose(DZ2, DZ1, rtol=0, atol=1e-10 * np.abs(DZ1).max())
+        np.testing.assert_allclose(it2["obj_vals_z"], it1["obj_vals_z"], rtol=1e-10)
+        os.environ["CCSC_TEST_FAIL_RANK"] = f"{ndev - 1}:1"
+        try:
+            with pytest.raises(L.CCSCError) as ei:
+                E.admm_learn_conv2D_large_dzParallel(*args, ni=ni, ctx=mctx)
+            assert "injected fault" in str(ei.value)
+        finally:
+            del os.environ["CCSC_TEST_FAIL_RANK"]
+        d3, _, _, _ = E.admm_learn_conv2D_large_dzParallel(*args, ni=ni, ctx=mctx)
+        assert mctx.comm_ranks() == (ndev, "rccl")
+        np.testing.assert_allclose(d3, d1, rtol=0, atol=1e-10 * np.abs(d1).max())
+    finally:
+        mctx.close()

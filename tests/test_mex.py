@@ -52,7 +52,8 @@ def _harness(path=HARNESS):
     from ccsc_code_iccv2017_amd import _lib as L
     L.lib()                       # libccsc first (one HIP runtime per process, _lib.lib)
     if not os.path.exists(path):
-        pytest.fail(f"{path} missing: run tests/mex_stub/build.sh")
+        pytest.skip(f"{path} missing: the test MEX harness did not build (tests/mex_stub/build.sh; "
+                    "test_gateway_compiles_warning_free reports why)")
     h = C.CDLL(path)
     P = C.c_void_p
     h.hx_double.restype = P
@@ -130,6 +131,13 @@ def test_mexfunction_matches_engine(gpu_ctx, devices):
         rc, err, _ = _call(h, 1, bad)
         assert rc == 1 and "ccsc:" in err
         h.hx_free(bad[1])
+        # init.d / init.z of the wrong size: an error before the library copies them
+        for slot, arr in ((8, d0[:, :, :-1]), (9, z0[..., :-1])):
+            bad = list(args)
+            bad[slot] = _mx(h, arr)
+            rc, err, _ = _call(h, 1, bad)
+            assert rc == 1 and "ccsc:args" in err and "init" in err, err
+            h.hx_free(bad[slot])
     finally:
         for a in args:
             h.hx_free(a)
@@ -174,6 +182,44 @@ def test_solve_mexfunction_matches_engine(gpu_ctx, name):
         rc, err, _ = _call(h, 1, bad)
         assert rc == 1 and "ccsc:" in err
         h.hx_free(bad[3])
+        # smooth_init / x_orig of the wrong size (the library would read past them)
+        for slot, key in ((9, "smooth_init"), (11, "x_orig")):
+            if key not in inp:
+                continue
+            bad = list(args)
+            bad[slot] = _mx(h, inp[key].ravel(order="F")[:-1])
+            rc, err, _ = _call(h, 1, bad)
+            assert rc == 1 and "ccsc:args" in err and key in err, err
+            h.hx_free(bad[slot])
+    finally:
+        for a in args:
+            h.hx_free(a)
+        h.hx_exit()
+
+
+@pytest.mark.gpu
+def test_mex_hs23_with_a_device_list_runs_on_one_device(gpu_ctx):
+    """The 2-3D learner through ccsc_mex with CCSC_DEVICES listing several GPUs: the
+    gateway builds a one-device context for it (its d-solve couples every image per
+    frequency), instead of a multi-device context the learner rejects."""
+    from ccsc_code_iccv2017_amd import learners as E
+    h = _harness()
+    rng = np.random.default_rng(43)
+    W, K, psf, n = 3, 4, 5, 2
+    b = np.abs(rng.standard_normal((10, 9, W, n))) + 0.1
+    smooth = 0.5 * b
+    d0 = rng.standard_normal((psf, psf, K))
+    z0 = rng.standard_normal((14, 13, K, n))
+    d_e, _, _, _ = E.admm_learn(b, [psf, psf, W, K], 1.0, 1.0, 2, 0.0, "none", {"d": d0, "z": z0},
+                                smooth, ctx=gpu_ctx)
+    args = [_mx(h, 4), _mx(h, b), _mx(h, [psf, psf, W, K]), _mx(h, 1.0), _mx(h, 1.0), _mx(h, 2),
+            _mx(h, 0.0), h.hx_string(b"none"), _mx(h, d0), _mx(h, z0), _mx(h, [0, 0]),
+            _mx(h, smooth)]
+    try:
+        rc, err, out = _call(h, 1, args)
+        assert rc == 0, err
+        np.testing.assert_allclose(_np(h, out[0]), d_e, rtol=0, atol=1e-10 * np.abs(d_e).max())
+        h.hx_free(out[0])
     finally:
         for a in args:
             h.hx_free(a)
