@@ -48,29 +48,63 @@ def cpu_model():
     return platform.processor() or "unknown"
 
 
+def cpu_threads():
+    """Threads the CPU baseline may use: the CPUs this process is allowed to run on,
+    bounded by the job's declared CPU share (OMP_NUM_THREADS; the GPU box grants 16
+    CPUs per GPU although nproc shows the whole machine)."""
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        avail = os.cpu_count() or 1
+    share = os.environ.get("OMP_NUM_THREADS", "")
+    return min(avail, int(share)) if share.isdigit() and int(share) > 0 else avail
+
+
 def cpu_baseline(args):
-    """Time the float64 NumPy/SciPy port on the host (bounded sample)."""
+    """SURVEY.md §8(d) CPU baseline: the float64 NumPy/SciPy port of the learner with
+    C1's constants (2D dParallel, rho_D = 500, 10 d-its, rho_Z = 50, threshold
+    lambda / 50, 10 z-its; K = 100 11x11, 100x100 patches, ni = 100), median of 2 outer
+    iterations (tol = 0, objective excluded), on ONE block of ni = 100 patches -- a C1
+    outer iteration is 10 such blocks (per-block precompute, d-solves and z-steps; the
+    consensus mean between them is 12,100 values), so C1 patch-iters/s = 10 ni /
+    (10 t_block) = ni / t_block.  The reference MATLAB cannot run here."""
     from oracle.ccsc_port import DzPort
     from ccsc_code_iccv2017_amd import synth
 
-    cores = min(16, os.cpu_count() or 1)
+    threads = cpu_threads()
     ni = 100
-    b = synth.images_2d(ni, device="cpu", seed=2017 + 2)
+    b = synth.images_2d(ni, device="cpu", seed=2017 + 0)
     rng = np.random.default_rng(11)
     d0 = rng.standard_normal((11, 11, 100))
     z0 = rng.standard_normal((110, 110, 100, ni))
-    port = DzPort(b, d0, z0, 1.0, ni=ni, workers=cores)
-    t0 = time.perf_counter()
-    port.outer()
-    dt = time.perf_counter() - t0
+    port = DzPort(b, d0, z0, 1.0, ni=ni, rho_d=500.0, rho_z=50.0, theta_div=50.0, max_it_d=10,
+                  max_it_z=10, workers=threads, replicate_z0=False)
+    ts = []
+    try:
+        from threadpoolctl import threadpool_limits
+        limit = threadpool_limits(limits=threads)   # BLAS / LAPACK threads
+    except ImportError:
+        import contextlib
+        limit = contextlib.nullcontext()
+    with limit:
+        for _ in range(2):
+            t0 = time.perf_counter()
+            port.outer()
+            ts.append(time.perf_counter() - t0)
+    dt = float(np.median(ts))
     return {
         "value": ni / dt,
         "unit": "patch-iters/s",
-        "cores": cores,
+        "cores": threads,
         "kind": "port",
-        "sample": f"1 outer iteration of dzParallel (5 d-its + 10 z-its, K=100, 11x11) on ONE "
-                  f"block of ni=100 synthetic 100x100 patches; oracle/ccsc_port.py float64, "
-                  f"scipy.fft workers={cores}, host CPU '{cpu_model()}', {dt:.1f} s",
+        "nproc": os.cpu_count(),
+        "cpu_model": cpu_model(),
+        "sample": f"C1 (2D dParallel: rho_D=500, 10 d-its, rho_Z=50, lambda/50, 10 z-its; K=100 "
+                  f"11x11, 100x100 synthetic local-CN patches) on ONE block of ni={ni} patches, "
+                  f"median of 2 outer iterations ({', '.join(f'{t:.1f}' for t in ts)} s); a C1 "
+                  f"outer iteration is 10 such blocks, so C1 patch-iters/s = ni / t_block; "
+                  f"oracle/ccsc_port.py float64, scipy.fft + BLAS on {threads} threads "
+                  f"(nproc {os.cpu_count()}), host CPU '{cpu_model()}'",
     }
 
 
@@ -78,24 +112,63 @@ def pmc_traffic(n_local):
     """HBM bytes per launch of the dominant z-step kernel from the committed rocprofv3
     PMC passes (FETCH_SIZE doubled for 16-B streaming loads on gfx950 and WRITE_SIZE,
     both kB per dispatch; MI355X_MICROARCH.md "HBM"), scaled to this run's patch count
-    when the profile was taken at another n.  Returns (bytes, source, kernel, stale):
-    stale is True when the kernel sources changed since the summary was taken
-    (tools/pmc_summary.py records their hash).  (None, ...) without a summary."""
+    when the profile was taken at another n, plus the SQ pass of the same kernel (VALU /
+    LDS activity, wave waits) that says what bounds it.  Returns (bytes, source, kernel,
+    stale, sq): stale is True when the kernel sources changed since the summary was
+    taken (tools/pmc_summary.py records their hash).  (None, ...) without a summary."""
     from tools.pmc_summary import source_hash
     try:
         d = json.load(open(PMC_SUMMARY))
     except (OSError, ValueError):
-        return None, None, None, None
+        return None, None, None, None, None
     cands = [(v.get("avg_s", 0) * v.get("dispatches", 0), name, v) for name, v in d.items()
              if name.startswith(ZKERNEL_PREFIX) and isinstance(v, dict)]
     if not cands:
-        return None, None, None, None
+        return None, None, None, None, None
     _, name, k = max(cands)
-    if "FETCH_SIZE" not in k or "WRITE_SIZE" not in k:
-        return None, None, None, None
-    per = (2.0 * k["FETCH_SIZE"] + k["WRITE_SIZE"]) * 1024.0 * n_local / d.get("n_local", n_local)
     stale = d.get("src_sha256") != source_hash()
-    return per, os.path.relpath(PMC_SUMMARY, ROOT), name, stale
+    sq = sq_limits(k)
+    if "FETCH_SIZE" not in k or "WRITE_SIZE" not in k:
+        return None, os.path.relpath(PMC_SUMMARY, ROOT), name, stale, sq
+    per = (2.0 * k["FETCH_SIZE"] + k["WRITE_SIZE"]) * 1024.0 * n_local / d.get("n_local", n_local)
+    return per, os.path.relpath(PMC_SUMMARY, ROOT), name, stale, sq
+
+
+def sq_limits(k):
+    """What bounds the kernel, from its SQ counters (per dispatch): SIMD-cycle shares of
+    VALU and LDS issue, and the wave-lifetime shares spent parked (s_waitcnt /
+    barrier) or issue-stalled.  SQ_WAVE_CYCLES / SQ_ACTIVE_INST_* / SQ_WAIT_* count
+    quad-cycles; the clock is GRBM_GUI_ACTIVE / 8 XCDs / kernel time
+    (MI355X_MICROARCH.md, cycle constants and DVFS)."""
+    need = ("SQ_WAVE_CYCLES", "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_LDS", "SQ_WAIT_ANY",
+            "SQ_WAIT_INST_ANY", "GRBM_GUI_ACTIVE")
+    if any(c not in k for c in need) or not k.get("sq_avg_s"):
+        return None
+    t = k["sq_avg_s"]
+    clk = k["GRBM_GUI_ACTIVE"] / 8.0 / t
+    simd_cycles = t * clk * 1024.0            # 256 CUs x 4 SIMDs
+    wc = k["SQ_WAVE_CYCLES"]
+    return {
+        "clock_GHz": clk / 1e9,
+        "valu_busy": 4.0 * k["SQ_ACTIVE_INST_VALU"] / simd_cycles,
+        "lds_busy": 4.0 * k["SQ_ACTIVE_INST_LDS"] / simd_cycles,
+        "wave_parked": k["SQ_WAIT_ANY"] / wc,
+        "wave_issue_stalled": k["SQ_WAIT_INST_ANY"] / wc,
+        "valu_insts_per_wave": k.get("SQ_INSTS_VALU", float("nan")) / max(k.get("SQ_WAVES", 1), 1),
+    }
+
+
+def limiter(frac_dram, sq):
+    """The measured bound: HBM when the DRAM traffic runs at >= 60% of peak, else the
+    busiest issue pipe if it is busy >= 50% of the SIMD cycles, else latency (waves
+    parked on memory / barriers)."""
+    if frac_dram is not None and frac_dram >= 0.6:
+        return "hbm"
+    if sq is None:
+        return "unmeasured"
+    if max(sq["valu_busy"], sq["lds_busy"]) >= 0.5:
+        return "valu" if sq["valu_busy"] >= sq["lds_busy"] else "lds"
+    return "latency"
 
 
 def step_alg_bytes(n, K, ni, P, F, mid, miz, s=8, V=1):
@@ -187,6 +260,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
+    comm_ranks, transport = ctx.comm_ranks()
     launches, zms, zbytes = sess.kernel_stats(0)
     kstats = {}
     for kid, name in enumerate(["zstep", "gram_chol", "dsolve", "dual_r2c", "c2r_dout"]):
@@ -207,15 +281,18 @@ def main():
     if rank == 0 and not (np.isfinite(obj) and obj < obj_start):
         log(f"WARNING: objective did not decrease: {obj_start:.6e} -> {obj:.6e}")
     avg_ms = zms / max(launches, 1)
-    achieved = zbytes / (avg_ms * 1e-3) / 1e9 if launches else 0.0
-    traffic, traffic_src, traffic_kernel, traffic_stale = pmc_traffic(n_local)
+    t_launch = avg_ms * 1e-3
+    traffic, traffic_src, traffic_kernel, traffic_stale, sq = pmc_traffic(n_local)
     if traffic_stale:
         log(f"WARNING: {traffic_src} predates the current kernel sources (traffic is stale)")
     r = psf // 2
     Pg, Fg = (100 + 2 * r) ** 2, (100 + 2 * r) * ((100 + 2 * r) // 2 + 1)
-    # compulsory HBM bytes of the fused z-step per launch: the state a read + written once
-    # (2 s P per slice) and the per-patch w read + written and B^ read (3 c F per patch)
+    # algorithmic bytes of the fused z-step per launch: every byte it must
+    # move once -- the state a read + written (2 s P per (patch, filter) slice) and, per
+    # patch, w read + written and B^ read (3 c F); the filter spectra (K c F) are shared
     compulsory = n_local * (K * 2 * 8 * Pg + 3 * 16 * Fg)
+    achieved = compulsory / t_launch / 1e9 if launches else 0.0
+    frac_dram = traffic / t_launch / 1e9 / HBM_PEAK_GBS if (traffic and launches) else None
     step_bytes = step_alg_bytes(args.n, K, ni, Pg, Fg, p.max_it_d, p.max_it_z)
     step_s = dt / max(done_steps, 1)
     result = {
@@ -242,8 +319,12 @@ def main():
             "parallelism": f"consensus blocks sharded over {world} rank(s); RCCL all-reduce "
                            f"per d-iteration, broadcast per outer iteration",
         },
+        # the communicator the engine actually exchanged over (ccsc_comm_ranks:
+        # ncclCommCount for RCCL) -- not WORLD_SIZE
+        "comm": {"transport": transport, "ranks": comm_ranks},
+        "rccl_ranks": comm_ranks if transport == "rccl" else None,
         "roofline": {
-            "bound": "hbm",
+            "bound": limiter(frac_dram, sq),
             "kernel": "z-step (C2R of the w term + prox/dual + R2C + per-bin reduction, one WG/patch)",
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
@@ -253,18 +334,18 @@ def main():
             "traffic_source": traffic_src,
             "traffic_kernel": traffic_kernel,
             "traffic_stale": traffic_stale,
-            "alg_bytes_per_launch": zbytes,
+            "alg_bytes_per_launch": compulsory,
             "avg_launch_ms": avg_ms,
-            # the fused kernel moves less than §8(d)'s staged model: its own compulsory bytes
-            # and the PMC-measured DRAM bytes against the same peak
-            "compulsory_bytes_per_launch": compulsory,
-            "frac_compulsory": compulsory / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if launches else None,
-            "frac_dram": (traffic / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
-                          if (traffic and launches) else None),
-            "observed_limiter": "fp64 VALU + LDS (slice FFTs in LDS, DESIGN.md §7)",
+            "frac_dram": frac_dram,
+            "sq": sq,
+            # SURVEY.md §8(d)'s staged z-iteration model (n K (4sP + 4cF) + n c F): it
+            # counts every stage's operands through HBM, which the fused kernel never
+            # moves, so its fraction exceeds 1 -- kept for continuity, not the roofline
+            "s8d_bytes_per_launch": zbytes,
+            "frac_s8d": zbytes / t_launch / 1e9 / HBM_PEAK_GBS if launches else None,
             # whole outer iteration: §8(d) bytes of every stage / step time / node peak
             "step_alg_bytes": step_bytes,
-            "step_frac": step_bytes / step_s / 1e9 / (HBM_PEAK_GBS * world),
+            "step_frac_s8d": step_bytes / step_s / 1e9 / (HBM_PEAK_GBS * world),
         },
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

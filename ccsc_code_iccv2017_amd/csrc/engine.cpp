@@ -271,6 +271,10 @@ static void resolve_problem(ccsc_problem& p) {
   if (p.precision != CCSC_FP64 && p.precision != CCSC_FP32) throw Err(CCSC_E_INVALID, "bad precision");
   if (p.dfactor < CCSC_DFACTOR_AUTO || p.dfactor > CCSC_DFACTOR_WOODBURY)
     throw Err(CCSC_E_INVALID, "bad dfactor");
+  // AUTO resolves to the form the consensus learners will run (observable through
+  // ccsc_resolve): the ni x ni Woodbury factor for blocks of few patches, else K x K
+  if (p.variant != CCSC_HS23 && p.dfactor == CCSC_DFACTOR_AUTO)
+    p.dfactor = woodbury_fits(p.K, p.ni) ? CCSC_DFACTOR_WOODBURY : CCSC_DFACTOR_CHOLESKY;
   const int r = p.psf / 2;
   for (int i = 0; i < p.ndim; ++i)
     if (p.sb[i] + 2 * r < p.psf) throw Err(CCSC_E_INVALID, "grid smaller than the filter");

@@ -132,6 +132,135 @@ def images_2d(n: int, size=(100, 100), K: int = 100, psf: int = 11, seed: int = 
     return out
 
 
+def _sparse_codes(shape, density, g, device):
+    mask = torch.rand(shape, generator=g, device=device) < density
+    return (torch.randn(shape, generator=g, device=device) * mask).to(torch.float32)
+
+
+def _single(t: torch.Tensor) -> torch.Tensor:
+    """Stored as single, then widened (the reference's datasets are single: CI:367,
+    learn_kernels_4D_extract_patches.m:16-53)."""
+    return t.to(torch.float32).to(torch.float64)
+
+
+def clips_3d(n: int, size=(64, 64, 32), K: int = 49, psf: int = 11, seed: int = 2017 + 3,
+             density: float = 0.002, noise: float = 0.01, device: str = "cpu",
+             chunk: int = 8) -> np.ndarray:
+    """Synthetic video clips for the 3D learner (config C4), MATLAB layout [x, y, t, n].
+
+    b_raw = sum_k d*_k (*) z*_k + noise ('valid' 3D convolution of sparse codes with K
+    zero-mean unit-norm psf^3 filters), then the local contrast normalisation of every
+    frame -- the reference's clips are crops of a frame-wise local-CN movie
+    (learn_kernels_3D.m:12, extractContrastNormalizatonMovie.m:30)."""
+    rng = np.random.default_rng(seed)
+    d = make_filters(K, psf, 3, rng)                         # [K, x, y, t]
+    X, Y, T = size
+    G = (T + psf - 1, Y + psf - 1, X + psf - 1)               # codes' support, torch order (t, y, x)
+    # the 'valid' 3D convolution as a circular one on the codes' grid (its outputs at
+    # indices >= psf - 1 never wrap): filters zero-padded to G, one rfftn each
+    dpad = np.zeros((K,) + G)
+    dpad[:, :psf, :psf, :psf] = d.transpose(0, 3, 2, 1)
+    dh = torch.fft.rfftn(torch.as_tensor(dpad, device=device), dim=(1, 2, 3))
+    out = np.empty((X, Y, T, n), order="F")
+    for c0 in range(0, n, chunk):
+        m = min(chunk, n - c0)
+        g = torch.Generator(device=device).manual_seed(seed * 1000003 + c0 // chunk)
+        codes = _sparse_codes((m, K) + G, density, g, device).double()
+        zh = torch.fft.rfftn(codes, dim=(2, 3, 4))
+        del codes
+        full = torch.fft.irfftn((zh * dh[None]).sum(dim=1), s=G, dim=(1, 2, 3))
+        del zh
+        raw = full[:, psf - 1:, psf - 1:, psf - 1:]           # [m, T, Y, X]
+        raw = raw + noise * torch.randn(raw.shape, generator=g, device=device, dtype=torch.float64)
+        frames = raw.reshape(m * T, Y, X).transpose(1, 2)     # [m T, X(rows), Y]
+        cn = local_cn(frames.contiguous()).reshape(m, T, X, Y)
+        out[:, :, :, c0:c0 + m] = cn.permute(2, 3, 1, 0).cpu().numpy()
+    return out
+
+
+def lightfields_4d(n: int, size=(64, 64), views: int = 5, K: int = 49, psf: int = 11,
+                   seed: int = 2017 + 4, density: float = 0.002, noise: float = 0.01,
+                   device: str = "cpu", chunk: int = 16) -> np.ndarray:
+    """Synthetic light fields for the 4D learner (config C5), MATLAB layout
+    [x, y, U, V, n], single precision widened to double like the reference's patches.
+
+    Every view (u, v) sees the same sparse codes through its own slice of the K
+    filters d*_k(x, y, u, v) (spatial convolution only, the model of L4:18-21); each
+    view image is then locally contrast normalised (the reference's light fields are
+    local-CN data, learn_kernels_4D.m:10-12)."""
+    rng = np.random.default_rng(seed)
+    U = V = views
+    d = rng.standard_normal((K, psf, psf, U, V))
+    d -= d.mean(axis=(1, 2), keepdims=True)
+    d /= np.sqrt((d ** 2).sum(axis=(1, 2), keepdims=True))  # unit norm per (u, v, k) slice
+    # conv2d weight [U V, K, y, x] (output channel = view, u fastest as MATLAB's layout)
+    wt = d.transpose(4, 3, 0, 2, 1).reshape(V * U, K, psf, psf)[:, :, ::-1, ::-1]
+    w = torch.as_tensor(np.ascontiguousarray(wt), dtype=torch.float32, device=device)
+    X, Y = size
+    out = np.empty((X, Y, U, V, n), order="F")
+    for c0 in range(0, n, chunk):
+        m = min(chunk, n - c0)
+        g = torch.Generator(device=device).manual_seed(seed * 1000003 + c0 // chunk)
+        codes = _sparse_codes((m, K, Y + psf - 1, X + psf - 1), density, g, device)
+        raw = Fnn.conv2d(codes, w).double()                   # [m, V U, Y, X]
+        del codes
+        raw = raw + noise * torch.randn(raw.shape, generator=g, device=device, dtype=torch.float64)
+        imgs = raw.reshape(m * U * V, Y, X).transpose(1, 2).contiguous()
+        cn = _single(local_cn(imgs)).reshape(m, V, U, X, Y)
+        out[..., c0:c0 + m] = cn.permute(3, 4, 2, 1, 0).cpu().numpy()
+    return out
+
+
+def gauss_symmetric(b: np.ndarray, size: int = 13, sigma: float = 3 * 1.591,
+                    device: str = "cpu") -> np.ndarray:
+    """imfilter(b, fspecial('gaussian', 13, 3*1.591), 'same', 'conv', 'symmetric') over
+    the first two dims of b (learn_hyperspectral.m:15-16): mirror padding that repeats
+    the edge sample."""
+    k = fspecial_gaussian(size, sigma)
+    h = (size - 1) // 2
+    X, Y = b.shape[:2]
+    rest = b.shape[2:]
+    t = torch.as_tensor(np.ascontiguousarray(b.reshape(X, Y, -1, order="F").transpose(2, 1, 0)),
+                        device=device)                        # [m, Y, X]
+    ix = torch.as_tensor(np.pad(np.arange(X), h, mode="symmetric"), device=device)
+    iy = torch.as_tensor(np.pad(np.arange(Y), h, mode="symmetric"), device=device)
+    t = t[:, iy][:, :, ix]
+    kk = torch.as_tensor(np.ascontiguousarray(k.T[::-1, ::-1]), dtype=t.dtype, device=device)
+    o = Fnn.conv2d(t[:, None], kk[None, None])[:, 0]          # [m, Y, X]
+    return np.asfortranarray(o.permute(2, 1, 0).cpu().numpy().reshape((X, Y) + rest, order="F"))
+
+
+def cubes_23(n: int, size=(100, 100), W: int = 31, K: int = 100, psf: int = 11,
+             seed: int = 2017 + 2, density: float = 0.002, noise: float = 0.01,
+             device: str = "cpu", chunk: int = 8):
+    """Synthetic hyperspectral cubes for the 2-3D learner (config C3), MATLAB layout
+    [x, y, W, n], and their smooth_init.  b(x, y, w) = sum_k d*_k(., ., w) (*) z*_k(x, y)
+    + noise (one code map per atom shared by the W wavelengths, the model of
+    L23:302-324), shifted and scaled to [0.05, 1]: "similarly normalized but not
+    contrast normalized" nonnegative data (learn_hyperspectral.m:9-11), so max(b) > 0
+    as gamma_heuristic needs (L23:36).  smooth_init = the 13x13 Gaussian low-pass of b
+    with symmetric padding (learn_hyperspectral.m:15-16)."""
+    rng = np.random.default_rng(seed)
+    d = rng.standard_normal((K, psf, psf, W))
+    d -= d.mean(axis=(1, 2, 3), keepdims=True)
+    d /= np.sqrt((d ** 2).sum(axis=(1, 2, 3), keepdims=True))
+    wt = d.transpose(3, 0, 2, 1)[:, :, ::-1, ::-1]           # [W, K, y, x]
+    w = torch.as_tensor(np.ascontiguousarray(wt), dtype=torch.float32, device=device)
+    X, Y = size
+    raw = np.empty((X, Y, W, n), order="F")
+    for c0 in range(0, n, chunk):
+        m = min(chunk, n - c0)
+        g = torch.Generator(device=device).manual_seed(seed * 1000003 + c0 // chunk)
+        codes = _sparse_codes((m, K, Y + psf - 1, X + psf - 1), density, g, device)
+        r_ = Fnn.conv2d(codes, w).double()                    # [m, W, Y, X]
+        del codes
+        r_ = r_ + noise * torch.randn(r_.shape, generator=g, device=device, dtype=torch.float64)
+        raw[..., c0:c0 + m] = r_.permute(3, 2, 1, 0).cpu().numpy()
+    lo, hi = raw.min(), raw.max()
+    b = np.asfortranarray(0.05 + 0.95 * (raw - lo) / (hi - lo))
+    return b, gauss_symmetric(b, device=device)
+
+
 def init_2d(kernel_size, size_z, seed: int = 7):
     """d0 = randn(kernel_size); z0 = randn(size_z) (dP:38,45 draw order)."""
     rng = np.random.default_rng(seed)

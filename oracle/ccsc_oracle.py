@@ -130,19 +130,25 @@ def crop_filters(D, ndim_spatial, psf_radius):
 # ----------------------------------------------------------------------------
 # Per-frequency solves (literal restatements).
 # ----------------------------------------------------------------------------
-def precompute_H_hat_D(z_hat_block, ss, k, ni, rho, rep_views=1):
+def precompute_H_hat_D(z_hat_block, ss, k, ni, rho, rep_views=1, factored=False):
     """dP:221-237.  Returns (zhat_mat [ss, ni, k], zhat_inv_mat [ss, k, k]).
 
     zhat_mat{f} = permute(reshape(z_hat, [ss, k, ni]), [3,2,1]) -> ni x k.
     zhat_inv_mat{f} = 1/rho*eye(k) - 1/rho*A'*pinv(rho*eye(ni) + A*A')*A.
     ``rep_views`` > 1 restates L4:252 (repmat over the 5x5 views: the same
     matrix repeated once per view, frequency index = spatial + ss_sp*view).
+    ``factored``: zhat_inv_mat is kept as the reference's own factors (rho, pinv(rho I
+    + A A')) and applied right to left in solve_conv_term_D -- the same formula without
+    the ss x k x k array (8.8 GB on C4's 74x74x42 grid at K = 49).
     """
     zh = _F(z_hat_block, (ss, k, ni))
     A = np.transpose(zh, (0, 2, 1))                     # [ss, ni, k]
     AH = np.conj(np.transpose(A, (0, 2, 1)))            # [ss, k, ni]
     M = rho * np.eye(ni)[None] + A @ AH                 # [ss, ni, ni]
     P = np.linalg.pinv(M)
+    if factored:
+        assert rep_views == 1
+        return A, ("pinv", rho, P)
     inv = (np.eye(k)[None] - AH @ P @ A) / rho          # [ss, k, k]
     if rep_views > 1:
         A = np.concatenate([A] * rep_views, axis=0)
@@ -157,7 +163,13 @@ def solve_conv_term_D(zhat_mat, zhat_inv_mat, d_rhs_hat, B_block_hat, rho, spati
     xi2 = _F(d_rhs_hat, (ss, k))
     AH = np.conj(np.transpose(zhat_mat, (0, 2, 1)))
     rhs = np.einsum("fkp,fp->fk", AH, xi1) + rho * xi2
-    x = np.einsum("fkj,fj->fk", zhat_inv_mat, rhs)
+    if isinstance(zhat_inv_mat, tuple):                 # factored: (I - A' P A) rhs / rho
+        _, rho_f, P = zhat_inv_mat
+        t = np.einsum("fpk,fk->fp", zhat_mat, rhs)
+        t = np.einsum("fpq,fq->fp", P, t)
+        x = (rhs - np.einsum("fkp,fp->fk", AH, t)) / rho_f
+    else:
+        x = np.einsum("fkj,fj->fk", zhat_inv_mat, rhs)
     return _F(x, tuple(spatial_shape) + (k,))
 
 
@@ -457,7 +469,7 @@ def _objective_nd(z, dhat, b, lambda_residual, lambda_prior, r, nsp):
 
 def learn_3d(b, kernel_size, lambda_residual, lambda_prior, max_it, tol, verbose, init, *,
              ni=None, max_it_d=10, max_it_z=10, rho_d=5000.0, rho_z=1.0, theta_div=1.0,
-             trace_objective=False):
+             trace_objective=False, factored=False):
     """Restatement of admm_learn_conv3D_large (L3:1-230).  ni = sqrt(n) (L3:11)."""
     b = np.asarray(b, dtype=np.float64)
     k = kernel_size[-1]
@@ -497,7 +509,8 @@ def learn_3d(b, kernel_size, lambda_residual, lambda_prior, max_it, tol, verbose
     for i in range(max_it):                                       # L3:100
         zm, zi = [], []
         for nn in range(N):                                       # L3:106-110
-            A, S = precompute_H_hat_D(z_hat[..., nn * ni:(nn + 1) * ni], ss, k, ni, rho_d)
+            A, S = precompute_H_hat_D(z_hat[..., nn * ni:(nn + 1) * ni], ss, k, ni, rho_d,
+                                      factored=factored)
             zm.append(A)
             zi.append(S)
         od, zd = [], []

@@ -29,6 +29,22 @@ def test_precompute_D_is_regularised_normal_inverse():
         np.testing.assert_allclose(S[f], np.linalg.inv(G), rtol=1e-10, atol=1e-14)
 
 
+def test_factored_pinv_form_equals_explicit_inverse():
+    """precompute_H_hat_D(factored=True) keeps (rho, pinv(rho I + A A')) and applies
+    (I - A' P A) / rho right to left: the same dP:235 / dP:270 formula as the explicit
+    K x K array (the C4-grid parity case needs it: 8.8 GB otherwise)."""
+    rng = _rng(7)
+    X, Y, K, ni, rho = 6, 5, 9, 2, 5000.0
+    zh = rng.standard_normal((X, Y, K, ni)) + 1j * rng.standard_normal((X, Y, K, ni))
+    Bb = rng.standard_normal((X, Y, ni)) + 1j * rng.standard_normal((X, Y, ni))
+    c = rng.standard_normal((X, Y, K)) + 1j * rng.standard_normal((X, Y, K))
+    A, S = O.precompute_H_hat_D(zh, X * Y, K, ni, rho)
+    A2, S2 = O.precompute_H_hat_D(zh, X * Y, K, ni, rho, factored=True)
+    x = O.solve_conv_term_D(A, S, c, Bb, rho, [X, Y], K, ni)
+    x2 = O.solve_conv_term_D(A2, S2, c, Bb, rho, [X, Y], K, ni)
+    np.testing.assert_allclose(x2, x, rtol=1e-12, atol=1e-15 * np.abs(x).max())
+
+
 def test_solve_D_satisfies_normal_equations():
     """solve_conv_term_D (dP:252-276): (A^H A + rho I) x = A^H b + rho c per frequency."""
     rng = _rng(2)

@@ -66,6 +66,10 @@ def reference_norms():
         "2D/Filters/Filters_ours_2D_large.mat": (2, 0.01),
         "3D/Filters/3D_video_filters.mat": (3, 0.01),
         "4D/Filters/4d_filters_lightfield.mat": (2, 0.01),
+        # the 2-3D learner projects every (wavelength, atom) 11x11 slice (L23:246); its
+        # d_res is the d-solve output (L23:126, 231), not the projected split, so it
+        # spreads wider around the sphere (0.9954 .. 1.0250)
+        "2-3D/Filters/2D-3D-Hyperspectral.mat": (2, 0.03),
     }
     for rel, (nsp, tol) in spec.items():
         path = os.path.join(REF, rel)
@@ -76,6 +80,12 @@ def reference_norms():
         out[rel] = {"shape": list(d.shape), "norms": [round(float(x), 6) for x in norms],
                     "tol": tol}
     return out
+
+
+def write_reference_norms():
+    norms = reference_norms()
+    if norms:
+        json.dump(norms, open(os.path.join(GOLD, "reference_filter_norms.json"), "w"), indent=0)
 
 
 def solver_fixture(name):
@@ -96,12 +106,13 @@ if __name__ == "__main__":
         solver_fixture(nm)
     if "--solvers" in sys.argv:
         sys.exit(0)
+    if "--norms" in sys.argv:
+        write_reference_norms()
+        sys.exit(0)
     learner_fixture("dp_small", "dp", (12, 12), 5, 3, 4, 2, 2, 101)
     learner_fixture("dz_small", "dz", (12, 12), 5, 3, 4, 2, 2, 102)
     learner_fixture("dp_odd", "dp", (11, 10), 5, 3, 6, 3, 2, 103)
     learner_fixture("dz_110", "dz", (100, 100), 11, 2, 2, 1, 1, 104)
     hs_fixture("hs_small", (10, 9), 3, 5, 4, 3, 1.0, 2, 105)
-    norms = reference_norms()
-    if norms:
-        json.dump(norms, open(os.path.join(GOLD, "reference_filter_norms.json"), "w"), indent=0)
+    write_reference_norms()
     print("fixtures:", sorted(os.listdir(GOLD)))

@@ -53,7 +53,13 @@ if __name__ == "__main__":
                   "src_sha256": source_hash()}
         for p in args[3:]:
             for k, d in summarize(p).items():
-                merged.setdefault(k, {}).update(d)
+                m = merged.setdefault(k, {})
+                if any(c.startswith("SQ_") for c in d):
+                    # the SQ pass's own kernel time (its clock = GRBM_GUI_ACTIVE / 8 / time)
+                    d = dict(d)
+                    d["sq_avg_s"] = d.pop("avg_s")
+                    d.pop("dispatches", None)
+                m.update(d)
         json.dump(merged, open(out, "w"), indent=1)
         sys.exit(0)
     for p in args:
