@@ -104,11 +104,14 @@ def _run_session(ctx, p, b, d0, outer, smooth_init=None):
     return np.array(objs), d_res
 
 
-def _check_objective(objs, expect0, what, strict=True):
+def _check_objective(objs, expect0, what, strict=True, rtol0=2e-3):
+    """rtol0 ~ 5 standard deviations of the iteration-0 objective over the random init
+    (Monte Carlo on the host with the same d0: C5's 17M code entries through 25 views
+    of one fixed filter set spread 1.1e-3; C2/C3/C4 draw 10^8 - 10^9 entries)."""
     print(f"{what}: objective {objs[0]:.6e} (closed form {expect0:.6e}) -> {objs[-1]:.6e} "
           f"after {len(objs) - 1} outer iterations")
     assert np.all(np.isfinite(objs))
-    assert abs(objs[0] / expect0 - 1) < 2e-3, (objs[0], expect0)
+    assert abs(objs[0] / expect0 - 1) < rtol0, (objs[0], expect0)
     assert objs[1] < objs[0], objs
     assert objs[-1] < objs[1] if strict else objs[-1] <= objs[1], objs
 
@@ -152,7 +155,7 @@ def test_c5_fullsize_20_iterations(gpu_ctx):
     X = sb[0] + 2 * (psf // 2)
     expect0 = 0.5 * (n * sb[0] * sb[1] * float((d0 ** 2).sum()) + float((b ** 2).sum())) \
         + math.sqrt(2 / math.pi) * n * K * X * X
-    _check_objective(objs, expect0, "C5")
+    _check_objective(objs, expect0, "C5", rtol0=6e-3)
     norms = np.sqrt((d_res ** 2).sum(axis=(0, 1)))              # per (u, v, k) slice (L4:224-225)
     ref = np.array(_ref_norms("4D/Filters/4d_filters_lightfield.mat")["norms"])
     print(f"C5 filter norms {norms.min():.6f} .. {norms.max():.6f} "

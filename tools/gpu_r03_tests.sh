@@ -6,7 +6,7 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 out=gpurun_out/$tag
 mkdir -p $out
 sel=${2:-tests}
-timeout -k 10 1100 python -u -m pytest $sel -m gpu -v -rs --timeout 300 --timeout-method thread \
+timeout -k 10 1100 python -u -m pytest $sel -m gpu -v -rsP --timeout 300 --timeout-method thread \
     > $out/pytest_gpu.txt 2>&1
 rc=$?
 tail -5 $out/pytest_gpu.txt
