@@ -22,6 +22,11 @@
 
 #include "common.hpp"
 
+// DFT of size 2 M (M odd) as a prime-factor split (dft_sink); -DCCSC_DFT_PFA=0 for A/B
+#ifndef CCSC_DFT_PFA
+#define CCSC_DFT_PFA 1
+#endif
+
 #include <utility>
 
 namespace ccsc {
@@ -122,6 +127,22 @@ __device__ __forceinline__ void dft_sink(cpx<T> (&v)[R], Sink&& sink) {
     sink(2, csub(a0, b0));
     sink(1, cadd(a1, b1i));
     sink(3, csub(a1, b1i));
+#if CCSC_DFT_PFA
+  } else if constexpr (R % 4 == 2 && R > 2) {
+    // R = 2 M, M odd: prime-factor (Good-Thomas) split, no twiddles -- input
+    // n = (M n1 + 2 n2) mod R, output k = (M k1 + (M + 1) k2) mod R; M two-point
+    // butterflies then two M-point DFTs (DFT-10: 92 instead of 124 flops)
+    constexpr int M = R / 2;
+    cpx<T> e[M], o[M];
+    sfor<M>([&](auto i) {
+      constexpr int n2 = decltype(i)::value;
+      constexpr int ia = (2 * n2) % R, ib = (M + 2 * n2) % R;
+      e[n2] = cadd(v[ia], v[ib]);
+      o[n2] = csub(v[ia], v[ib]);
+    });
+    dft_sink<T, M, SIGN>(e, [&](int k2, cpx<T> val) { sink(((M + 1) * k2) % R, val); });
+    dft_sink<T, M, SIGN>(o, [&](int k2, cpx<T> val) { sink((M + (M + 1) * k2) % R, val); });
+#endif
   } else {
     constexpr int H = (R - 1) / 2;
     constexpr bool EVEN = (R % 2) == 0;

@@ -59,20 +59,27 @@
 #define CCSC_ZL_WLDS 1
 #endif
 
+// timing-only ablations (wrong results; tools/gpu_ab_zl.sh): CCSC_ABL_NODK replaces the
+// per-slice filter-spectrum loads (dcorr_k, dhat_k: L2 hits) by register constants,
+// CCSC_ABL_NOSTATE drops the state stream (HBM; _NOSTLOAD / _NOSTSTORE only its loads /
+// stores), CCSC_ABL_NOBAR the workgroup barriers
+
 namespace ccsc {
 
 #if CCSC_ZL_WLDS
 constexpr int kZlWL = 7;   // waves whose w bins stay in LDS (35 columns x 110 bins, 61.6 KB)
-constexpr size_t kZlSmem = zl::kSmem + (size_t)kZlWL * 5 * zl::Y * 16;
+constexpr size_t kZlWBytes = (size_t)kZlWL * 5 * zl::Y * 16;
 #else
-constexpr size_t kZlSmem = zl::kSmem;
+constexpr size_t kZlWBytes = 0;
 #endif
+constexpr size_t kZlSmem = zl::kSmem + kZlWBytes;
 static_assert(kZlSmem <= 160 * 1024, "z-step LDS");
 
 template <typename T>
 __device__ __forceinline__ T soft_l(T a, T theta) {
   return (fabs(a) > theta) ? a - copysign(theta, a) : (T)0;
 }
+
 
 __device__ __forceinline__ void wave_lds_fence() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -111,6 +118,16 @@ __device__ __forceinline__ void inv_line(cpx<T> (&in)[10], cpx<T>* E, int s, Sin
   dft_sink<T, 11, +1>(v, sink);
 }
 
+__device__ __forceinline__ void zl_sync() {
+#ifdef CCSC_ABL_NOBAR
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#else
+  lds_sync();
+#endif
+}
+
 // (e mod 110) for 0 <= e < 220
 __device__ __forceinline__ int mod110(int e) { return e >= 110 ? e - 110 : e; }
 // slot of element x of a row pair's spectrum Z_j in layout-B order (k1*11 + k2)
@@ -122,6 +139,19 @@ template <typename V>
 __device__ __forceinline__ V zld(const void* base, uint32_t boff) {
   return *reinterpret_cast<const V*>(reinterpret_cast<const char*>(base) + boff);
 }
+// the per-slice filter-spectrum loads (dcorr_k, dhat_k)
+template <typename V>
+__device__ __forceinline__ V dld(const void* base, uint32_t boff) {
+#ifdef CCSC_ABL_NODK
+  V v;
+  v.x = 1e-3 * (double)(boff & 255);
+  v.y = 1e-3;
+  (void)base;
+  return v;
+#else
+  return zld<V>(base, boff);
+#endif
+}
 template <typename V>
 __device__ __forceinline__ void zst(void* base, uint32_t boff, V v) {
   *reinterpret_cast<V*>(reinterpret_cast<char*>(base) + boff) = v;
@@ -131,7 +161,13 @@ __device__ __forceinline__ void zst(void* base, uint32_t boff, V v) {
 typedef double nt_d2 __attribute__((ext_vector_type(2)));
 template <typename V>
 __device__ __forceinline__ V sld(const void* base, uint32_t boff) {
-#if CCSC_ZL_NT
+#if defined(CCSC_ABL_NOSTATE) || defined(CCSC_ABL_NOSTLOAD)
+  V s;
+  s.x = 1e-3 * (double)(boff & 255);
+  s.y = -s.x;
+  (void)base;
+  return s;
+#elif CCSC_ZL_NT
   const nt_d2 r = __builtin_nontemporal_load(
       reinterpret_cast<const nt_d2*>(reinterpret_cast<const char*>(base) + boff));
   V v;
@@ -144,7 +180,9 @@ __device__ __forceinline__ V sld(const void* base, uint32_t boff) {
 }
 template <typename V>
 __device__ __forceinline__ void sst(void* base, uint32_t boff, V v) {
-#if CCSC_ZL_NT
+#if defined(CCSC_ABL_NOSTATE) || defined(CCSC_ABL_NOSTSTORE)
+  if (v.x == 12345.678) zst<V>(base, boff, v);   // keeps the value live, never stores
+#elif CCSC_ZL_NT
   const nt_d2 r = {v.x, v.y};
   __builtin_nontemporal_store(r, reinterpret_cast<nt_d2*>(reinterpret_cast<char*>(base) + boff));
 #else
@@ -238,7 +276,7 @@ __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn
 #pragma unroll
       for (int k1 = 0; k1 < 10; ++k1)
 #if CCSC_ZL_WLDS
-        b[k1] = cmulc(zld<cpx<T>>(dk, bo + k1 * 616 * 16),
+        b[k1] = cmulc(dld<cpx<T>>(dk, bo + k1 * 616 * 16),
                       wl ? sW[k1 * 385 + c * 11 + sb] : zld<cpx<T>>(Wp, bo + k1 * 616 * 16));
 #else
         b[k1] = cmulc(zld<cpx<T>>(dk, bo + k1 * 616 * 16), zld<cpx<T>>(Wp, bo + k1 * 616 * 16));
@@ -246,7 +284,7 @@ __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn
       inv_line<T, zl::RS>(b, Ey, sb, [&](int n2, cpx<T> val) {
         sT[mod110(11 * sa + 10 * n2) * zl::RS + c] = val;
       });
-      lds_sync();   // P2
+      zl_sync();   // P2
       if (xwave) {
         // ---- P3: x-C2R of row pair j: Z(x) = R_2j(x) + i R_2j+1(x), Hermitian ext. ----
         const int s3 = fresh(sb);
@@ -349,7 +387,7 @@ __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn
       cpx<T>* r0 = sT + 2 * j * zl::RS;   // Z_j in layout-B slot order (zslot)
       fwd_line<T, 1>(zc, Ex, s5, [&](int k1, cpx<T> val) { r0[k1 * 11 + s5] = val; });
     }
-    lds_sync();   // P6
+    zl_sync();   // P6
     // ---- P7: column c, rows y = n1 + 10 n2: two-for-one separation ----
     cpx<T> col[11];
     {
@@ -367,14 +405,14 @@ __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn
         col[n2] = {odd ? ox : ex, odd ? oy : ey};
       }
     }
-    lds_sync();   // P8
+    zl_sync();   // P8
     // ---- P9: y-R2C of column c -> bins, accumulate sum_k dhat_k C_k ----
     {
       const int s9 = fresh(sb);
       const cpx<T>* dk = dhat + (int64_t)k * zl::F;
       const uint32_t bo = (uint32_t)(c * 11 + s9) * 16u;
       fwd_line<T, zl::RS>(col, Ey, s9, [&](int k1, cpx<T> cb) {
-        acc[k1] = cadd(acc[k1], cmul(zld<cpx<T>>(dk, bo + k1 * 616 * 16), cb));
+        acc[k1] = cadd(acc[k1], cmul(dld<cpx<T>>(dk, bo + k1 * 616 * 16), cb));
       });
     }
   }
