@@ -796,11 +796,17 @@ struct Session2D {
                                     supp.as<double>(), dnorm.as<double>(), owner0 ? KG : 0,
                                     1.0 / (double)P, r, nbl * KG, Tn, twc, G, st));
   }
+  // what a z-step launch left for the tol test (register-line z-step, zline.hip):
+  // `lagged` the test of the iterate it started from (zpart, one launch late: the
+  // launch was speculative), `form` the test of the iterate it produced (fpart)
+  struct ZTests {
+    bool lagged = false, form = false;
+  };
+  double* zpart() { return znorm.as<double>(); }
+  double* fpart() { return znorm.as<double>() + 2 * np; }
   // one z-iteration over the local patches (dP:147-157; 4D L4:163-167; 3D L3:164-178).
-  // Returns true when the launch measured the iterate it started from instead of the
-  // one it produced (register-line z-step with tol > 0, see zline.hip); the others
-  // leave the test of the produced iterate in znorm when tol_on.
-  bool zstep_iter(bool tol_on) {
+  // The other z-steps leave the test of the produced iterate in znorm when tol_on.
+  ZTests zstep_iter(bool tol_on) {
     const auto* twc = tw.as<cpx<double>>();
     if (is4) {
       HIPCHK(launch_zstep_diag<double>(z.as<double>(), yz.as<double>(), E.as<cpx<double>>(),
@@ -826,20 +832,32 @@ struct Session2D {
                                       Tn, twc, G, st));
     } else if (zl_on) {
       // register-line z-step (zline.hip): mode 0 reads (z, y) and leaves a in state order.
-      // tol > 0: the launch stores the z it starts from in `yz` and, when `yz` holds the
-      // one before it, measures it (the test of the previous iteration, returned true)
+      // tol > 0: a launch whose starting w was solved with the current filters measures
+      // the iterate it produces in place (Form); otherwise (the first z-iteration after a
+      // d-phase, or a materialised state) it stores the z it starts from in `yz`, and the
+      // next launch measures that iterate against it (Cmp, one launch late)
       const int mode = zmode == 2 ? 2 : 0;
+      const bool same = mode == 2 && dws == dhs.as<cpx<double>>();
       int tolv = 0;
-      if (tol_on) tolv = mode == 0 ? 1 : (zt == ZT_PREV ? 2 : (zt == ZT_CUR ? 0 : 1));
+      if (tol_on) {
+        if (!same) tolv = kZlTolStore;
+        else if (zt == ZT_PREV) tolv = kZlTolStore | kZlTolCmp | kZlTolForm;
+        else tolv = kZlTolForm;
+      }
       HIPCHK(launch_zline<double>(z.as<double>(), z.as<double>(), z.as<double>(), yz.as<double>(),
                                   W.as<cpx<double>>(), Bhs.as<cpx<double>>(),
                                   zmode == 2 ? dws : dhs.as<cpx<double>>(), dhs.as<cpx<double>>(),
-                                  sdens.as<double>(), np, K, theta, mode, st, tolv,
-                                  yz.as<double>(), znorm.as<double>()));
+                                  sdens.as<double>(), np, K, theta, p.rho_z, mode, st, tolv,
+                                  yz.as<double>(), zpart(), fpart()));
       zmode = 2;
       dws = dhs.as<cpx<double>>();
-      if (tol_on) zt = ZT_PREV;
-      return tolv == 2;
+      // `yz` holds the z before the current iterate only after a lone Store launch; after a
+      // Cmp launch it holds the iterate the test covered (kept for zl_rollback only)
+      if (tol_on) zt = (tolv == kZlTolStore) ? ZT_PREV : ZT_NONE;
+      ZTests r;
+      r.lagged = (tolv & kZlTolCmp) != 0;
+      r.form = (tolv & kZlTolForm) != 0;
+      return r;
     } else if (!tol_on) {
       // one pass per patch over the pre-threshold state a (zsplit.hip): `z` holds a
       HIPCHK(launch_zsplit<double>(z.as<double>(), z.as<double>(), yz.as<double>(),
@@ -860,15 +878,16 @@ struct Session2D {
                                  znorm.as<double>(), np, twc, G, K, theta, st));
       zmode = 0;
     }
-    return false;
+    return ZTests{};
   }
   // register-line state + tol: the test of the current iterate against the z before it
   // (in `yz`, ZT_PREV) without advancing (end of a z-phase)
   void zl_finalize() {
     HIPCHK(launch_zline<double>(z.as<double>(), z.as<double>(), z.as<double>(), yz.as<double>(),
                                 W.as<cpx<double>>(), Bhs.as<cpx<double>>(), dws,
-                                dhs.as<cpx<double>>(), sdens.as<double>(), np, K, theta, 3, st, 2,
-                                yz.as<double>(), znorm.as<double>()));
+                                dhs.as<cpx<double>>(), sdens.as<double>(), np, K, theta, p.rho_z,
+                                3, st, kZlTolStore | kZlTolCmp, yz.as<double>(), zpart(),
+                                fpart()));
     zt = ZT_CUR;
   }
   // register-line state + tol: materialise (z, y) of the current iterate and measure it
@@ -1107,27 +1126,31 @@ struct Session2D {
     const bool want_oz = verbose_refresh_z() || p.trace_objective;
     int nz = 0;
     // z_diff of iteration iz (dP:156-157, dZ:163-164) from `count` partial pairs
-    auto z_test = [&](int iz, int64_t count) {
-      HIPCHK(launch_sum_pairs<double>(znorm.as<double>(), (int)count, pair.as<double>(), st));
+    // (||z - z_old||^2, ||z||^2); the Parseval form of zline.hip may round a vanishing
+    // difference to a tiny negative sum
+    auto z_test = [&](int iz, const double* parts, int64_t count) {
+      HIPCHK(launch_sum_pairs<double>(parts, (int)count, pair.as<double>(), st));
       allreduce(pair.as<double>(), 2);
       double h2[2];
       pair_to_host(h2);
-      const double zd = std::sqrt(h2[0]) / std::sqrt(h2[1]);
+      const double zd = std::sqrt(std::max(h2[0], 0.0)) / std::sqrt(h2[1]);
       last_z = zd;
       tr_zd[(size_t)it * p.max_it_z + iz] = zd;
       return zd;
     };
     // register-line z-step with tol (zline.hip): a launch measures the iterate it
-    // starts from, so the test of iteration iz arrives with launch iz + 1, which
-    // was then speculative when the test fires (zl_rollback); the objective's
-    // materialisation measures without the lag (zl_materialize_tol)
+    // produces (ZTests::form) once its starting w was solved with the current filters;
+    // after a d-phase the first launch stores its starting z and the second measures
+    // that iterate one launch late (ZTests::lagged; the second launch was speculative
+    // when the test fires: zl_rollback); the objective's materialisation measures
+    // without the lag (zl_materialize_tol)
     const bool zl_tol = zl_on && tol_on;
     bool zbreak = false;
     for (int iz = 0; iz < p.max_it_z; ++iz) {
-      bool lagged = false;
-      timed(0, [&] { lagged = zstep_iter(tol_on); });
+      ZTests zt_done;
+      timed(0, [&] { zt_done = zstep_iter(tol_on); });
       ++nz;
-      if (lagged && z_test(iz - 1, np) < p.tol) {   // dP:165-167 for iteration iz - 1
+      if (zt_done.lagged && z_test(iz - 1, zpart(), np) < p.tol) {   // dP:165-167 for iz - 1
         zl_rollback();
         --nz;
         zbreak = true;
@@ -1136,9 +1159,11 @@ struct Session2D {
       double zd = std::numeric_limits<double>::quiet_NaN();
       if (zl_tol && want_oz) {
         zl_materialize_tol();
-        zd = z_test(iz, np * K);
+        zd = z_test(iz, znorm.as<double>(), np * K);
+      } else if (zt_done.form) {
+        zd = z_test(iz, fpart(), np);
       } else if (tol_on && !zl_tol) {
-        zd = z_test(iz, np * K * Tn);
+        zd = z_test(iz, znorm.as<double>(), np * K * Tn);
       }
       if (want_oz) {
         const double o = objective_timed(dhat.as<cpx<double>>());
@@ -1152,7 +1177,7 @@ struct Session2D {
     }
     if (zl_tol && !zbreak && zt == ZT_PREV) {   // the last iteration's test
       zl_finalize();
-      z_test(nz - 1, np);
+      z_test(nz - 1, zpart(), np);
     }
     HIPCHK(hipEventRecord(e1, st));
     HIPCHK(hipEventSynchronize(e1));

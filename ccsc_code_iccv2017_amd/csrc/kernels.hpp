@@ -71,13 +71,18 @@ hipError_t launch_zhat_split(const T* A, const cpx<T>* W, const cpx<T>* dcorr, c
 // mode 0: (z, y) materialised in Zn / Yn (natural layout); mode 2: state in A.
 bool zline_grid(const Grid2D& G);
 size_t zline_smem_bytes();
-// tol: 0 off; 1 z of the starting iterate -> Zt (state order); 2 also the patch
-// sums of ||z - Zt||^2, ||z||^2 -> zpart[2p..2p+1]; mode 3 = finalize (tol 2, no advance).
+// tol (kZlTol* bits): Store: z of the starting iterate -> Zt (state order); Cmp: also the
+// patch sums of ||z - Zt||^2, ||z||^2 -> zpart[2p..2p+1]; Form: the patch sums of
+// ||z_new - z||^2, ||z_new||^2 of the produced iterate -> fpart[2p..2p+1] (needs
+// dcorr == dhat); mode 3 = finalize (Store | Cmp, no advance).
 template <typename T>
 hipError_t launch_zline(const T* A, T* Ao, const T* Zn, const T* Yn, cpx<T>* W, const cpx<T>* Bs,
                         const cpx<T>* dcorr, const cpx<T>* dhat, const T* sden, int64_t npatch,
-                        int K, T theta, int mode, hipStream_t st, int tol = 0, T* Zt = nullptr,
-                        T* zpart = nullptr);
+                        int K, T theta, T rho, int mode, hipStream_t st, int tol = 0,
+                        T* Zt = nullptr, T* zpart = nullptr, T* fpart = nullptr);
+// tol bits of launch_zline (zline.hip): store z_cur / compare with the stored z / the
+// Parseval test of the produced iterate
+constexpr int kZlTolStore = 1, kZlTolCmp = 2, kZlTolForm = 4;
 template <typename T>
 hipError_t launch_state_to_nat_inplace(T* a, int64_t count, hipStream_t st);
 // fft2(z) of the register-line state for the D-precompute (k_zhat_split's result in

@@ -203,15 +203,29 @@ __device__ __forceinline__ int fresh(int v) {
 // W <- w.  Bs, dcorr, dhat, sden in bin-slot order.
 //
 // The tol test (dP:156-157 / dZ:163-169: ||z - z_old|| / ||z|| after every
-// z-iteration) without a third z-sized buffer: the z of the iterate a launch
-// starts from, z_cur = (u - y)(A) + corr (mode 2) or the materialised z (mode 0),
-// is formed in registers anyway; TOL 1 stores it in state order to Zt (the
-// otherwise idle y buffer; in mode 0 Zt may alias Yn: read before written),
-// TOL 2 also reads the z before it from Zt and adds ||z_cur - z_prev||^2 and
-// ||z_cur||^2 of the patch into zpart[2p], [2p + 1] -- the test for the iterate
-// the launch started from, one launch late (the engine treats the launch as
-// speculative).  MODE 3 ("finalize"): TOL 2 without advancing:
-// no state write, no R2C, W untouched.
+// z-iteration) without a third z-sized buffer.  TOL is a set of kZt* bits:
+//  kZtForm  the test of the iterate the launch PRODUCES, in the launch itself, when the
+//           state's w was solved with the current filters (dcorr == dhat): the launch
+//           holds c_t = 2 soft(a) - a of the iterate it starts from and c_t+1 of the one it
+//           produces, and w_t, w_t+1 at its end; with z = c + ifft(conj(dhat) w_true),
+//           w_true = XY w = (B - acc) / (rho + s), Parseval gives
+//             ||z_t+1 - z_t||^2 = sum ||c_t+1 - c_t||^2 - XY sum_f |w_t+1 - w_t|^2 (2 rho + s)
+//             ||z_t+1||^2       = sum ||c_t+1||^2 + sum_f [2 Re(w conj(acc)) + XY s |w|^2]
+//           (half-spectrum bins weighted 2 but the self-conjugate columns x' = 0, 55;
+//           the cross terms use acc_t+1 - acc_t = -(rho + s) XY (w_t+1 - w_t)) into
+//           fpart[2p], [2p + 1] -- no z-sized stream;
+//  kZtStore z_cur = (u - y)(A) + corr (mode 2) or the materialised z (mode 0), the z of
+//           the iterate the launch starts from, formed in registers anyway, to Zt in state
+//           order (the otherwise idle y buffer; in mode 0 Zt may alias Yn: read before
+//           written) -- after a launch whose starting w came from other filters (the first
+//           z-iteration of an outer iteration) or a materialised state;
+//  kZtCmp   reads the z before it from Zt and adds ||z_cur - z_prev||^2, ||z_cur||^2 of the
+//           patch into zpart[2p], [2p + 1] -- the test of the iterate the launch started
+//           from, one launch late (the engine treats the launch as speculative, DESIGN.md
+//           §4).
+// MODE 3 ("finalize"): kZtStore | kZtCmp without advancing: no state write, no R2C, W
+// untouched.
+constexpr int kZtStore = kZlTolStore, kZtCmp = kZlTolCmp, kZtForm = kZlTolForm;
 template <typename T, int MODE, int TOL>
 __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn, const T* Yn,
                                                   cpx<T>* __restrict__ W,
@@ -219,10 +233,14 @@ __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn
                                                   const cpx<T>* __restrict__ dcorr,
                                                   const cpx<T>* __restrict__ dhat,
                                                   const T* __restrict__ sden, int K, T theta,
-                                                  T* Zt, T* __restrict__ zpart) {
+                                                  T rho, T* Zt, T* __restrict__ zpart,
+                                                  T* __restrict__ fpart) {
   static_assert(MODE == 0 || MODE == 2 || MODE == 3, "zline mode");
-  static_assert(TOL >= 0 && TOL <= 2 && (MODE != 0 || TOL < 2) && (MODE != 3 || TOL == 2),
+  static_assert(TOL >= 0 && TOL <= 7 && (!(TOL & kZtCmp) || (TOL & kZtStore)) &&
+                    (MODE != 0 || TOL <= kZtStore) &&
+                    (MODE != 3 || TOL == (kZtStore | kZtCmp)),
                 "zline tol variant");
+  constexpr bool kStore = TOL & kZtStore, kCmp = TOL & kZtCmp, kForm = TOL & kZtForm;
   using V2 = typename vec2_t<T>::type;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   cpx<T>* sT = reinterpret_cast<cpx<T>*>(smem);
@@ -233,7 +251,8 @@ __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn
   const cpx<T>* Wp = W + p * zl::F;
   // the last wave owns one y-line and no x-line (55 row pairs = 11 waves of 5)
   const bool xwave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6) < 11;
-  T nd = (T)0, nz = (T)0;   // TOL 2: ||z_cur - z_prev||^2, ||z_cur||^2 of the lanes' own elements
+  T nd = (T)0, nz = (T)0;   // kCmp: ||z_cur - z_prev||^2, ||z_cur||^2 of the lanes' own elements
+  T fd = (T)0, fz = (T)0;   // kForm: ||z_t+1 - z_t||^2, ||z_t+1||^2 (element, then bin terms)
 #if CCSC_ZL_WLDS
   // w is the same for every slice of the patch: the y-lines of waves 0..kZlWL-1 (columns
   // 0..5 kZlWL - 1) keep their bins in the LDS left over beside T, each lane its own ten
@@ -307,8 +326,8 @@ __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn
         V2 av[11];
 #pragma unroll
         for (int n2 = 0; n2 < 11; ++n2) av[n2] = sld<V2>(A + sl, po + n2 * 550 * 16);
-        V2 zo[TOL == 2 ? 11 : 1];
-        if constexpr (TOL == 2) {
+        V2 zo[kCmp ? 11 : 1];
+        if constexpr (kCmp) {
 #pragma unroll
           for (int n2 = 0; n2 < 11; ++n2) zo[n2] = sld<V2>(Zt + sl, po + n2 * 550 * 16);
         }
@@ -317,11 +336,12 @@ __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn
         inv_line<T, 1>(zb, Ex, s3, [&](int n2, cpx<T> corr) {
           V2 a = av[n2];
           const T sx = soft_l(a.x, theta), sy = soft_l(a.y, theta);
-          if constexpr (TOL >= 1) {   // z_cur = (u - y)(A) + corr
+          const T ctx = sx - (a.x - sx), cty = sy - (a.y - sy);   // c_t = u - y
+          if constexpr (kStore) {   // z_cur = (u - y)(A) + corr
             V2 zn;
-            zn.x = (sx - (a.x - sx)) + corr.x;
-            zn.y = (sy - (a.y - sy)) + corr.y;
-            if constexpr (TOL == 2) {
+            zn.x = ctx + corr.x;
+            zn.y = cty + corr.y;
+            if constexpr (kCmp) {
               const T ex = zn.x - zo[n2].x, ey = zn.y - zo[n2].y;
               nd += own * (ex * ex + ey * ey);
               nz += own * (zn.x * zn.x + zn.y * zn.y);
@@ -334,6 +354,11 @@ __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn
             sst<V2>(Ao + sl, po + n2 * 550 * 16, a);
             const T ux = soft_l(a.x, theta), uy = soft_l(a.y, theta);
             zc[n2] = {ux - (a.x - ux), uy - (a.y - uy)};
+            if constexpr (kForm) {   // c_t+1 - c_t and c_t+1 of the lanes' own elements
+              const T dx = zc[n2].x - ctx, dy = zc[n2].y - cty;
+              fd += own * (dx * dx + dy * dy);
+              fz += own * (zc[n2].x * zc[n2].x + zc[n2].y * zc[n2].y);
+            }
           }
         });
       }
@@ -356,8 +381,8 @@ __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn
           zc[n2] = {ux - (a.x - ux), uy - (a.y - uy)};
         }
       }
-      V2 zv[TOL == 1 ? 11 : 1];
-      if constexpr (TOL == 1) {
+      V2 zv[kStore ? 11 : 1];
+      if constexpr (kStore) {
         if (xwave) {
           const T* z0 = Zn + sl + 2 * j * zl::X;
 #pragma unroll
@@ -373,7 +398,7 @@ __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn
 #pragma unroll
         for (int n2 = 0; n2 < 11; ++n2) {
           zst<V2>(Ao + sl, po + n2 * 550 * 16, av[n2]);
-          if constexpr (TOL == 1) zst<V2>(Zt + sl, po + n2 * 550 * 16, zv[n2]);
+          if constexpr (kStore) zst<V2>(Zt + sl, po + n2 * 550 * 16, zv[n2]);
         }
       }
     }
@@ -416,39 +441,60 @@ __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn
       });
     }
   }
-  if constexpr (TOL == 2) {   // patch sums of the tol norms (T is free after the last slice)
-    T* red = reinterpret_cast<T*>(smem);
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    nd = wave_sum(nd);
-    nz = wave_sum(nz);
-    lds_sync();
-    if (lane == 0) {
-      red[2 * wave] = nd;
-      red[2 * wave + 1] = nz;
-    }
-    lds_sync();
-    if (threadIdx.x == 0) {
-      T sd = 0, sz = 0;
-      for (int w = 0; w < zl::NW; ++w) {
-        sd += red[2 * w];
-        sz += red[2 * w + 1];
-      }
-      zpart[2 * p] = sd;
-      zpart[2 * p + 1] = sz;
-    }
-  }
-  if constexpr (MODE == 3) return;
   // w = (B - acc) * sden  (sden = 1/((rho + s) X Y)); each lane owns its slots
-  {
+  if constexpr (MODE != 3) {
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int l = lane / 11, s = lane - 11 * l, line = 5 * wave + l;
     if (l < 5 && line < 56) {
       cpx<T>* Wo = W + p * zl::F;
       const cpx<T>* Bp = Bs + p * zl::F;
+      const T wt = (line == 0 || line == zl::Xh - 1) ? (T)1 : (T)2;   // self-conjugate columns
 #pragma unroll
       for (int k1 = 0; k1 < 10; ++k1) {
         const int sl2 = k1 * 616 + line * 11 + s;
-        Wo[sl2] = cscale(csub(Bp[sl2], acc[k1]), sden[sl2]);
+        const T sd = sden[sl2];
+        const cpx<T> wn = cscale(csub(Bp[sl2], acc[k1]), sd);
+        if constexpr (kForm) {   // the bin terms of the Parseval forms (w_t is read first)
+          const cpx<T> dw = csub(wn, Wo[sl2]);
+          const T rs = (T)1 / (sd * (T)zl::P);   // rho + s(f)
+          fd -= wt * (T)zl::P * cabs2(dw) * (rs + rho);
+          fz += wt * ((T)2 * (wn.x * acc[k1].x + wn.y * acc[k1].y) +
+                      (T)zl::P * (rs - rho) * cabs2(wn));
+        }
+        Wo[sl2] = wn;
+      }
+    }
+  }
+  if constexpr (kCmp || kForm) {   // patch sums of the tol norms (T is free after the last slice)
+    T* red = reinterpret_cast<T*>(smem);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    nd = wave_sum(nd);
+    nz = wave_sum(nz);
+    fd = wave_sum(fd);
+    fz = wave_sum(fz);
+    lds_sync();
+    if (lane == 0) {
+      red[4 * wave] = nd;
+      red[4 * wave + 1] = nz;
+      red[4 * wave + 2] = fd;
+      red[4 * wave + 3] = fz;
+    }
+    lds_sync();
+    if (threadIdx.x == 0) {
+      T sd = 0, sz = 0, sfd = 0, sfz = 0;
+      for (int w = 0; w < zl::NW; ++w) {
+        sd += red[4 * w];
+        sz += red[4 * w + 1];
+        sfd += red[4 * w + 2];
+        sfz += red[4 * w + 3];
+      }
+      if constexpr (kCmp) {
+        zpart[2 * p] = sd;
+        zpart[2 * p + 1] = sz;
+      }
+      if constexpr (kForm) {
+        fpart[2 * p] = sfd;
+        fpart[2 * p + 1] = sfz;
       }
     }
   }
@@ -577,28 +623,36 @@ bool zline_grid(const Grid2D& G) { return grid_is<Grid110>(G); }
 template <typename T, int MODE, int TOL>
 static void zline_go(hipStream_t st, int64_t npatch, const T* A, T* Ao, const T* Zn, const T* Yn,
                      cpx<T>* W, const cpx<T>* Bs, const cpx<T>* dcorr, const cpx<T>* dhat,
-                     const T* sden, int K, T theta, T* Zt, T* zpart) {
+                     const T* sden, int K, T theta, T rho, T* Zt, T* zpart, T* fpart) {
   hipLaunchKernelGGL((k_zline<T, MODE, TOL>), dim3((unsigned)npatch), dim3(zl::NT), kZlSmem, st,
-                     A, Ao, Zn, Yn, W, Bs, dcorr, dhat, sden, K, theta, Zt, zpart);
+                     A, Ao, Zn, Yn, W, Bs, dcorr, dhat, sden, K, theta, rho, Zt, zpart, fpart);
 }
 
 template <typename T>
 hipError_t launch_zline(const T* A, T* Ao, const T* Zn, const T* Yn, cpx<T>* W, const cpx<T>* Bs,
                         const cpx<T>* dcorr, const cpx<T>* dhat, const T* sden, int64_t npatch,
-                        int K, T theta, int mode, hipStream_t st, int tol, T* Zt, T* zpart) {
+                        int K, T theta, T rho, int mode, hipStream_t st, int tol, T* Zt,
+                        T* zpart, T* fpart) {
   if (npatch <= 0) return hipSuccess;
-  if (tol && !Zt) return hipErrorInvalidValue;
-  if ((tol == 2 || mode == 3) && !zpart) return hipErrorInvalidValue;
+  if ((tol & kZtStore) && !Zt) return hipErrorInvalidValue;
+  if ((tol & kZtCmp) && !zpart) return hipErrorInvalidValue;
+  if ((tol & kZtForm) && (!fpart || dcorr != dhat)) return hipErrorInvalidValue;
   const int v = mode * 10 + tol;
+#define ZL_GO(M, TL)                                                                          \
+  zline_go<T, M, TL>(st, npatch, A, Ao, Zn, Yn, W, Bs, dcorr, dhat, sden, K, theta, rho, Zt, \
+                     zpart, fpart)
   switch (v) {
-    case 0: zline_go<T, 0, 0>(st, npatch, A, Ao, Zn, Yn, W, Bs, dcorr, dhat, sden, K, theta, Zt, zpart); break;
-    case 1: zline_go<T, 0, 1>(st, npatch, A, Ao, Zn, Yn, W, Bs, dcorr, dhat, sden, K, theta, Zt, zpart); break;
-    case 20: zline_go<T, 2, 0>(st, npatch, A, Ao, Zn, Yn, W, Bs, dcorr, dhat, sden, K, theta, Zt, zpart); break;
-    case 21: zline_go<T, 2, 1>(st, npatch, A, Ao, Zn, Yn, W, Bs, dcorr, dhat, sden, K, theta, Zt, zpart); break;
-    case 22: zline_go<T, 2, 2>(st, npatch, A, Ao, Zn, Yn, W, Bs, dcorr, dhat, sden, K, theta, Zt, zpart); break;
-    case 32: zline_go<T, 3, 2>(st, npatch, A, Ao, Zn, Yn, W, Bs, dcorr, dhat, sden, K, theta, Zt, zpart); break;
+    case 0: ZL_GO(0, 0); break;
+    case 1: ZL_GO(0, 1); break;
+    case 20: ZL_GO(2, 0); break;
+    case 21: ZL_GO(2, 1); break;
+    case 23: ZL_GO(2, 3); break;
+    case 24: ZL_GO(2, 4); break;
+    case 27: ZL_GO(2, 7); break;
+    case 33: ZL_GO(3, 3); break;
     default: return hipErrorInvalidValue;
   }
+#undef ZL_GO
   return hipGetLastError();
 }
 
@@ -647,7 +701,8 @@ hipError_t launch_zhat_line(const T* A, const cpx<T>* W, const cpx<T>* dcorr, cp
 template hipError_t launch_zline<double>(const double*, double*, const double*, const double*,
                                          cpx<double>*, const cpx<double>*, const cpx<double>*,
                                          const cpx<double>*, const double*, int64_t, int, double,
-                                         int, hipStream_t, int, double*, double*);
+                                         double, int, hipStream_t, int, double*, double*,
+                                         double*);
 template hipError_t launch_zhat_line<double>(const double*, const cpx<double>*,
                                              const cpx<double>*, cpx<double>*, int64_t, int,
                                              double, hipStream_t);
