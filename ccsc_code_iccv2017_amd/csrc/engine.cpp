@@ -375,8 +375,13 @@ static Plan2D plan2d(const ccsc_problem& p, const Geom& g, int rank, int nranks)
   m.Ch = m.nbl * K * NV * F * 16;
   m.Dh = m.Ch;
   m.Zh = (size_t)p.ni * K * F * 16;
-  // 4D: view correlations E; 3D: spectra of the z-step's plane/t transforms
-  m.E = (is4 || is3) ? m.np * K * F * 16 : 0;
+  // 4D: view correlations E; 3D: spectra of the z-step's plane/t transforms, in the
+  // t-minor tile order when k_tsolve3 runs (padded to whole tiles: sized for TC = 4),
+  // with B^, the filter spectrum and sden in that order (misc)
+  const size_t F3t = is3 ? (size_t)std::max<int64_t>(ttile_bins(g.Tn, G.Y, G.Xh, 4),
+                                                     ttile_bins(g.Tn, G.Y, G.Xh, 2))
+                         : 0;
+  m.E = is4 ? m.np * K * F * 16 : is3 ? m.np * K * std::max(F, F3t) * 16 : 0;
   // register-line z-step (zline.hip, 110 grid): B^ and the two filter spectra in
   // bin-slot order, sden in bin-slot order
   m.zl = zline ? m.np * F * 16 + 2 * K * F * 16 + F * 8 : 0;
@@ -384,7 +389,7 @@ static Plan2D plan2d(const ccsc_problem& p, const Geom& g, int rank, int nranks)
   if (zline) m.zl += m.Zh;
   m.misc = (2 * K * NV * F) * 16 + F * 8 + (m.nbl + 2) * K * NV * SS * 8 * 2 +
            (4 * m.np * NV * g.Tn + 4 * K * NV * g.Tn + 64) * 8 + (size_t)(G.ntw + g.Gt.ntw) * 16 +
-           (is3 ? F * 16 + P * 8 : 0);
+           (is3 ? F * 16 + P * 8 + (m.np + K) * F3t * 16 + F3t * 8 : 0);
   return m;
 }
 
@@ -449,6 +454,7 @@ struct Session2D {
   int tsolve_tc = 0;       // 3D: x' columns per k_tsolve3 workgroup (0: three-kernel z-solve)
   Grid2D gt2{};            //     its t plan (K * tsolve_tc lines) and twiddles
   DevBuf twt2;
+  DevBuf BhatT, dhatT, sdenT;   // B^, the filter spectrum, sden in k_tsolve3's tile order
 
   // host-side log
   int outer_done = 0;
@@ -664,6 +670,14 @@ struct Session2D {
               Bhat.as<cpx<double>>(), np * NV);
     if (zl_on)
       HIPCHK(launch_to_slots<double>(Bhat.as<cpx<double>>(), Bhs.as<cpx<double>>(), np, st));
+    if (tsolve_tc) {
+      const size_t F3t = (size_t)ttile_bins(Tn, G.Y, G.Xh, tsolve_tc);
+      BhatT.alloc((size_t)np * F3t * 16);
+      dhatT.alloc((size_t)K * F3t * 16);
+      sdenT.alloc(F3t * 8);
+      HIPCHK(launch_to_ttiles<double>(Bhat.as<cpx<double>>(), BhatT.as<cpx<double>>(), Tn, G.Y,
+                                      G.Xh, tsolve_tc, np, st));
+    }
     // filters: init.d or device RNG (dP:38-39; 4D: [psf,psf,U,V,K], L4:39-40; 3D: psf^3, L3:39-40)
     DevBuf d0dev;
     const size_t nd0 = (size_t)SS * KG;
@@ -816,10 +830,10 @@ struct Session2D {
       cpx<double>* C = E.as<cpx<double>>();
       const auto* twtc = twt.as<cpx<double>>();
       HIPCHK(launch_plane_fwd<double>(1, z.as<double>(), yz.as<double>(), nullptr, 0, 0, 0, 0,
-                                      theta, 1, r, C, np * K, Tn, twc, G, st));
+                                      theta, 1, r, C, np * K, Tn, twc, G, st, tsolve_tc));
       if (tsolve_tc) {
-        HIPCHK(launch_tsolve3<double>(C, Bhat.as<cpx<double>>(), dhat.as<cpx<double>>(),
-                                      sden.as<double>(), np, K, G.Y, G.Xh, G.F, tsolve_tc,
+        HIPCHK(launch_tsolve3<double>(C, BhatT.as<cpx<double>>(), dhatT.as<cpx<double>>(),
+                                      sdenT.as<double>(), np, K, G.Y, G.Xh, tsolve_tc,
                                       1.0 / (double)P, twt2.as<cpx<double>>(), gt2, st));
       } else {
         HIPCHK(launch_tfft<double>(C, C, np * K, G.Y, G.F, -1, twtc, g.Gt, st));
@@ -829,7 +843,7 @@ struct Session2D {
       }
       HIPCHK(launch_plane_inv<double>(1, C, z.as<double>(), nullptr, nullptr,
                                       tol_on ? znorm.as<double>() : nullptr, 0, 1.0, r, np * K,
-                                      Tn, twc, G, st));
+                                      Tn, twc, G, st, tsolve_tc));
     } else if (zl_on) {
       // register-line z-step (zline.hip): mode 0 reads (z, y) and leaves a in state order.
       // tol > 0: a launch whose starting w was solved with the current filters measures
@@ -1118,6 +1132,12 @@ struct Session2D {
     if (zl_on) {
       HIPCHK(launch_to_slots<double>(dhat.as<cpx<double>>(), dhs.as<cpx<double>>(), K, st));
       HIPCHK(launch_to_slots_real<double>(sden.as<double>(), sdens.as<double>(), st));
+    }
+    if (tsolve_tc) {
+      HIPCHK(launch_to_ttiles<double>(dhat.as<cpx<double>>(), dhatT.as<cpx<double>>(), Tn, G.Y,
+                                      G.Xh, tsolve_tc, K, st));
+      HIPCHK(launch_to_ttiles_real<double>(sden.as<double>(), sdenT.as<double>(), Tn, G.Y, G.Xh,
+                                           tsolve_tc, st));
     }
     if (is4)   // L4:327 first term, constant over the z-iterations
       HIPCHK(launch_view_corr<double>(dhat.as<cpx<double>>(), Bhat.as<cpx<double>>(),

@@ -149,24 +149,34 @@ hipError_t launch_dsolve_wb(const cpx<T>* L, const cpx<T>* h, const cpx<T>* Ch, 
 // ---- kernels3d.hip: the 3D learner's factored transforms -------------------
 // Spectra [slice][t][F2]; P2 = X*Y plane voxels.  Modes: see kernels3d.hip.
 size_t tfft_smem_bytes(const Grid2D& Gt, size_t tsize);
+// tc > 0: the plane spectra go to / come from the t-minor tile order of k_tsolve3
+// ([slice][y][x'/tc][t][tc], ttile_bins per slice) instead of [slice][t][F2]
 template <typename T>
 hipError_t launch_plane_fwd(int mode, const T* a, T* b, const T* usup, int sx, int sy, int st,
                             int o, T theta, int KG, int r, cpx<T>* dst, int64_t nslices, int Tn,
-                            const cpx<T>* tw, const Grid2D& G, hipStream_t stream);
+                            const cpx<T>* tw, const Grid2D& G, hipStream_t stream, int tc = 0);
+int64_t ttile_bins(int Tn, int Yn, int Xh, int tc);
+template <typename T>
+hipError_t launch_to_ttiles(const cpx<T>* src, cpx<T>* dst, int Tn, int Yn, int Xh, int tc,
+                            int64_t count, hipStream_t stream);
+template <typename T>
+hipError_t launch_to_ttiles_real(const T* src, T* dst, int Tn, int Yn, int Xh, int tc,
+                                 hipStream_t stream);
 template <typename T>
 hipError_t launch_tfft(const cpx<T>* src, cpx<T>* dst, int64_t nslices, int Yn, int F2, int sign,
                        const cpx<T>* tw, const Grid2D& Gt, hipStream_t stream);
 template <typename T>
 hipError_t launch_plane_inv(int mode, const cpx<T>* src, T* dst, const T* yv, T* supp, T* norms,
                             int64_t nfirst, T scale, int r, int64_t nslices, int Tn,
-                            const cpx<T>* tw, const Grid2D& G, hipStream_t stream);
+                            const cpx<T>* tw, const Grid2D& G, hipStream_t stream, int tc = 0);
 // fused t-FFT + z-solve + inverse t-FFT over (patch, y, TC x' columns) tiles; Gt2 plans
-// the t lines of K * TC columns (make_gridt with Xh = K * TC)
+// the t lines of K * TC columns (make_gridt with Xh = K * TC); C, Bhat, dhat, sden in the
+// t-minor tile order of tile width TC
 bool tsolve3_ok(int Tn, int K, int TC);
 size_t tsolve3_smem_bytes(const Grid2D& Gt2, int K, int TC, size_t tsize);
 template <typename T>
 hipError_t launch_tsolve3(cpx<T>* C, const cpx<T>* Bhat, const cpx<T>* dhat, const T* sden,
-                          int64_t npatch, int K, int Yn, int Xh, int F2, int TC, T invP3,
+                          int64_t npatch, int K, int Yn, int Xh, int TC, T invP3,
                           const cpx<T>* tw, const Grid2D& Gt2, hipStream_t stream);
 template <typename T>
 hipError_t launch_zsolve3(cpx<T>* C, const cpx<T>* Bhat, const cpx<T>* dhat, const T* sden,

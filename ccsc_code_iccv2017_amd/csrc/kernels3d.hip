@@ -7,7 +7,12 @@
 // LDS-resident 2D machinery and fuse the elementwise stages (prox + dual,
 // D-step dual, support gather, padding); the t kernel holds one y-row of
 // lines (T x Xh complex) in LDS.  Spectra are stored [slice][t][y][x'] with
-// plane bins dense (F2 = Xh * Y), F3 = F2 * T.
+// plane bins dense (F2 = Xh * Y), F3 = F2 * T -- except between the z-step's plane
+// transforms and its fused t-solve (k_tsolve3), which exchange them "t-minor":
+// [slice][y][x' / TC][t][TC] (F3t = Y * ntile * T * TC, ntile = ceil(Xh / TC)), so the
+// t-solve reads and writes T * TC contiguous values per filter instead of TC-complex
+// segments at the plane stride, and the filter spectrum, B^ and sden it reads are
+// kept in the same order (k_to_ttiles).
 #include "slice.hpp"
 
 namespace ccsc {
@@ -16,13 +21,20 @@ namespace ccsc {
 // mode 0: embed src sub-volume [st][sy][sx] at offset (o, o, o) (zero padding)
 // mode 1: z-step prox + dual on z, y (L3:168-172)
 // mode 2: D-step dual y += D - u, c = u - y (L3:121-123), u from the (2r+1)^3 support
+// index of bin (t, y, x') of a slice in the t-minor tile order
+__device__ __forceinline__ int64_t ttile_idx(int t, int f2, int Tn, int Xh, int tc, int ntile) {
+  const int y = f2 / Xh, x = f2 - y * Xh;
+  const int tile = x / tc, c = x - tile * tc;
+  return ((int64_t)(y * ntile + tile) * Tn + t) * tc + c;
+}
+
 template <typename T>
 __global__ __launch_bounds__(kNT) void k_plane_fwd(int mode, const T* __restrict__ a,
                                                    T* __restrict__ b, const T* __restrict__ usup,
                                                    int sx, int sy, int st, int o, T theta,
                                                    int KG, int r, cpx<T>* __restrict__ dst,
                                                    int Tn, const cpx<T>* __restrict__ twg,
-                                                   Grid2D G) {
+                                                   Grid2D G, int tc) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   Smem<T> S = carve<T>(smem, G);
   load_twiddles(S.tw, twg, G.ntw);
@@ -68,6 +80,13 @@ __global__ __launch_bounds__(kNT) void k_plane_fwd(int mode, const T* __restrict
     zero_pad_row(S.slice, G);
   }
   slice_r2c<T, kMaxB>(S.slice, G, S.tw);
+  if (tc > 0) {   // t-minor tiles (k_tsolve3's order)
+    const int ntile = (G.Xh + tc - 1) / tc;
+    cpx<T>* out = dst + slice * ((int64_t)G.Y * ntile * Tn * tc);
+    for (int f = threadIdx.x; f < G.F; f += kNT)
+      out[ttile_idx(t, f, Tn, G.Xh, tc, ntile)] = lds_cpx(S.slice + bin_off(f, G), 1);
+    return;
+  }
   cpx<T>* out = dst + (slice * Tn + t) * G.F;
   for (int f = threadIdx.x; f < G.F; f += kNT) out[f] = lds_cpx(S.slice + bin_off(f, G), 1);
 }
@@ -107,14 +126,22 @@ __global__ __launch_bounds__(kNT) void k_plane_inv(int mode, const cpx<T>* __res
                                                    T* __restrict__ dst, const T* __restrict__ yv,
                                                    T* __restrict__ supp, T* __restrict__ norms,
                                                    int64_t nfirst, T scale, int r, int Tn,
-                                                   const cpx<T>* __restrict__ twg, Grid2D G) {
+                                                   const cpx<T>* __restrict__ twg, Grid2D G,
+                                                   int tc) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   Smem<T> S = carve<T>(smem, G);
   load_twiddles(S.tw, twg, G.ntw);
   const int64_t slice = blockIdx.x / Tn;
   const int t = blockIdx.x - (int)(slice * Tn);
-  const cpx<T>* in = src + (slice * Tn + t) * G.F;
-  for (int f = threadIdx.x; f < G.F; f += kNT) lds_cpx_store(S.slice + bin_off(f, G), 1, in[f]);
+  if (tc > 0) {   // t-minor tiles (k_tsolve3's order)
+    const int ntile = (G.Xh + tc - 1) / tc;
+    const cpx<T>* in = src + slice * ((int64_t)G.Y * ntile * Tn * tc);
+    for (int f = threadIdx.x; f < G.F; f += kNT)
+      lds_cpx_store(S.slice + bin_off(f, G), 1, in[ttile_idx(t, f, Tn, G.Xh, tc, ntile)]);
+  } else {
+    const cpx<T>* in = src + (slice * Tn + t) * G.F;
+    for (int f = threadIdx.x; f < G.F; f += kNT) lds_cpx_store(S.slice + bin_off(f, G), 1, in[f]);
+  }
   slice_c2r<T, kMaxB>(S.slice, G, S.tw);
   const int P = G.X * G.Y;
   const int64_t off = (slice * Tn + t) * P;
@@ -178,8 +205,8 @@ __global__ void k_zsolve3(cpx<T>* __restrict__ C, const cpx<T>* __restrict__ Bha
 // columns) holds the K filters' T x TC plane-spectrum columns in LDS, layout
 // [t][k*TC + c] (K*TC complex lines of length T), so the spectra cross HBM once
 // each way per z-iteration instead of three times (L3:172-178, the closed form of
-// k_zsolve3).  Gt2: the t plan for K*TC lines.  Neighbouring x' tiles of one row are
-// consecutive workgroups (their 16*TC-byte column segments share cache lines).
+// k_zsolve3).  C, B^, dhat and sden are in the t-minor tile order (F3t per slice):
+// a (slice, y, tile) block is T * TC contiguous complex.  Gt2: the t plan for K*TC lines.
 constexpr int kTsKmax = 16;   // k values per thread of k_tsolve3's solve phase
 
 template <typename T>
@@ -187,7 +214,7 @@ __global__ __launch_bounds__(kNT) void k_tsolve3(cpx<T>* __restrict__ C,
                                                  const cpx<T>* __restrict__ Bhat,
                                                  const cpx<T>* __restrict__ dhat,
                                                  const T* __restrict__ sden, int K, int Yn,
-                                                 int Xh, int F2, int TC, int xtiles, T invP3,
+                                                 int Xh, int TC, int xtiles, T invP3,
                                                  const cpx<T>* __restrict__ twg, Grid2D Gt) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   cpx<T>* s_tw = reinterpret_cast<cpx<T>*>(smem);
@@ -198,18 +225,17 @@ __global__ __launch_bounds__(kNT) void k_tsolve3(cpx<T>* __restrict__ C,
   const int y = (int)(rest % Yn);
   const int64_t p = rest / Yn;
   const int Tn = Gt.Y;
-  const int x0 = tile * TC;
-  const int nc = min(TC, Xh - x0);
+  const int nc = min(TC, Xh - tile * TC);
   const int NL = K * TC;
-  const int64_t F3 = (int64_t)F2 * Tn;
-  const int64_t colbase = (int64_t)y * Xh + x0;
-  cpx<T>* Cp = C + p * K * F3;
-  for (int i = threadIdx.x; i < K * Tn * TC; i += kNT) {
-    const int c = i % TC;
-    const int r = i / TC;
-    const int t = r % Tn, k = r / Tn;
+  const int TT = Tn * TC;                                   // one (slice, y, tile) block
+  const int64_t F3t = (int64_t)Yn * xtiles * TT;
+  const int64_t blk = (int64_t)(y * xtiles + tile) * TT;
+  cpx<T>* Cp = C + p * K * F3t + blk;
+  for (int i = threadIdx.x; i < K * TT; i += kNT) {
+    const int k = i / TT, rem = i - k * TT;
+    const int t = rem / TC, c = rem - t * TC;
     cpx<T> v = {(T)0, (T)0};
-    if (c < nc) v = Cp[(int64_t)k * F3 + (int64_t)t * F2 + colbase + c];
+    if (c < nc) v = Cp[(int64_t)k * F3t + rem];
     lds_cpx_store(lds + 2 * (t * NL + k * TC + c), 1, v);
   }
   lds_sync();
@@ -218,21 +244,21 @@ __global__ __launch_bounds__(kNT) void k_tsolve3(cpx<T>* __restrict__ C,
   // per bin (t, c): w = (B - sum_k d_k C_k) sden, C_k <- C_k / P3 + conj(d_k) w.
   // G = kNT / (T TC) threads per bin split the k range (their d_k stay in registers
   // between the two sweeps); partial sums meet in LDS past the spectra.
-  const int nb = Tn * TC;
+  const int nb = TT;
   const int G = max(1, kNT / nb);
   const int kg = (K + G - 1) / G;
   cpx<T>* part = reinterpret_cast<cpx<T>*>(lds + 2 * (size_t)Tn * NL);   // [G][nb]
   const int b = threadIdx.x % nb, grp = threadIdx.x / nb;
   const int t = b / TC, c = b - t * TC;
   const bool on = grp < G && c < nc;
-  const int64_t f3 = (int64_t)t * F2 + colbase + c;
+  const int64_t f3 = blk + b;                               // t * TC + c inside the block
   T* row = lds + 2 * (t * NL + c);
   cpx<T> dv[kTsKmax];
   cpx<T> acc = {(T)0, (T)0};
 #pragma unroll
   for (int j = 0; j < kTsKmax; ++j) {
     const int k = grp * kg + j;
-    dv[j] = (on && j < kg && k < K) ? dhat[(int64_t)k * F3 + f3] : cpx<T>{(T)0, (T)0};
+    dv[j] = (on && j < kg && k < K) ? dhat[(int64_t)k * F3t + f3] : cpx<T>{(T)0, (T)0};
   }
 #pragma unroll
   for (int j = 0; j < kTsKmax; ++j) {
@@ -244,7 +270,7 @@ __global__ __launch_bounds__(kNT) void k_tsolve3(cpx<T>* __restrict__ C,
   if (on) {
     cpx<T> tot = {(T)0, (T)0};
     for (int q = 0; q < G; ++q) tot = cadd(tot, part[q * nb + b]);
-    const cpx<T> w = cscale(csub(Bhat[p * F3 + f3], tot), sden[f3]);
+    const cpx<T> w = cscale(csub(Bhat[p * F3t + f3], tot), sden[f3]);
 #pragma unroll
     for (int j = 0; j < kTsKmax; ++j) {
       const int k = grp * kg + j;
@@ -256,12 +282,34 @@ __global__ __launch_bounds__(kNT) void k_tsolve3(cpx<T>* __restrict__ C,
   }
   lds_sync();
   fft_dir<T, kMaxB, +1>(lds, kModePlain, g, g, Gt, Gt.py, s_tw);
-  for (int i = threadIdx.x; i < K * Tn * TC; i += kNT) {
-    const int c = i % TC;
-    const int r = i / TC;
-    const int t = r % Tn, k = r / Tn;
-    if (c < nc) Cp[(int64_t)k * F3 + (int64_t)t * F2 + colbase + c] = lds_cpx(lds + 2 * (t * NL + k * TC + c), 1);
+  for (int i = threadIdx.x; i < K * TT; i += kNT) {
+    const int k = i / TT, rem = i - k * TT;
+    const int t = rem / TC, c = rem - t * TC;
+    if (c < nc) Cp[(int64_t)k * F3t + rem] = lds_cpx(lds + 2 * (t * NL + k * TC + c), 1);
   }
+}
+
+// dst[s][t-minor tile order] = src[s][t][y][x'] (count spectra of F3 = T Y Xh bins; the
+// padding columns x' >= Xh of the last tile are zero)
+template <typename T, typename V>
+__global__ void k_to_ttiles(const V* __restrict__ src, V* __restrict__ dst, int Tn, int Yn,
+                            int Xh, int tc, int64_t count) {
+  const int ntile = (Xh + tc - 1) / tc;
+  const int64_t F3t = (int64_t)Yn * ntile * Tn * tc;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count * F3t) return;
+  const int64_t s = i / F3t;
+  int64_t r = i - s * F3t;
+  const int c = (int)(r % tc);
+  r /= tc;
+  const int t = (int)(r % Tn);
+  r /= Tn;
+  const int tile = (int)(r % ntile);
+  const int y = (int)(r / ntile);
+  const int x = tile * tc + c;
+  V v{};
+  if (x < Xh) v = src[(s * Tn + t) * ((int64_t)Yn * Xh) + (int64_t)y * Xh + x];
+  dst[i] = v;
 }
 
 // ---- objective helper: acc[p][f] = sum_k Zhat[p][k][f] d[k][f] --------------
@@ -312,11 +360,33 @@ size_t tfft_smem_bytes(const Grid2D& Gt, size_t tsize) {
 template <typename T>
 hipError_t launch_plane_fwd(int mode, const T* a, T* b, const T* usup, int sx, int sy, int st,
                             int o, T theta, int KG, int r, cpx<T>* dst, int64_t nslices, int Tn,
-                            const cpx<T>* tw, const Grid2D& G, hipStream_t stream) {
+                            const cpx<T>* tw, const Grid2D& G, hipStream_t stream, int tc) {
   if (nslices <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_plane_fwd<T>, dim3((unsigned)(nslices * Tn)), dim3(kNT),
                      slice_smem_bytes(G, sizeof(T)), stream, mode, a, b, usup, sx, sy, st, o,
-                     theta, KG, r, dst, Tn, tw, G);
+                     theta, KG, r, dst, Tn, tw, G, tc);
+  return hipGetLastError();
+}
+
+int64_t ttile_bins(int Tn, int Yn, int Xh, int tc) {
+  return (int64_t)Yn * ((Xh + tc - 1) / tc) * Tn * tc;
+}
+
+template <typename T>
+hipError_t launch_to_ttiles(const cpx<T>* src, cpx<T>* dst, int Tn, int Yn, int Xh, int tc,
+                            int64_t count, hipStream_t stream) {
+  if (count <= 0) return hipSuccess;
+  const int64_t n = count * ttile_bins(Tn, Yn, Xh, tc);
+  hipLaunchKernelGGL((k_to_ttiles<T, cpx<T>>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     stream, src, dst, Tn, Yn, Xh, tc, count);
+  return hipGetLastError();
+}
+template <typename T>
+hipError_t launch_to_ttiles_real(const T* src, T* dst, int Tn, int Yn, int Xh, int tc,
+                                 hipStream_t stream) {
+  const int64_t n = ttile_bins(Tn, Yn, Xh, tc);
+  hipLaunchKernelGGL((k_to_ttiles<T, T>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
+                     src, dst, Tn, Yn, Xh, tc, (int64_t)1);
   return hipGetLastError();
 }
 
@@ -350,7 +420,7 @@ size_t tsolve3_smem_bytes(const Grid2D& Gt2, int K, int TC, size_t tsize) {
 
 template <typename T>
 hipError_t launch_tsolve3(cpx<T>* C, const cpx<T>* Bhat, const cpx<T>* dhat, const T* sden,
-                          int64_t npatch, int K, int Yn, int Xh, int F2, int TC, T invP3,
+                          int64_t npatch, int K, int Yn, int Xh, int TC, T invP3,
                           const cpx<T>* tw, const Grid2D& Gt2, hipStream_t stream) {
   if (npatch <= 0) return hipSuccess;
   if (Gt2.Xh != K * TC) return hipErrorInvalidValue;   // the plan's line count
@@ -358,18 +428,18 @@ hipError_t launch_tsolve3(cpx<T>* C, const cpx<T>* Bhat, const cpx<T>* dhat, con
   const int xtiles = (Xh + TC - 1) / TC;
   const dim3 grid((unsigned)(npatch * Yn * xtiles));
   hipLaunchKernelGGL(k_tsolve3<T>, grid, dim3(kNT), tsolve3_smem_bytes(Gt2, K, TC, sizeof(T)),
-                     stream, C, Bhat, dhat, sden, K, Yn, Xh, F2, TC, xtiles, invP3, tw, Gt2);
+                     stream, C, Bhat, dhat, sden, K, Yn, Xh, TC, xtiles, invP3, tw, Gt2);
   return hipGetLastError();
 }
 
 template <typename T>
 hipError_t launch_plane_inv(int mode, const cpx<T>* src, T* dst, const T* yv, T* supp, T* norms,
                             int64_t nfirst, T scale, int r, int64_t nslices, int Tn,
-                            const cpx<T>* tw, const Grid2D& G, hipStream_t stream) {
+                            const cpx<T>* tw, const Grid2D& G, hipStream_t stream, int tc) {
   if (nslices <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_plane_inv<T>, dim3((unsigned)(nslices * Tn)), dim3(kNT),
                      slice_smem_bytes(G, sizeof(T)), stream, mode, src, dst, yv, supp, norms,
-                     nfirst, scale, r, Tn, tw, G);
+                     nfirst, scale, r, Tn, tw, G, tc);
   return hipGetLastError();
 }
 
@@ -400,16 +470,21 @@ hipError_t launch_crop_sq(const T* Dz, const T* b, int sx, int sy, int st, int r
 
 template hipError_t launch_plane_fwd<double>(int, const double*, double*, const double*, int, int,
                                              int, int, double, int, int, cpx<double>*, int64_t,
-                                             int, const cpx<double>*, const Grid2D&, hipStream_t);
+                                             int, const cpx<double>*, const Grid2D&, hipStream_t,
+                                             int);
+template hipError_t launch_to_ttiles<double>(const cpx<double>*, cpx<double>*, int, int, int, int,
+                                             int64_t, hipStream_t);
+template hipError_t launch_to_ttiles_real<double>(const double*, double*, int, int, int, int,
+                                                  hipStream_t);
 template hipError_t launch_tfft<double>(const cpx<double>*, cpx<double>*, int64_t, int, int, int,
                                         const cpx<double>*, const Grid2D&, hipStream_t);
 template hipError_t launch_plane_inv<double>(int, const cpx<double>*, double*, const double*,
                                              double*, double*, int64_t, double, int, int64_t, int,
-                                             const cpx<double>*, const Grid2D&, hipStream_t);
+                                             const cpx<double>*, const Grid2D&, hipStream_t, int);
 template hipError_t launch_tsolve3<double>(cpx<double>*, const cpx<double>*,
                                            const cpx<double>*, const double*, int64_t, int, int,
-                                           int, int, int, double, const cpx<double>*,
-                                           const Grid2D&, hipStream_t);
+                                           int, int, double, const cpx<double>*, const Grid2D&,
+                                           hipStream_t);
 template hipError_t launch_zsolve3<double>(cpx<double>*, const cpx<double>*, const cpx<double>*,
                                            const double*, int64_t, int64_t, int, double,
                                            hipStream_t);
