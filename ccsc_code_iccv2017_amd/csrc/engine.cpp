@@ -50,6 +50,11 @@ static int64_t generic_tasks(int n, int nlines, int p) {
   return (int64_t)nlines * (n / p) * (((p - 1) / 2 + kGenericQP - 1) / kGenericQP);
 }
 
+static bool pfa_disabled() {   // CCSC_FFT_PFA=0: the generic pass (A/B)
+  const char* e = std::getenv("CCSC_FFT_PFA");
+  return e && e[0] == '0';
+}
+
 static bool plan1d(int n, int nlines, Plan1D& out) {
   Plan1D best{};
   best.npass = 99;
@@ -99,6 +104,9 @@ static bool plan1d(int n, int nlines, Plan1D& out) {
       best.npass = rest.npass + 1;
       for (int s = 0; s < rest.npass; ++s) best.rad[s] = rest.rad[s];
       best.rad[rest.npass] = p;
+      // 2 * kPfaM: the prime-factor pass with immediate roots (fft_pass_pfa)
+      best.pfa = (n == 2 * kPfaM && p == kPfaM && best.npass == 2 &&
+                  pfa_slots(nlines, kPfaM, kPfaQP) <= kNT && !pfa_disabled());
       break;
     }
   }

@@ -216,6 +216,7 @@ struct Plan1D {
   int twoff[kPlanSlots];  // offset (complex units) of pass s's twiddle table,
                         // entries (r-1)*Ns + k = exp(-2 pi i r k / (Ns R)); a
                         // generic-radix pass appends its R roots exp(-2 pi i m/R)
+  int pfa;              // n = 2 M, rad = {2, M}: the M pass is fft_pass_pfa (M = kPfaM)
 };
 // Radices with an unrolled in-register butterfly; any other prime factor (up
 // to kMaxGenericRadix, e.g. 37 for the 74-point grids of the 3D/4D configs, or a
@@ -466,14 +467,138 @@ __device__ __forceinline__ void fft_pass_generic(T* lds, int R, int mode, const 
   lds_sync();
 }
 
-template <typename T, int MAXB, int SIGN, int NT = kNT, int GT = 1, int BS = 1>
+// Second pass of a length N = 2 M line (M odd prime, compile-time roots) as a
+// prime-factor (Good-Thomas) split, no twiddles.  The radix-2 Stockham pass before it
+// (Ns = 1) left out[2j] = x_j + x_{j+M}, out[2j+1] = x_j - x_{j+M}; with n = (M n1 +
+// 2 n2) mod N and k = (M k1 + (M+1) k2) mod N,
+//   X_k = sum_{n2} W_M^{n2 k2} u^{k1}_{n2},   u^{k1}_{n2} = +-out[2 j + k1], j = 2 n2 mod M
+// (the minus for k1 = 1 when 2 n2 >= M: the pair is then (x_{j+M}, x_j)).  One task =
+// (line, k1, output group g of QP conjugate pairs); the slots are laid out g-major then
+// k1 then line, padded to whole waves, so g and k1 are wave-uniform and every root is
+// an immediate (fft_pass_generic reads one per term from LDS and twiddles its inputs).
+constexpr int kPfaM = 37;   // the 74-point grids of the 3D / 4D configs (74 = 64 + 2 * 5)
+constexpr int kPfaQP = 3;   // conjugate output pairs per task
+
+__host__ __device__ constexpr int pfa_slots(int nlines, int M, int QP) {
+  return ((M - 1) / 2 + QP - 1) / QP * 2 * ((nlines + 63) / 64 * 64);
+}
+
+template <typename T, int M, int SIGN, int QP, int NT>
+__device__ __forceinline__ void fft_pass_pfa(T* lds, const LineGeom& g) {
+  constexpr int H = (M - 1) / 2;
+  constexpr int NG = (H + QP - 1) / QP;
+  const int nl = g.nlines;
+  const int lpad = (nl + 63) & ~63;
+  int o = (int)threadIdx.x;
+  asm volatile("" : "+v"(o));
+  const int grp = __builtin_amdgcn_readfirstlane(o / (2 * lpad));
+  const int k1 = __builtin_amdgcn_readfirstlane((o / lpad) & 1);
+  const int line = o % lpad;
+  const bool on = grp < NG && line < nl;
+  T* base = lds + line * g.lstride;
+  const int es = g.estride, im = g.imoff;
+  cpx<T> A[QP], S[QP], dc = {(T)0, (T)0};
+#pragma unroll
+  for (int i = 0; i < QP; ++i) A[i] = S[i] = {(T)0, (T)0};   // (A starts at u_0)
+  auto in = [&](auto n2c, auto k1c) {
+    constexpr int n2 = decltype(n2c)::value, kk = decltype(k1c)::value;
+    constexpr int j = (2 * n2) % M;
+    cpx<T> v = lds_cpx(base + (2 * j + kk) * es, im);
+    if constexpr (kk == 1 && 2 * n2 >= M) v = {-v.x, -v.y};
+    return v;
+  };
+  auto body = [&](auto gc, auto k1c) {
+    constexpr int gg = decltype(gc)::value;
+    {
+      const cpx<T> u0 = in(std::integral_constant<int, 0>{}, k1c);
+      if constexpr (gg == 0) dc = u0;
+#pragma unroll
+      for (int i = 0; i < QP; ++i) A[i] = u0;
+    }
+    // the scheduling fence per term keeps the compiler from hoisting all 2 H loads
+    // (4 H VGPRs of complex) to the top: 8 waves per SIMD cover the LDS latency
+    sfor<H>([&](auto ri) {
+      constexpr int r = decltype(ri)::value + 1;
+      const cpx<T> a = in(std::integral_constant<int, r>{}, k1c);
+      const cpx<T> b = in(std::integral_constant<int, M - r>{}, k1c);
+      const cpx<T> sr = cadd(a, b), dr = csub(a, b);
+      if constexpr (gg == 0) dc = cadd(dc, sr);
+      sfor<QP>([&](auto ii) {
+        constexpr int q = gg * QP + decltype(ii)::value + 1;
+        if constexpr (q <= H) {
+          constexpr int m = (r * q) % M;
+          constexpr T c = (T)TC<M, m>::c;
+          constexpr T sn = (T)TC<M, m>::s;
+          A[ii].x += sr.x * c;
+          A[ii].y += sr.y * c;
+          S[ii].x += dr.x * sn;
+          S[ii].y += dr.y * sn;
+        }
+      });
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  };
+  if (on) {
+    sfor<NG>([&](auto gc) {
+      if (grp == decltype(gc)::value) {
+        if (k1 == 0) body(gc, std::integral_constant<int, 0>{});
+        else body(gc, std::integral_constant<int, 1>{});
+      }
+    });
+  }
+  lds_sync();
+  auto put = [&](auto gc, auto k1c) {
+    constexpr int gg = decltype(gc)::value, kk = decltype(k1c)::value;
+    constexpr int N = 2 * M;
+    if constexpr (gg == 0) lds_cpx_store(base + ((M * kk) % N) * es, im, dc);
+    sfor<QP>([&](auto ii) {
+      constexpr int q = gg * QP + decltype(ii)::value + 1;
+      if constexpr (q <= H) {
+        // X_q = A + SIGN i S, X_{M-q} = A - SIGN i S
+        const cpx<T> iS = {-(T)SIGN * S[ii].y, (T)SIGN * S[ii].x};
+        constexpr int kq = (M * kk + (M + 1) * q) % N;
+        constexpr int kr = (M * kk + (M + 1) * (M - q)) % N;
+        lds_cpx_store(base + kq * es, im, cadd(A[ii], iS));
+        lds_cpx_store(base + kr * es, im, csub(A[ii], iS));
+      }
+    });
+  };
+  if (on) {
+    sfor<NG>([&](auto gc) {
+      if (grp == decltype(gc)::value) {
+        if (k1 == 0) put(gc, std::integral_constant<int, 0>{});
+        else put(gc, std::integral_constant<int, 1>{});
+      }
+    });
+  }
+  lds_sync();
+}
+
+// Pass kinds a kernel instantiation compiles (RM): bit R for the native radix R, plus the
+// generic and the prime-factor pass.  A kernel holds the registers of the largest pass it
+// compiles, so the slice kernels of a known grid instantiate only that grid's passes
+// (the 74-point grids: radix 2 + fft_pass_pfa, ~60 instead of ~95-127 VGPRs) and the host
+// checks plan_mask(plan) against the instantiation it launches (engine.cpp).
+constexpr int kRmGeneric = 1 << 12, kRmPfa = 1 << 13;
+constexpr int kRmAll = 0x3fff;
+constexpr int kRm74 = (1 << 2) | kRmPfa;                  // 74 = 2 * 37 (C4 / C5 planes)
+constexpr int kRm42 = (1 << 2) | (1 << 3) | (1 << 7);     // 42 = 2 * 3 * 7 (C4 t lines)
+
+// butterflies per thread of a native pass: the 74-point instantiation holds the 2 its
+// radix-2 pass needs (37 x 38 butterflies over kNT threads) instead of maxb_for_radix's 4
+__host__ __device__ constexpr int rm_maxb(int rm, int R) {
+  return rm == kRm74 ? 2 : maxb_for_radix(R);
+}
+
+template <typename T, int MAXB, int SIGN, int NT = kNT, int GT = 1, int BS = 1, int RM = kRmAll>
 __device__ __forceinline__ void fft_pass_dispatch(int R, T* lds, int mode, const LineGeom& gin,
                                                   const LineGeom& gout, const Grid2D& G, int n,
                                                   int Ns, const cpx<T>* tw) {
   switch (R) {
 #define CCSC_NATIVE_PASS(RR)                                                                   \
     case RR:                                                                                   \
-      fft_pass<T, RR, maxb_for_radix(RR) * BS, SIGN, NT>(lds, mode, gin, gout, G, n, Ns, tw);  \
+      if constexpr ((RM >> RR) & 1)                                                            \
+        fft_pass<T, RR, rm_maxb(RM, RR) * BS, SIGN, NT>(lds, mode, gin, gout, G, n, Ns, tw);   \
       break;
     CCSC_NATIVE_PASS(2)
     CCSC_NATIVE_PASS(3)
@@ -484,7 +609,10 @@ __device__ __forceinline__ void fft_pass_dispatch(int R, T* lds, int mode, const
     CCSC_NATIVE_PASS(10)
     CCSC_NATIVE_PASS(11)
 #undef CCSC_NATIVE_PASS
-    default: fft_pass_generic<T, SIGN, NT, GT>(lds, R, mode, gin, gout, G, n, Ns, tw); break;
+    default:
+      if constexpr ((RM & kRmGeneric) != 0)
+        fft_pass_generic<T, SIGN, NT, GT>(lds, R, mode, gin, gout, G, n, Ns, tw);
+      break;
   }
 }
 
@@ -497,7 +625,7 @@ __device__ __forceinline__ void fft_pass_dispatch(int R, T* lds, int mode, const
 // index math out of the loop and keep it live in registers (256 VGPRs + 5 KB
 // of scratch per lane).
 template <typename T, int MAXB, int SIGN, int NSLOT = kMaxPass, int NT = kNT, int GT = 1,
-          int BS = 1>
+          int BS = 1, int RM = kRmAll>
 __device__ __forceinline__ void fft_dir(T* lds, int mode0, const LineGeom& gfirst,
                                         const LineGeom& g, const Grid2D& G, const Plan1D& p,
                                         const cpx<T>* tw) {
@@ -510,10 +638,15 @@ __device__ __forceinline__ void fft_dir(T* lds, int mode0, const LineGeom& gfirs
     if (s < p.npass) {
       const int R = p.rad[s];
       const cpx<T>* tws = tw + p.twoff[s];
-      if constexpr (s == 0)
-        fft_pass_dispatch<T, MAXB, SIGN, NT, GT, BS>(R, lds, mode0, gfirst, g, G, n, Ns, tws);
-      else
-        fft_pass_dispatch<T, MAXB, SIGN, NT, GT, BS>(R, lds, kModePlain, g, g, G, n, Ns, tws);
+      if constexpr (s == 0) {
+        fft_pass_dispatch<T, MAXB, SIGN, NT, GT, BS, RM>(R, lds, mode0, gfirst, g, G, n, Ns, tws);
+      } else if constexpr (s == 1 && NT == kNT && (RM & kRmPfa) != 0) {
+        // (the prime-factor pass: plans of kNT-thread slice kernels only)
+        if (p.pfa) fft_pass_pfa<T, kPfaM, SIGN, kPfaQP, NT>(lds, g);
+        else fft_pass_dispatch<T, MAXB, SIGN, NT, GT, BS, RM>(R, lds, kModePlain, g, g, G, n, Ns, tws);
+      } else {
+        fft_pass_dispatch<T, MAXB, SIGN, NT, GT, BS, RM>(R, lds, kModePlain, g, g, G, n, Ns, tws);
+      }
       Ns *= R;
     }
   });
@@ -528,24 +661,39 @@ __device__ __forceinline__ LineGeom geom_ycols(const Grid2D& G) {
 
 // Forward 2D R2C of the real slice in LDS rows [y*RS, y*RS+X) (rows Y..Yp-1 zero).
 // Result: interleaved half spectrum, bin (x', y) at lds[y*RS + 2x'].
-template <typename T, int MAXB>
+template <typename T, int MAXB, int RM = kRmAll>
 __device__ __forceinline__ void slice_r2c(T* lds, const Grid2D& G, const cpx<T>* tw) {
   const LineGeom gx = geom_xsplit(G);
   const LineGeom gy = geom_ycols(G);
   lds_sync();
-  fft_dir<T, MAXB, -1>(lds, kModePlain, gx, gx, G, G.px, tw);
-  fft_dir<T, MAXB, -1>(lds, kModeSplitToHalf, gy, gy, G, G.py, tw);
+  fft_dir<T, MAXB, -1, kMaxPass, kNT, 1, 1, RM>(lds, kModePlain, gx, gx, G, G.px, tw);
+  fft_dir<T, MAXB, -1, kMaxPass, kNT, 1, 1, RM>(lds, kModeSplitToHalf, gy, gy, G, G.py, tw);
 }
 
 // Inverse 2D C2R (unnormalised) of the interleaved half spectrum in LDS.
 // Result: real rows [y*RS, y*RS+X).
-template <typename T, int MAXB>
+template <typename T, int MAXB, int RM = kRmAll>
 __device__ __forceinline__ void slice_c2r(T* lds, const Grid2D& G, const cpx<T>* tw) {
   const LineGeom gx = geom_xsplit(G);
   const LineGeom gy = geom_ycols(G);
   lds_sync();
-  fft_dir<T, MAXB, +1>(lds, kModePlain, gy, gy, G, G.py, tw);
-  fft_dir<T, MAXB, +1>(lds, kModeHermPair, gx, gx, G, G.px, tw);
+  fft_dir<T, MAXB, +1, kMaxPass, kNT, 1, 1, RM>(lds, kModePlain, gy, gy, G, G.py, tw);
+  fft_dir<T, MAXB, +1, kMaxPass, kNT, 1, 1, RM>(lds, kModeHermPair, gx, gx, G, G.px, tw);
 }
+
+// The pass kinds a plan needs (RM bits of fft_pass_dispatch / fft_dir).
+__host__ __device__ inline int plan_mask(const Plan1D& p) {
+  int m = 0;
+  for (int s = 0; s < p.npass; ++s) {
+    const int R = p.rad[s];
+    if (s == 1 && p.pfa) m |= kRmPfa;
+    else if (R == 2 || R == 3 || R == 4 || R == 5 || R == 7 || R == 8 || R == 10 || R == 11)
+      m |= 1 << R;
+    else m |= kRmGeneric;
+  }
+  return m;
+}
+// the first of the candidate instantiations that covers mask m
+__host__ __device__ inline bool rm_covers(int rm, int m) { return (m & ~rm) == 0; }
 
 }  // namespace ccsc

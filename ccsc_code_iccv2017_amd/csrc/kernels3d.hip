@@ -28,8 +28,16 @@ __device__ __forceinline__ int64_t ttile_idx(int t, int f2, int Tn, int Xh, int 
   return ((int64_t)(y * ntile + tile) * Tn + t) * tc + c;
 }
 
-template <typename T>
-__global__ __launch_bounds__(kNT) void k_plane_fwd(int mode, const T* __restrict__ a,
+// Waves per SIMD a slice kernel of pass mask RM is compiled for: the masked 74-point
+// instantiations fit 64 VGPRs, so two 1024-thread workgroups (two planes) share a CU
+// and one's barriers and HBM waits overlap the other's passes; the all-radix build
+// needs ~95-127 VGPRs (one workgroup per CU).
+template <int RM>
+constexpr int slice_waves() { return RM == kRmAll ? 4 : 8; }
+
+template <typename T, int RM>
+__global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(slice_waves<RM>())))
+void k_plane_fwd(int mode, const T* __restrict__ a,
                                                    T* __restrict__ b, const T* __restrict__ usup,
                                                    int sx, int sy, int st, int o, T theta,
                                                    int KG, int r, cpx<T>* __restrict__ dst,
@@ -79,7 +87,7 @@ __global__ __launch_bounds__(kNT) void k_plane_fwd(int mode, const T* __restrict
     }
     zero_pad_row(S.slice, G);
   }
-  slice_r2c<T, kMaxB>(S.slice, G, S.tw);
+  slice_r2c<T, kMaxB, RM>(S.slice, G, S.tw);
   if (tc > 0) {   // t-minor tiles (k_tsolve3's order)
     const int ntile = (G.Xh + tc - 1) / tc;
     cpx<T>* out = dst + slice * ((int64_t)G.Y * ntile * Tn * tc);
@@ -93,8 +101,9 @@ __global__ __launch_bounds__(kNT) void k_plane_fwd(int mode, const T* __restrict
 
 // ---- t-direction complex FFT (src may equal dst); one workgroup per (slice, y)
 // Gt describes the T x Xh tile: Gt.Y = T (plan Gt.py), Gt.Xh = lines, Gt.RS = row stride.
-template <typename T, int SIGN>
-__global__ __launch_bounds__(kNT) void k_tfft(const cpx<T>* src, cpx<T>* dst, int Yn, int F2,
+template <typename T, int SIGN, int RM>
+__global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(slice_waves<RM>())))
+void k_tfft(const cpx<T>* src, cpx<T>* dst, int Yn, int F2,
                                               const cpx<T>* __restrict__ twg, Grid2D Gt) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   cpx<T>* s_tw = reinterpret_cast<cpx<T>*>(smem);
@@ -110,7 +119,7 @@ __global__ __launch_bounds__(kNT) void k_tfft(const cpx<T>* src, cpx<T>* dst, in
   }
   lds_sync();
   const LineGeom g = {Xh, 2, Gt.RS, 1};
-  fft_dir<T, kMaxB, SIGN>(lds, kModePlain, g, g, Gt, Gt.py, s_tw);
+  fft_dir<T, kMaxB, SIGN, kMaxPass, kNT, 1, 1, RM>(lds, kModePlain, g, g, Gt, Gt.py, s_tw);
   for (int e = threadIdx.x; e < Tn * Xh; e += kNT) {
     const int t = e / Xh, x = e - t * Xh;
     dst[base + (int64_t)t * F2 + x] = lds_cpx(lds + t * Gt.RS + 2 * x, 1);
@@ -121,8 +130,9 @@ __global__ __launch_bounds__(kNT) void k_tfft(const cpx<T>* src, cpx<T>* dst, in
 // mode 0: dst = plane * scale
 // mode 1: z-step: z = plane (1/P3 folded into the solve), tol norms vs old z
 // mode 2: D-step: D = plane * scale; support gather of D + y (L3:239-240), d-norms
-template <typename T>
-__global__ __launch_bounds__(kNT) void k_plane_inv(int mode, const cpx<T>* __restrict__ src,
+template <typename T, int RM>
+__global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(slice_waves<RM>())))
+void k_plane_inv(int mode, const cpx<T>* __restrict__ src,
                                                    T* __restrict__ dst, const T* __restrict__ yv,
                                                    T* __restrict__ supp, T* __restrict__ norms,
                                                    int64_t nfirst, T scale, int r, int Tn,
@@ -142,7 +152,7 @@ __global__ __launch_bounds__(kNT) void k_plane_inv(int mode, const cpx<T>* __res
     const cpx<T>* in = src + (slice * Tn + t) * G.F;
     for (int f = threadIdx.x; f < G.F; f += kNT) lds_cpx_store(S.slice + bin_off(f, G), 1, in[f]);
   }
-  slice_c2r<T, kMaxB>(S.slice, G, S.tw);
+  slice_c2r<T, kMaxB, RM>(S.slice, G, S.tw);
   const int P = G.X * G.Y;
   const int64_t off = (slice * Tn + t) * P;
   const bool nrm = (mode == 1 && norms) || (mode == 2 && slice < nfirst);
@@ -209,7 +219,7 @@ __global__ void k_zsolve3(cpx<T>* __restrict__ C, const cpx<T>* __restrict__ Bha
 // a (slice, y, tile) block is T * TC contiguous complex.  Gt2: the t plan for K*TC lines.
 constexpr int kTsKmax = 16;   // k values per thread of k_tsolve3's solve phase
 
-template <typename T>
+template <typename T, int RM>
 __global__ __launch_bounds__(kNT) void k_tsolve3(cpx<T>* __restrict__ C,
                                                  const cpx<T>* __restrict__ Bhat,
                                                  const cpx<T>* __restrict__ dhat,
@@ -240,7 +250,7 @@ __global__ __launch_bounds__(kNT) void k_tsolve3(cpx<T>* __restrict__ C,
   }
   lds_sync();
   const LineGeom g = {NL, 2, 2 * NL, 1};
-  fft_dir<T, kMaxB, -1>(lds, kModePlain, g, g, Gt, Gt.py, s_tw);
+  fft_dir<T, kMaxB, -1, kMaxPass, kNT, 1, 1, RM>(lds, kModePlain, g, g, Gt, Gt.py, s_tw);
   // per bin (t, c): w = (B - sum_k d_k C_k) sden, C_k <- C_k / P3 + conj(d_k) w.
   // G = kNT / (T TC) threads per bin split the k range (their d_k stay in registers
   // between the two sweeps); partial sums meet in LDS past the spectra.
@@ -281,7 +291,7 @@ __global__ __launch_bounds__(kNT) void k_tsolve3(cpx<T>* __restrict__ C,
     }
   }
   lds_sync();
-  fft_dir<T, kMaxB, +1>(lds, kModePlain, g, g, Gt, Gt.py, s_tw);
+  fft_dir<T, kMaxB, +1, kMaxPass, kNT, 1, 1, RM>(lds, kModePlain, g, g, Gt, Gt.py, s_tw);
   for (int i = threadIdx.x; i < K * TT; i += kNT) {
     const int k = i / TT, rem = i - k * TT;
     const int t = rem / TC, c = rem - t * TC;
@@ -362,9 +372,14 @@ hipError_t launch_plane_fwd(int mode, const T* a, T* b, const T* usup, int sx, i
                             int o, T theta, int KG, int r, cpx<T>* dst, int64_t nslices, int Tn,
                             const cpx<T>* tw, const Grid2D& G, hipStream_t stream, int tc) {
   if (nslices <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_plane_fwd<T>, dim3((unsigned)(nslices * Tn)), dim3(kNT),
-                     slice_smem_bytes(G, sizeof(T)), stream, mode, a, b, usup, sx, sy, st, o,
-                     theta, KG, r, dst, Tn, tw, G, tc);
+  const int m = plan_mask(G.px) | plan_mask(G.py);
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3((unsigned)(nslices * Tn)), dim3(kNT),
+                       slice_smem_bytes(G, sizeof(T)), stream, mode, a, b, usup, sx, sy, st, o,
+                       theta, KG, r, dst, Tn, tw, G, tc);
+  };
+  if (rm_covers(kRm74, m)) go(k_plane_fwd<T, kRm74>);
+  else go(k_plane_fwd<T, kRmAll>);
   return hipGetLastError();
 }
 
@@ -395,12 +410,18 @@ hipError_t launch_tfft(const cpx<T>* src, cpx<T>* dst, int64_t nslices, int Yn, 
                        const cpx<T>* tw, const Grid2D& Gt, hipStream_t stream) {
   if (nslices <= 0) return hipSuccess;
   const dim3 grid((unsigned)(nslices * Yn));
-  if (sign < 0)
-    hipLaunchKernelGGL((k_tfft<T, -1>), grid, dim3(kNT), tfft_smem_bytes(Gt, sizeof(T)), stream,
-                       src, dst, Yn, F2, tw, Gt);
-  else
-    hipLaunchKernelGGL((k_tfft<T, 1>), grid, dim3(kNT), tfft_smem_bytes(Gt, sizeof(T)), stream,
-                       src, dst, Yn, F2, tw, Gt);
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, grid, dim3(kNT), tfft_smem_bytes(Gt, sizeof(T)), stream, src, dst,
+                       Yn, F2, tw, Gt);
+  };
+  const bool r42 = rm_covers(kRm42, plan_mask(Gt.py));
+  if (sign < 0) {
+    if (r42) go(k_tfft<T, -1, kRm42>);
+    else go(k_tfft<T, -1, kRmAll>);
+  } else {
+    if (r42) go(k_tfft<T, 1, kRm42>);
+    else go(k_tfft<T, 1, kRmAll>);
+  }
   return hipGetLastError();
 }
 
@@ -427,8 +448,12 @@ hipError_t launch_tsolve3(cpx<T>* C, const cpx<T>* Bhat, const cpx<T>* dhat, con
   if (!tsolve3_ok(Gt2.Y, K, TC)) return hipErrorInvalidValue;   // <= kTsKmax k per thread
   const int xtiles = (Xh + TC - 1) / TC;
   const dim3 grid((unsigned)(npatch * Yn * xtiles));
-  hipLaunchKernelGGL(k_tsolve3<T>, grid, dim3(kNT), tsolve3_smem_bytes(Gt2, K, TC, sizeof(T)),
-                     stream, C, Bhat, dhat, sden, K, Yn, Xh, TC, xtiles, invP3, tw, Gt2);
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, grid, dim3(kNT), tsolve3_smem_bytes(Gt2, K, TC, sizeof(T)), stream,
+                       C, Bhat, dhat, sden, K, Yn, Xh, TC, xtiles, invP3, tw, Gt2);
+  };
+  if (rm_covers(kRm42, plan_mask(Gt2.py))) go(k_tsolve3<T, kRm42>);
+  else go(k_tsolve3<T, kRmAll>);
   return hipGetLastError();
 }
 
@@ -437,9 +462,14 @@ hipError_t launch_plane_inv(int mode, const cpx<T>* src, T* dst, const T* yv, T*
                             int64_t nfirst, T scale, int r, int64_t nslices, int Tn,
                             const cpx<T>* tw, const Grid2D& G, hipStream_t stream, int tc) {
   if (nslices <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_plane_inv<T>, dim3((unsigned)(nslices * Tn)), dim3(kNT),
-                     slice_smem_bytes(G, sizeof(T)), stream, mode, src, dst, yv, supp, norms,
-                     nfirst, scale, r, Tn, tw, G, tc);
+  const int m = plan_mask(G.px) | plan_mask(G.py);
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3((unsigned)(nslices * Tn)), dim3(kNT),
+                       slice_smem_bytes(G, sizeof(T)), stream, mode, src, dst, yv, supp, norms,
+                       nfirst, scale, r, Tn, tw, G, tc);
+  };
+  if (rm_covers(kRm74, m)) go(k_plane_inv<T, kRm74>);
+  else go(k_plane_inv<T, kRmAll>);
   return hipGetLastError();
 }
 
