@@ -463,6 +463,7 @@ struct Session2D {
   Grid2D gt2{};            //     its t plan (K * tsolve_tc lines) and twiddles
   DevBuf twt2;
   DevBuf BhatT, dhatT, sdenT;   // B^, the filter spectrum, sden in k_tsolve3's tile order
+  int tsolve_ppw = 16;          // patches per k_tsolve3 workgroup (CCSC_TSOLVE3_PPW)
 
   // host-side log
   int outer_done = 0;
@@ -614,6 +615,7 @@ struct Session2D {
       // the three-kernel form (CCSC_TSOLVE3=0), 0.587 at TC = 1
       const char* ev = std::getenv("CCSC_TSOLVE3");
       const char* etc = std::getenv("CCSC_TSOLVE3_TC");
+      if (const char* ep = std::getenv("CCSC_TSOLVE3_PPW")) tsolve_ppw = std::max(1, std::atoi(ep));
       if (!(ev && ev[0] == '0')) {
         std::string why2;
         for (int tc : {2, 4, 1}) {
@@ -842,7 +844,8 @@ struct Session2D {
       if (tsolve_tc) {
         HIPCHK(launch_tsolve3<double>(C, BhatT.as<cpx<double>>(), dhatT.as<cpx<double>>(),
                                       sdenT.as<double>(), np, K, G.Y, G.Xh, tsolve_tc,
-                                      1.0 / (double)P, twt2.as<cpx<double>>(), gt2, st));
+                                      1.0 / (double)P, twt2.as<cpx<double>>(), gt2, st,
+                                      tsolve_ppw));
       } else {
         HIPCHK(launch_tfft<double>(C, C, np * K, G.Y, G.F, -1, twtc, g.Gt, st));
         HIPCHK(launch_zsolve3<double>(C, Bhat.as<cpx<double>>(), dhat.as<cpx<double>>(),

@@ -587,7 +587,7 @@ constexpr int kRm42 = (1 << 2) | (1 << 3) | (1 << 7);     // 42 = 2 * 3 * 7 (C4 
 // butterflies per thread of a native pass: the 74-point instantiation holds the 2 its
 // radix-2 pass needs (37 x 38 butterflies over kNT threads) instead of maxb_for_radix's 4
 __host__ __device__ constexpr int rm_maxb(int rm, int R) {
-  return rm == kRm74 ? 2 : maxb_for_radix(R);
+  return rm == kRm74 ? 2 : rm == kRm42 ? (R == 2 ? 3 : R == 3 ? 2 : 1) : maxb_for_radix(R);
 }
 
 template <typename T, int MAXB, int SIGN, int NT = kNT, int GT = 1, int BS = 1, int RM = kRmAll>
@@ -693,7 +693,18 @@ __host__ __device__ inline int plan_mask(const Plan1D& p) {
   }
   return m;
 }
-// the first of the candidate instantiations that covers mask m
+// instantiation rm runs plan p over nlines lines: it compiles every pass kind p needs
+// and holds enough butterflies per thread for each native pass
 __host__ __device__ inline bool rm_covers(int rm, int m) { return (m & ~rm) == 0; }
+__host__ inline bool rm_fits(int rm, const Plan1D& p, int nlines) {
+  if (!rm_covers(rm, plan_mask(p))) return false;
+  for (int s = 0; s < p.npass; ++s) {
+    const int R = p.rad[s];
+    if (s == 1 && p.pfa) continue;
+    if ((plan_mask(Plan1D{R, 1, {R}, {0}, 0}) & kRmGeneric) != 0) continue;
+    if ((int64_t)(p.n / R) * nlines > (int64_t)rm_maxb(rm, R) * kNT) return false;
+  }
+  return true;
+}
 
 }  // namespace ccsc

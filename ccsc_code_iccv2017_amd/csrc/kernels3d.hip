@@ -211,21 +211,25 @@ __global__ void k_zsolve3(cpx<T>* __restrict__ C, const cpx<T>* __restrict__ Bha
 }
 
 // ---- fused t-FFT + z-solve + inverse t-FFT (replaces k_tfft(-1), k_zsolve3,
-// k_tfft(+1) of the 3D z-step): one workgroup per (patch p, y row, tile of TC x'
-// columns) holds the K filters' T x TC plane-spectrum columns in LDS, layout
-// [t][k*TC + c] (K*TC complex lines of length T), so the spectra cross HBM once
-// each way per z-iteration instead of three times (L3:172-178, the closed form of
-// k_zsolve3).  C, B^, dhat and sden are in the t-minor tile order (F3t per slice):
-// a (slice, y, tile) block is T * TC contiguous complex.  Gt2: the t plan for K*TC lines.
-constexpr int kTsKmax = 16;   // k values per thread of k_tsolve3's solve phase
-
-template <typename T, int RM>
+// k_tfft(+1) of the 3D z-step): one workgroup per (y row, tile of TC x' columns,
+// group of ppw patches) holds, per patch in turn, the K filters' T x TC plane-spectrum
+// columns in LDS, layout [t][k*TC + c] (K*TC complex lines of length T), so the spectra
+// cross HBM once each way per z-iteration instead of three times (L3:172-178, the
+// closed form of k_zsolve3).  C, B^, dhat and sden are in the t-minor tile order (F3t
+// per slice): a (slice, y, tile) block is T * TC contiguous complex.  The patch loop
+// keeps the block's K filter-spectrum columns hot in L2 across the ppw patches (one
+// HBM read of dhat per workgroup instead of per patch) and prefetches the next patch's
+// block into registers (LD complex per thread) while the current one is transformed
+// (82 KB of LDS at TC = 2: one workgroup per CU, nothing else hides the HBM reads).
+// Gt2: the t plan for K*TC lines.
+template <typename T, int RM, int LD, int KMAX>
 __global__ __launch_bounds__(kNT) void k_tsolve3(cpx<T>* __restrict__ C,
                                                  const cpx<T>* __restrict__ Bhat,
                                                  const cpx<T>* __restrict__ dhat,
                                                  const T* __restrict__ sden, int K, int Yn,
                                                  int Xh, int TC, int xtiles, T invP3,
-                                                 const cpx<T>* __restrict__ twg, Grid2D Gt) {
+                                                 const cpx<T>* __restrict__ twg, Grid2D Gt,
+                                                 int64_t npatch, int ppw) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   cpx<T>* s_tw = reinterpret_cast<cpx<T>*>(smem);
   T* lds = reinterpret_cast<T*>(s_tw + Gt.ntw);
@@ -233,69 +237,111 @@ __global__ __launch_bounds__(kNT) void k_tsolve3(cpx<T>* __restrict__ C,
   const int tile = blockIdx.x % xtiles;
   const int64_t rest = blockIdx.x / xtiles;
   const int y = (int)(rest % Yn);
-  const int64_t p = rest / Yn;
+  const int64_t p0 = (rest / Yn) * ppw;
+  const int64_t p1 = min(npatch, p0 + ppw);
   const int Tn = Gt.Y;
   const int nc = min(TC, Xh - tile * TC);
   const int NL = K * TC;
   const int TT = Tn * TC;                                   // one (slice, y, tile) block
+  const int KT = K * TT;
   const int64_t F3t = (int64_t)Yn * xtiles * TT;
   const int64_t blk = (int64_t)(y * xtiles + tile) * TT;
-  cpx<T>* Cp = C + p * K * F3t + blk;
-  for (int i = threadIdx.x; i < K * TT; i += kNT) {
+  const LineGeom g = {NL, 2, 2 * NL, 1};
+  // load slot j of this thread: i = threadIdx.x + j * kNT < K * TT -> global offset
+  // (K F3t < 2^31: checked by the host) and LDS offset; recomputed where used from a
+  // laundered thread index, so the patch loop does not keep them (and every FFT pass's
+  // per-thread index math) live in registers across its iterations
+  auto slot = [&](int tid, int j, int& src, int& dst) {
+    const int i = tid + j * kNT;
     const int k = i / TT, rem = i - k * TT;
     const int t = rem / TC, c = rem - t * TC;
-    cpx<T> v = {(T)0, (T)0};
-    if (c < nc) v = Cp[(int64_t)k * F3t + rem];
-    lds_cpx_store(lds + 2 * (t * NL + k * TC + c), 1, v);
-  }
-  lds_sync();
-  const LineGeom g = {NL, 2, 2 * NL, 1};
-  fft_dir<T, kMaxB, -1, kMaxPass, kNT, 1, 1, RM>(lds, kModePlain, g, g, Gt, Gt.py, s_tw);
-  // per bin (t, c): w = (B - sum_k d_k C_k) sden, C_k <- C_k / P3 + conj(d_k) w.
-  // G = kNT / (T TC) threads per bin split the k range (their d_k stay in registers
-  // between the two sweeps); partial sums meet in LDS past the spectra.
+    src = (i < KT && c < nc) ? k * (int)F3t + rem : -1;
+    dst = i < KT ? 2 * (t * NL + k * TC + c) : -1;
+  };
+  cpx<T> pre[LD];
+  // solve-phase geometry: G = kNT / (T TC) threads per bin split the k range
   const int nb = TT;
   const int G = max(1, kNT / nb);
   const int kg = (K + G - 1) / G;
   cpx<T>* part = reinterpret_cast<cpx<T>*>(lds + 2 * (size_t)Tn * NL);   // [G][nb]
-  const int b = threadIdx.x % nb, grp = threadIdx.x / nb;
-  const int t = b / TC, c = b - t * TC;
-  const bool on = grp < G && c < nc;
-  const int64_t f3 = blk + b;                               // t * TC + c inside the block
-  T* row = lds + 2 * (t * NL + c);
-  cpx<T> dv[kTsKmax];
-  cpx<T> acc = {(T)0, (T)0};
+  {
+    const cpx<T>* Cp = C + p0 * K * F3t + blk;
 #pragma unroll
-  for (int j = 0; j < kTsKmax; ++j) {
-    const int k = grp * kg + j;
-    dv[j] = (on && j < kg && k < K) ? dhat[(int64_t)k * F3t + f3] : cpx<T>{(T)0, (T)0};
-  }
-#pragma unroll
-  for (int j = 0; j < kTsKmax; ++j) {
-    const int k = grp * kg + j;
-    if (on && j < kg && k < K) acc = cadd(acc, cmul(dv[j], lds_cpx(row + 2 * k * TC, 1)));
-  }
-  if (grp < G) part[grp * nb + b] = acc;
-  lds_sync();
-  if (on) {
-    cpx<T> tot = {(T)0, (T)0};
-    for (int q = 0; q < G; ++q) tot = cadd(tot, part[q * nb + b]);
-    const cpx<T> w = cscale(csub(Bhat[p * F3t + f3], tot), sden[f3]);
-#pragma unroll
-    for (int j = 0; j < kTsKmax; ++j) {
-      const int k = grp * kg + j;
-      if (j < kg && k < K) {
-        const cpx<T> cv = lds_cpx(row + 2 * k * TC, 1);
-        lds_cpx_store(row + 2 * k * TC, 1, cadd(cscale(cv, invP3), cmulc(dv[j], w)));
-      }
+    for (int j = 0; j < LD; ++j) {
+      int src, dst;
+      slot((int)threadIdx.x, j, src, dst);
+      pre[j] = src >= 0 ? Cp[src] : cpx<T>{(T)0, (T)0};
     }
   }
-  lds_sync();
-  fft_dir<T, kMaxB, +1, kMaxPass, kNT, 1, 1, RM>(lds, kModePlain, g, g, Gt, Gt.py, s_tw);
-  for (int i = threadIdx.x; i < K * TT; i += kNT) {
-    const int k = i / TT, rem = i - k * TT;
-    const int t = rem / TC, c = rem - t * TC;
-    if (c < nc) Cp[(int64_t)k * F3t + rem] = lds_cpx(lds + 2 * (t * NL + k * TC + c), 1);
+  for (int64_t p = p0; p < p1; ++p) {
+    int tid = (int)threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    cpx<T>* Cp = C + p * K * F3t + blk;
+#pragma unroll
+    for (int j = 0; j < LD; ++j) {
+      int src, dst;
+      slot(tid, j, src, dst);
+      if (dst >= 0) lds_cpx_store(lds + dst, 1, pre[j]);
+    }
+    lds_sync();
+    if (p + 1 < p1) {   // the next patch's block, in flight across this one's transforms
+      const cpx<T>* Cn = Cp + K * F3t;
+#pragma unroll
+      for (int j = 0; j < LD; ++j) {
+        int src, dst;
+        slot(tid, j, src, dst);
+        pre[j] = src >= 0 ? Cn[src] : cpx<T>{(T)0, (T)0};
+      }
+    }
+    fft_dir<T, kMaxB, -1, kMaxPass, kNT, 1, 1, RM>(lds, kModePlain, g, g, Gt, Gt.py, s_tw);
+    // per bin (t, c): w = (B - sum_k d_k C_k) sden, C_k <- C_k / P3 + conj(d_k) w; the
+    // d_k of a thread's k range stay in registers between the two sweeps, partial sums
+    // meet in LDS past the spectra
+    tid = (int)threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    const int b = tid % nb, grp = tid / nb;
+    const int t = b / TC, c = b - t * TC;
+    const bool on = grp < G && c < nc;
+    const int64_t f3 = blk + b;                               // t * TC + c inside the block
+    T* row = lds + 2 * (t * NL + c);
+    cpx<T> dv[KMAX];
+    cpx<T> acc = {(T)0, (T)0};
+#pragma unroll
+    for (int j = 0; j < KMAX; ++j) {
+      const int k = grp * kg + j;
+      dv[j] = (on && j < kg && k < K) ? dhat[(int64_t)k * F3t + f3] : cpx<T>{(T)0, (T)0};
+    }
+#pragma unroll
+    for (int j = 0; j < KMAX; ++j) {
+      const int k = grp * kg + j;
+      if (on && j < kg && k < K) acc = cadd(acc, cmul(dv[j], lds_cpx(row + 2 * k * TC, 1)));
+    }
+    if (grp < G) part[grp * nb + b] = acc;
+    lds_sync();
+    if (on) {
+      cpx<T> tot = {(T)0, (T)0};
+      for (int q = 0; q < G; ++q) tot = cadd(tot, part[q * nb + b]);
+      const cpx<T> w = cscale(csub(Bhat[p * F3t + f3], tot), sden[f3]);
+#pragma unroll
+      for (int j = 0; j < KMAX; ++j) {
+        const int k = grp * kg + j;
+        if (j < kg && k < K) {
+          const cpx<T> cv = lds_cpx(row + 2 * k * TC, 1);
+          lds_cpx_store(row + 2 * k * TC, 1, cadd(cscale(cv, invP3), cmulc(dv[j], w)));
+        }
+      }
+    }
+    lds_sync();
+    fft_dir<T, kMaxB, +1, kMaxPass, kNT, 1, 1, RM>(lds, kModePlain, g, g, Gt, Gt.py, s_tw);
+    tid = (int)threadIdx.x;
+    asm volatile("" : "+v"(tid));
+#pragma unroll
+    for (int j = 0; j < LD; ++j) {
+      int src, dst;
+      slot(tid, j, src, dst);
+      if (src >= 0) Cp[src] = lds_cpx(lds + dst, 1);
+    }
+    lds_sync();   // (the next patch's block overwrites the LDS)
   }
 }
 
@@ -367,18 +413,22 @@ size_t tfft_smem_bytes(const Grid2D& Gt, size_t tsize) {
   return (size_t)Gt.ntw * 2 * tsize + (size_t)Gt.Y * Gt.RS * tsize;
 }
 
+// the slice kernels' x passes run Yp/2 column-pair lines, the y passes Xh columns
+static bool slice_fits(int rm, const Grid2D& G) {
+  return rm_fits(rm, G.px, G.Yp / 2) && rm_fits(rm, G.py, G.Xh);
+}
+
 template <typename T>
 hipError_t launch_plane_fwd(int mode, const T* a, T* b, const T* usup, int sx, int sy, int st,
                             int o, T theta, int KG, int r, cpx<T>* dst, int64_t nslices, int Tn,
                             const cpx<T>* tw, const Grid2D& G, hipStream_t stream, int tc) {
   if (nslices <= 0) return hipSuccess;
-  const int m = plan_mask(G.px) | plan_mask(G.py);
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3((unsigned)(nslices * Tn)), dim3(kNT),
                        slice_smem_bytes(G, sizeof(T)), stream, mode, a, b, usup, sx, sy, st, o,
                        theta, KG, r, dst, Tn, tw, G, tc);
   };
-  if (rm_covers(kRm74, m)) go(k_plane_fwd<T, kRm74>);
+  if (slice_fits(kRm74, G)) go(k_plane_fwd<T, kRm74>);
   else go(k_plane_fwd<T, kRmAll>);
   return hipGetLastError();
 }
@@ -414,7 +464,7 @@ hipError_t launch_tfft(const cpx<T>* src, cpx<T>* dst, int64_t nslices, int Yn, 
     hipLaunchKernelGGL(kern, grid, dim3(kNT), tfft_smem_bytes(Gt, sizeof(T)), stream, src, dst,
                        Yn, F2, tw, Gt);
   };
-  const bool r42 = rm_covers(kRm42, plan_mask(Gt.py));
+  const bool r42 = rm_fits(kRm42, Gt.py, Gt.Xh);
   if (sign < 0) {
     if (r42) go(k_tfft<T, -1, kRm42>);
     else go(k_tfft<T, -1, kRmAll>);
@@ -425,11 +475,17 @@ hipError_t launch_tfft(const cpx<T>* src, cpx<T>* dst, int64_t nslices, int Yn, 
   return hipGetLastError();
 }
 
+// per-thread k range of the solve phase (<= 16 k values) and block load slots (<= 8)
+static int tsolve3_kg(int Tn, int K, int TC) {
+  const int G = std::max(1, kNT / (Tn * TC));
+  return (K + G - 1) / G;
+}
+static int tsolve3_ld(int Tn, int K, int TC) { return (K * Tn * TC + kNT - 1) / kNT; }
+
 bool tsolve3_ok(int Tn, int K, int TC) {
   const int nb = Tn * TC;
   if (nb > kNT) return false;
-  const int G = std::max(1, kNT / nb);
-  return (K + G - 1) / G <= kTsKmax;
+  return tsolve3_kg(Tn, K, TC) <= 16 && tsolve3_ld(Tn, K, TC) <= 8;
 }
 
 size_t tsolve3_smem_bytes(const Grid2D& Gt2, int K, int TC, size_t tsize) {
@@ -442,18 +498,26 @@ size_t tsolve3_smem_bytes(const Grid2D& Gt2, int K, int TC, size_t tsize) {
 template <typename T>
 hipError_t launch_tsolve3(cpx<T>* C, const cpx<T>* Bhat, const cpx<T>* dhat, const T* sden,
                           int64_t npatch, int K, int Yn, int Xh, int TC, T invP3,
-                          const cpx<T>* tw, const Grid2D& Gt2, hipStream_t stream) {
+                          const cpx<T>* tw, const Grid2D& Gt2, hipStream_t stream, int ppw) {
   if (npatch <= 0) return hipSuccess;
   if (Gt2.Xh != K * TC) return hipErrorInvalidValue;   // the plan's line count
-  if (!tsolve3_ok(Gt2.Y, K, TC)) return hipErrorInvalidValue;   // <= kTsKmax k per thread
+  if (!tsolve3_ok(Gt2.Y, K, TC)) return hipErrorInvalidValue;
   const int xtiles = (Xh + TC - 1) / TC;
-  const dim3 grid((unsigned)(npatch * Yn * xtiles));
+  if ((int64_t)K * Yn * xtiles * Gt2.Y * TC >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
+  ppw = std::max(1, std::min<int>(ppw, (int)npatch));
+  const int64_t pgroups = (npatch + ppw - 1) / ppw;
+  const dim3 grid((unsigned)(pgroups * Yn * xtiles));
+  const size_t smem = tsolve3_smem_bytes(Gt2, K, TC, sizeof(T));
   auto go = [&](auto kern) {
-    hipLaunchKernelGGL(kern, grid, dim3(kNT), tsolve3_smem_bytes(Gt2, K, TC, sizeof(T)), stream,
-                       C, Bhat, dhat, sden, K, Yn, Xh, TC, xtiles, invP3, tw, Gt2);
+    hipLaunchKernelGGL(kern, grid, dim3(kNT), smem, stream, C, Bhat, dhat, sden, K, Yn, Xh, TC,
+                       xtiles, invP3, tw, Gt2, npatch, ppw);
   };
-  if (rm_covers(kRm42, plan_mask(Gt2.py))) go(k_tsolve3<T, kRm42>);
-  else go(k_tsolve3<T, kRmAll>);
+  const bool r42 = rm_fits(kRm42, Gt2.py, Gt2.Xh);
+  const bool small = tsolve3_ld(Gt2.Y, K, TC) <= 5 && tsolve3_kg(Gt2.Y, K, TC) <= 8;
+  if (r42 && small) go(k_tsolve3<T, kRm42, 5, 8>);
+  else if (r42) go(k_tsolve3<T, kRm42, 8, 16>);
+  else if (small) go(k_tsolve3<T, kRmAll, 5, 8>);
+  else go(k_tsolve3<T, kRmAll, 8, 16>);
   return hipGetLastError();
 }
 
@@ -462,13 +526,12 @@ hipError_t launch_plane_inv(int mode, const cpx<T>* src, T* dst, const T* yv, T*
                             int64_t nfirst, T scale, int r, int64_t nslices, int Tn,
                             const cpx<T>* tw, const Grid2D& G, hipStream_t stream, int tc) {
   if (nslices <= 0) return hipSuccess;
-  const int m = plan_mask(G.px) | plan_mask(G.py);
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3((unsigned)(nslices * Tn)), dim3(kNT),
                        slice_smem_bytes(G, sizeof(T)), stream, mode, src, dst, yv, supp, norms,
                        nfirst, scale, r, Tn, tw, G, tc);
   };
-  if (rm_covers(kRm74, m)) go(k_plane_inv<T, kRm74>);
+  if (slice_fits(kRm74, G)) go(k_plane_inv<T, kRm74>);
   else go(k_plane_inv<T, kRmAll>);
   return hipGetLastError();
 }
@@ -514,7 +577,7 @@ template hipError_t launch_plane_inv<double>(int, const cpx<double>*, double*, c
 template hipError_t launch_tsolve3<double>(cpx<double>*, const cpx<double>*,
                                            const cpx<double>*, const double*, int64_t, int, int,
                                            int, int, double, const cpx<double>*, const Grid2D&,
-                                           hipStream_t);
+                                           hipStream_t, int);
 template hipError_t launch_zsolve3<double>(cpx<double>*, const cpx<double>*, const cpx<double>*,
                                            const double*, int64_t, int64_t, int, double,
                                            hipStream_t);
