@@ -75,11 +75,39 @@ constexpr size_t kZlWBytes = 0;
 constexpr size_t kZlSmem = zl::kSmem + kZlWBytes;
 static_assert(kZlSmem <= 160 * 1024, "z-step LDS");
 
+// clamp(a, -theta, theta): the prox and the dual update of a z-iteration are
+// u = soft(a, theta) = a - clamp(a) and u - y = 2u - a = a - 2 clamp(a) (min/max + one
+// add or FMA each, no compare/select chains)
 template <typename T>
-__device__ __forceinline__ T soft_l(T a, T theta) {
-  return (fabs(a) > theta) ? a - copysign(theta, a) : (T)0;
+__device__ __forceinline__ T clamp_t(T a, T theta) {
+  return fmax(-theta, fmin(a, theta));
 }
 
+
+#ifdef CCSC_ABL_LDSLIN
+// timing-only ablation (wrong results): every LDS access of the slice loop goes to a
+// lane-linear, conflict-free slot (register r of wave w: slot lane + 64 (r mod 16) + 1024 (w mod 6))
+template <typename T>
+__device__ __forceinline__ cpx<T>& ablx(int r) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  return reinterpret_cast<cpx<T>*>(smem)[(threadIdx.x & 63) + 64 * (r & 15) + 1024 * ((threadIdx.x >> 6) % 6)];
+}
+#define LX(expr, r) ablx<T>(r)
+#else
+#define LX(expr, r) (expr)
+#endif
+
+// CCSC_ABL_NODFT (timing only, wrong results): the line DFTs of the slice loop pass their
+// inputs through unchanged (no butterfly arithmetic)
+template <typename T, int R, int SIGN, typename Sink>
+__device__ __forceinline__ void zdft(cpx<T> (&v)[R], Sink&& sink) {
+#ifdef CCSC_ABL_NODFT
+#pragma unroll
+  for (int q = 0; q < R; ++q) sink(q, v[q]);
+#else
+  dft_sink<T, R, SIGN>(v, sink);
+#endif
+}
 
 __device__ __forceinline__ void wave_lds_fence() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -97,25 +125,25 @@ __device__ __forceinline__ void wave_lds_fence() {
 template <typename T, int ES, typename Sink>
 __device__ __forceinline__ void fwd_line(cpx<T> (&v)[11], cpx<T>* E, int s, Sink&& sink) {
   const int sa = min(s, 9);
-  dft_sink<T, 11, -1>(v, [&](int k2, cpx<T> val) { E[(sa * 11 + k2) * ES] = val; });
+  zdft<T, 11, -1>(v, [&](int k2, cpx<T> val) { LX(E[(sa * 11 + k2) * ES], k2) = val; });
   wave_lds_fence();
   cpx<T> in[10];
 #pragma unroll
-  for (int n1 = 0; n1 < 10; ++n1) in[n1] = E[(n1 * 11 + s) * ES];
-  dft_sink<T, 10, -1>(in, sink);
+  for (int n1 = 0; n1 < 10; ++n1) in[n1] = LX(E[(n1 * 11 + s) * ES], n1);
+  zdft<T, 10, -1>(in, sink);
 }
 
 // Inverse (unnormalised) 110-point transform, layout B (in[k1], lane k2 = s)
 // -> layout A (out[n2], lane n1 = s < 10).
 template <typename T, int ES, typename Sink>
 __device__ __forceinline__ void inv_line(cpx<T> (&in)[10], cpx<T>* E, int s, Sink&& sink) {
-  dft_sink<T, 10, +1>(in, [&](int n1, cpx<T> val) { E[(n1 * 11 + s) * ES] = val; });
+  zdft<T, 10, +1>(in, [&](int n1, cpx<T> val) { LX(E[(n1 * 11 + s) * ES], n1) = val; });
   wave_lds_fence();
   const int sa = min(s, 9);
   cpx<T> v[11];
 #pragma unroll
-  for (int k2 = 0; k2 < 11; ++k2) v[k2] = E[(sa * 11 + k2) * ES];
-  dft_sink<T, 11, +1>(v, sink);
+  for (int k2 = 0; k2 < 11; ++k2) v[k2] = LX(E[(sa * 11 + k2) * ES], k2);
+  zdft<T, 11, +1>(v, sink);
 }
 
 __device__ __forceinline__ void zl_sync() {
@@ -132,6 +160,21 @@ __device__ __forceinline__ void zl_sync() {
 __device__ __forceinline__ int mod110(int e) { return e >= 110 ? e - 110 : e; }
 // slot of element x of a row pair's spectrum Z_j in layout-B order (k1*11 + k2)
 __device__ __forceinline__ int zslot(int x) { return (x % 10) * 11 + (x % 11); }
+
+// LDS bank placement (gfx950: a ds_read_b128 serves 16 lanes per cycle, one 16-B chunk of
+// the 256-B bank row each; tools/lds_sim.py models every access of this kernel):
+//  * T rows (P1 sink, P3 reads): column c at tcol(c) = even columns then odd ones -- the
+//    P3 reads of one register all have one column parity, which on the natural order
+//    leaves them 8 of the 16 chunks (modelled 2486 -> 1650 LDS cycles per slice);
+//  * a wave's five x-lines exchange at line offsets 110 l + {0, 0, 11, 12, 16} and store
+//    their spectra Z_j at 110 l + {0, 6, 7, 8, 11} of the wave's ten T rows (570 slots)
+//    instead of 110 l / 114 l (exchanges 2068 -> 1485, P7 reads 2968 -> 1888).
+// Every region a wave writes between two barriers stays inside the ten rows it alone
+// reads in P3, as before.
+__device__ __forceinline__ int tcol(int c) { return (c >> 1) + (c & 1) * 28; }
+__device__ __forceinline__ int xoff(int l) { return 110 * l + (l < 2 ? 0 : l == 2 ? 11 : l == 3 ? 12 : 16); }
+__device__ __forceinline__ int zoff(int l) { return 110 * l + (l < 1 ? 0 : l < 4 ? 5 + l : 11); }
+constexpr int kZlWR = 10 * zl::RS;   // complex slots of a wave's ten T rows
 
 // 16-B global access at a 32-bit byte offset from a wave-uniform base (saddr form:
 // SGPR base + one VGPR offset, no 64-bit VGPR address per access).
@@ -242,6 +285,7 @@ __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn
                 "zline tol variant");
   constexpr bool kStore = TOL & kZtStore, kCmp = TOL & kZtCmp, kForm = TOL & kZtForm;
   using V2 = typename vec2_t<T>::type;
+  theta = __builtin_canonicalize(theta);   // no per-use quieting in clamp_t's min/max
   extern __shared__ __attribute__((aligned(16))) char smem[];
   cpx<T>* sT = reinterpret_cast<cpx<T>*>(smem);
   const int64_t p = blockIdx.x;
@@ -279,8 +323,8 @@ __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn
     const int sb = min(s, 10), sa = min(s, 9);
     const int c = min(5 * wave + l, 55);   // y-line (column)
     const int j = min(5 * wave + l, 54);   // x-line (row pair)
-    cpx<T>* Ey = sT + c;                                       // column c: slot i at row i
-    cpx<T>* Ex = sT + 10 * min(wave, 10) * zl::RS + l * 110;   // the wave's rows, line l
+    cpx<T>* Ey = sT + tcol(c);   // the line's own T column (where P1 stores): slot i at row i
+    cpx<T>* Ex = sT + kZlWR * min(wave, 10) + xoff(l);   // the wave's rows, line l
     const int64_t sl = (p * K + k) * zl::P;
     cpx<T> zc[11];   // c = u - y of the row pair (x-lines, layout A) for the R2C
     const uint32_t po = (uint32_t)(j * 10 + fresh(sa)) * 16u;   // pair n2 at po + n2*550*16
@@ -301,7 +345,7 @@ __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn
         b[k1] = cmulc(zld<cpx<T>>(dk, bo + k1 * 616 * 16), zld<cpx<T>>(Wp, bo + k1 * 616 * 16));
 #endif
       inv_line<T, zl::RS>(b, Ey, sb, [&](int n2, cpx<T> val) {
-        sT[mod110(11 * sa + 10 * n2) * zl::RS + c] = val;
+        LX(sT[mod110(11 * sa + 10 * n2) * zl::RS + tcol(c)], n2 + 5) = val;
       });
       zl_sync();   // P2
       if (xwave) {
@@ -314,12 +358,10 @@ __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn
         for (int k1 = 0; k1 < 10; ++k1) {
           const int x = mod110(xb + 11 * k1);
           const bool hi = x >= zl::Xh;
-          const int cc = hi ? zl::X - x : x;
-          cpx<T> a = r0[cc], bb = r0[zl::RS + cc];
-          const T sg = hi ? (T)-1 : (T)1;
-          a.y *= sg;
-          bb.y *= sg;
-          zb[k1] = {a.x - bb.y, a.y + bb.x};
+          const int cc = tcol(hi ? zl::X - x : x);
+          const cpx<T> a = LX(r0[cc], 2 * k1), bb = LX(r0[zl::RS + cc], 2 * k1 + 1);
+          const T sg = hi ? (T)-1 : (T)1;   // conjugate both rows above Xh
+          zb[k1] = {fma(-sg, bb.y, a.x), fma(sg, a.y, bb.x)};
         }
         // ---- P4: state (row 2j, row 2j+1) at x = elem_a(n1, n2), in flight under the C2R;
         // each corr value is consumed as the last inverse stage forms it ----
@@ -335,8 +377,9 @@ __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn
         const T own = (s < 10 && lane < 55) ? (T)1 : (T)0;
         inv_line<T, 1>(zb, Ex, s3, [&](int n2, cpx<T> corr) {
           V2 a = av[n2];
-          const T sx = soft_l(a.x, theta), sy = soft_l(a.y, theta);
-          const T ctx = sx - (a.x - sx), cty = sy - (a.y - sy);   // c_t = u - y
+          const T tx = clamp_t(a.x, theta), ty = clamp_t(a.y, theta);
+          const T sx = a.x - tx, sy = a.y - ty;                          // u = soft(a)
+          const T ctx = fma((T)-2, tx, a.x), cty = fma((T)-2, ty, a.y);   // c_t = u - y
           if constexpr (kStore) {   // z_cur = (u - y)(A) + corr
             V2 zn;
             zn.x = ctx + corr.x;
@@ -352,8 +395,7 @@ __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn
             a.x = sx + corr.x;
             a.y = sy + corr.y;
             sst<V2>(Ao + sl, po + n2 * 550 * 16, a);
-            const T ux = soft_l(a.x, theta), uy = soft_l(a.y, theta);
-            zc[n2] = {ux - (a.x - ux), uy - (a.y - uy)};
+            zc[n2] = {fma((T)-2, clamp_t(a.x, theta), a.x), fma((T)-2, clamp_t(a.y, theta), a.y)};
             if constexpr (kForm) {   // c_t+1 - c_t and c_t+1 of the lanes' own elements
               const T dx = zc[n2].x - ctx, dy = zc[n2].y - cty;
               fd += own * (dx * dx + dy * dy);
@@ -377,8 +419,7 @@ __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn
 #pragma unroll
         for (int n2 = 0; n2 < 11; ++n2) {
           const V2 a = av[n2];
-          const T ux = soft_l(a.x, theta), uy = soft_l(a.y, theta);
-          zc[n2] = {ux - (a.x - ux), uy - (a.y - uy)};
+          zc[n2] = {fma((T)-2, clamp_t(a.x, theta), a.x), fma((T)-2, clamp_t(a.y, theta), a.y)};
         }
       }
       V2 zv[kStore ? 11 : 1];
@@ -409,8 +450,8 @@ __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn
     // ---- P5: x-R2C of the row pair -> Z_j into rows 2j, 2j+1 of T ----
     if (xwave) {
       const int s5 = fresh(sb);
-      cpx<T>* r0 = sT + 2 * j * zl::RS;   // Z_j in layout-B slot order (zslot)
-      fwd_line<T, 1>(zc, Ex, s5, [&](int k1, cpx<T> val) { r0[k1 * 11 + s5] = val; });
+      cpx<T>* r0 = sT + kZlWR * min(wave, 10) + zoff(l);   // Z_j in layout-B slot order (zslot)
+      fwd_line<T, 1>(zc, Ex, s5, [&](int k1, cpx<T> val) { LX(r0[k1 * 11 + s5], k1 + 3) = val; });
     }
     zl_sync();   // P6
     // ---- P7: column c, rows y = n1 + 10 n2: two-for-one separation ----
@@ -418,15 +459,17 @@ __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn
     {
       const int n1 = fresh(sa);
       const int zc1 = zslot(c), zc2 = zslot((c == 0) ? 0 : zl::X - c);
-      // even rows: (z1 + conj z2) / 2; odd rows: (z1 - conj z2) / 2i (row parity = n1's)
+      // even rows: z1 + conj z2; odd rows: (z1 - conj z2) / i (row parity = n1's) -- twice
+      // the row spectra: the 1/2 is applied once to the patch's accumulated bins
       const bool odd = n1 & 1;
 #pragma unroll
       for (int n2 = 0; n2 < 11; ++n2) {
-        const int y = mod110(11 * n1 + 10 * n2);
-        const cpx<T>* r0 = sT + (y >> 1) * (2 * zl::RS);
-        const cpx<T> z1 = r0[zc1], z2 = r0[zc2];
-        const T ex = (T)0.5 * (z1.x + z2.x), ey = (T)0.5 * (z1.y - z2.y);
-        const T ox = (T)0.5 * (z1.y + z2.y), oy = (T)-0.5 * (z1.x - z2.x);
+        // row y = (11 n1 + 10 n2) mod 110: pair y >> 1 is line n1 >> 1 of wave (n1 + n2) mod 11
+        const int wv = n1 + n2 >= 11 ? n1 + n2 - 11 : n1 + n2;
+        const cpx<T>* r0 = sT + kZlWR * wv + zoff(n1 >> 1);
+        const cpx<T> z1 = LX(r0[zc1], n2), z2 = LX(r0[zc2], n2 + 11);
+        const T ex = z1.x + z2.x, ey = z1.y - z2.y;
+        const T ox = z1.y + z2.y, oy = z2.x - z1.x;
         col[n2] = {odd ? ox : ex, odd ? oy : ey};
       }
     }
@@ -443,6 +486,8 @@ __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn
   }
   // w = (B - acc) * sden  (sden = 1/((rho + s) X Y)); each lane owns its slots
   if constexpr (MODE != 3) {
+#pragma unroll
+    for (int i = 0; i < 10; ++i) acc[i] = cscale(acc[i], (T)0.5);   // P7's unscaled separation
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int l = lane / 11, s = lane - 11 * l, line = 5 * wave + l;
     if (l < 5 && line < 56) {
@@ -522,6 +567,7 @@ __global__ __launch_bounds__(zl::NT) void k_zhat_line(const T* __restrict__ A,
   const cpx<T>* Wp = W + p * zl::F;
   const bool xwave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6) < 11;
   const T sc = (T)zl::P;
+  theta = __builtin_canonicalize(theta);
   for (int kk = 0; kk < KB; ++kk) {
     const int k = k0 + kk;
     if (k >= K) break;   // uniform
@@ -532,7 +578,7 @@ __global__ __launch_bounds__(zl::NT) void k_zhat_line(const T* __restrict__ A,
     const int sb = min(s, 10), sa = min(s, 9);
     const int c = min(5 * wave + l, 55);
     const int j = min(5 * wave + l, 54);
-    cpx<T>* Ey = sT + c;
+    cpx<T>* Ey = sT + tcol(c);
     cpx<T>* Ex = sT + 10 * min(wave, 10) * zl::RS + l * 110;
     const int64_t sl = (p * K + k) * zl::P;
     if (xwave) {
@@ -542,11 +588,10 @@ __global__ __launch_bounds__(zl::NT) void k_zhat_line(const T* __restrict__ A,
 #pragma unroll
       for (int n2 = 0; n2 < 11; ++n2) {
         const V2 a = zld<V2>(A + sl, po + n2 * 550 * 16);
-        const T ux = soft_l(a.x, theta), uy = soft_l(a.y, theta);
-        zc[n2] = {ux - (a.x - ux), uy - (a.y - uy)};
+        zc[n2] = {fma((T)-2, clamp_t(a.x, theta), a.x), fma((T)-2, clamp_t(a.y, theta), a.y)};
       }
       const int s5 = fresh(sb);
-      cpx<T>* r0 = sT + 2 * j * zl::RS;
+      cpx<T>* r0 = sT + kZlWR * min(wave, 10) + zoff(l);
       fwd_line<T, 1>(zc, Ex, s5, [&](int k1, cpx<T> val) { r0[k1 * 11 + s5] = val; });
     }
     lds_sync();
@@ -555,14 +600,15 @@ __global__ __launch_bounds__(zl::NT) void k_zhat_line(const T* __restrict__ A,
     {
       const int n1 = fresh(sa);
       const int zc1 = zslot(c), zc2 = zslot((c == 0) ? 0 : zl::X - c);
-      const bool odd = n1 & 1;
+      const bool odd = n1 & 1;   // twice the row spectra, halved at the store
 #pragma unroll
       for (int n2 = 0; n2 < 11; ++n2) {
-        const int y = mod110(11 * n1 + 10 * n2);
-        const cpx<T>* r0 = sT + (y >> 1) * (2 * zl::RS);
+        // row y = (11 n1 + 10 n2) mod 110: pair y >> 1 is line n1 >> 1 of wave (n1 + n2) mod 11
+        const int wv = n1 + n2 >= 11 ? n1 + n2 - 11 : n1 + n2;
+        const cpx<T>* r0 = sT + kZlWR * wv + zoff(n1 >> 1);
         const cpx<T> z1 = r0[zc1], z2 = r0[zc2];
-        const T ex = (T)0.5 * (z1.x + z2.x), ey = (T)0.5 * (z1.y - z2.y);
-        const T ox = (T)0.5 * (z1.y + z2.y), oy = (T)-0.5 * (z1.x - z2.x);
+        const T ex = z1.x + z2.x, ey = z1.y - z2.y;
+        const T ox = z1.y + z2.y, oy = z2.x - z1.x;
         col[n2] = {odd ? ox : ex, odd ? oy : ey};
       }
     }
@@ -575,7 +621,7 @@ __global__ __launch_bounds__(zl::NT) void k_zhat_line(const T* __restrict__ A,
       cpx<T>* out = dst + (p * K + k) * (int64_t)zl::F + c;
       fwd_line<T, zl::RS>(col, Ey, s9, [&](int k1, cpx<T> cb) {
         const cpx<T> q = cmulc(zld<cpx<T>>(dk, bo + k1 * 616 * 16), zld<cpx<T>>(Wp, bo + k1 * 616 * 16));
-        out[zl::elem_b(s9, k1) * zl::Xh] = {cb.x + sc * q.x, cb.y + sc * q.y};
+        out[zl::elem_b(s9, k1) * zl::Xh] = {fma((T)0.5, cb.x, sc * q.x), fma((T)0.5, cb.y, sc * q.y)};
       });
     }
     lds_sync();   // the next slice's P5 rewrites the rows of T
