@@ -331,6 +331,22 @@ constexpr int kDsJB = CCSC_DS_JB;
 #endif
 constexpr bool kDsBwRed = CCSC_DS_BWRED;   // A/B: reduction backward for every NVB
 
+// x[u] for a wave-uniform u < RPL (unrolled selects: no runtime register indexing)
+template <typename T, int RPL>
+__device__ __forceinline__ cpx<T> pick_reg(const cpx<T> (&x)[RPL], int u) {
+  cpx<T> r = x[0];
+#pragma unroll
+  for (int q = 1; q < RPL; ++q)
+    if (u == q) r = x[q];
+  return r;
+}
+template <typename T, int RPL>
+__device__ __forceinline__ void put_reg(cpx<T> (&x)[RPL], int u, cpx<T> v) {
+#pragma unroll
+  for (int q = 0; q < RPL; ++q)
+    if (u == q) x[q] = v;
+}
+
 template <typename T, int RPL, int NVB>
 __global__ __launch_bounds__(256) void k_dsolve(const cpx<T>* __restrict__ L,
                                                 const cpx<T>* __restrict__ h,
@@ -393,12 +409,8 @@ __global__ __launch_bounds__(256) void k_dsolve(const cpx<T>* __restrict__ L,
         const T inv = (T)1 / dg[jj];
 #pragma unroll
         for (int v = 0; v < NVB; ++v) {
-          const cpx<T> xs = (tj == 0) ? x[v][0] : x[v][RPL - 1];
-          const cpx<T> xj = cscale(readlane_c(xs, src), inv);
-          if (lane == src) {
-            if (tj == 0) x[v][0] = xj;
-            else x[v][RPL - 1] = xj;
-          }
+          const cpx<T> xj = cscale(readlane_c(pick_reg<T, RPL>(x[v], tj), src), inv);
+          if (lane == src) put_reg<T, RPL>(x[v], tj, xj);
 #pragma unroll
           for (int u = 0; u < RPL; ++u) {
             const int i = lane + 64 * u;
@@ -441,10 +453,7 @@ __global__ __launch_bounds__(256) void k_dsolve(const cpx<T>* __restrict__ L,
           }
           part.x = wave_sum_dpp(part.x);
           part.y = wave_sum_dpp(part.y);
-          if (lane == src) {
-            if (tj == 0) x[v][0] = cscale(csub(x[v][0], part), inv);
-            else x[v][RPL - 1] = cscale(csub(x[v][RPL - 1], part), inv);
-          }
+          if (lane == src) put_reg<T, RPL>(x[v], tj, cscale(csub(pick_reg<T, RPL>(x[v], tj), part), inv));
         }
       }
     }
@@ -472,12 +481,8 @@ __global__ __launch_bounds__(256) void k_dsolve(const cpx<T>* __restrict__ L,
         const T inv = (T)1 / dg[jj];
 #pragma unroll
         for (int v = 0; v < NVB; ++v) {
-          const cpx<T> xs = (tp == 0) ? x[v][0] : x[v][RPL - 1];
-          const cpx<T> xp = cscale(readlane_c(xs, src), inv);
-          if (lane == src) {
-            if (tp == 0) x[v][0] = xp;
-            else x[v][RPL - 1] = xp;
-          }
+          const cpx<T> xp = cscale(readlane_c(pick_reg<T, RPL>(x[v], tp), src), inv);
+          if (lane == src) put_reg<T, RPL>(x[v], tp, xp);
 #pragma unroll
           for (int u = 0; u < RPL; ++u)
             if (lane + 64 * u < p) x[v][u] = csub(x[v][u], cmulc(lr[jj][u], xp));
@@ -532,6 +537,9 @@ hipError_t launch_dsolve(const cpx<T>* L, const cpx<T>* h, const cpx<T>* Ch, cpx
   } else if (K <= 128) {
     if (NV == 1) dsolve_go<T, 2, 1>(grid, st, L, h, Ch, Dh, F, K, rho, fgroups, NV);
     else dsolve_go<T, 2, 4>(grid, st, L, h, Ch, Dh, F, K, rho, fgroups, NV);
+  } else if (K <= 192) {
+    if (NV == 1) dsolve_go<T, 3, 1>(grid, st, L, h, Ch, Dh, F, K, rho, fgroups, NV);
+    else dsolve_go<T, 3, 4>(grid, st, L, h, Ch, Dh, F, K, rho, fgroups, NV);
   } else {
     return hipErrorInvalidValue;
   }

@@ -305,7 +305,7 @@ static void check_supported(const ccsc_problem& p, Geom* Gout) {
   if (p.variant != CCSC_HS23 && (int64_t)p.K * p.views[0] * p.views[1] > 2048)
     throw Err(CCSC_E_UNSUPPORTED, "K * views > 2048 exceeds the gram kernel's RHS budget");
   if (p.precision != CCSC_FP64) throw Err(CCSC_E_UNSUPPORTED, "only CCSC_FP64 is built");
-  if (p.K > 110) throw Err(CCSC_E_UNSUPPORTED, "K > 110 exceeds the gram kernel's tile budget");
+  if (p.K > 192) throw Err(CCSC_E_UNSUPPORTED, "K > 192 exceeds the gram kernel's tile budget");
   if (p.dfactor == CCSC_DFACTOR_WOODBURY && (p.variant == CCSC_HS23 || !woodbury_ok(p.K, p.ni)))
     throw Err(CCSC_E_UNSUPPORTED, "the Woodbury D-factor needs ni <= 8 and ni K + ni^2 <= K (K + 1) / 2 "
                                   "(consensus learners only)");
@@ -1553,9 +1553,13 @@ struct SessionHS {
     // z_hat = fft2(z) (L23:100) and v_D{1} = H z of the first d-iteration (L23:108)
     objective_fresh();
     // opt_f = (Z_f' Z_f + rho I)^-1 as a Cholesky factor per bin (L23:290)
-    HIPCHK(launch_gram_chol<double>(Zh.as<cpx<double>>(), Zh.as<cpx<double>>(),
-                                    L.as<cpx<double>>(), h.as<cpx<double>>(), F, K, n, p.rho_d, 0,
-                                    st));
+    if (K > 128)   // beyond the LDS-resident VALU factor: the matrix-core kernel (no RHS here)
+      HIPCHK(launch_gram_chol_mf(Zh.as<cpx<double>>(), Zh.as<cpx<double>>(), L.as<cpx<double>>(),
+                                 h.as<cpx<double>>(), F, K, n, p.rho_d, 0, st));
+    else
+      HIPCHK(launch_gram_chol<double>(Zh.as<cpx<double>>(), Zh.as<cpx<double>>(),
+                                      L.as<cpx<double>>(), h.as<cpx<double>>(), F, K, n, p.rho_d,
+                                      0, st));
     for (int id = 0; id < p.max_it_d; ++id) {                                    // L23:102
       // c = 1: masked data split (L23:112, 117, 120-121)
       HIPCHK(launch_hs_data_r2c<double>(v.as<double>(), eD.as<double>(), bdev.as<double>(),

@@ -27,12 +27,19 @@ namespace ccsc {
 typedef double d4 __attribute__((ext_vector_type(4)));
 
 constexpr int kGcNT = 256;                  // 4 waves
-constexpr int kGcTM = 7;                    // tiles per dimension (K <= 112)
-constexpr int kGcTiles = kGcTM * (kGcTM + 1) / 2;
-constexpr int kGcTW = (kGcTiles + 3) / 4;   // tiles per wave
+// TM = tiles per dimension, K <= 16 TM: TM = 7 (K <= 112, the headline K = 100) runs two
+// workgroups per CU; TM = 8, 10, 12 (K <= 192) hold up to 20 accumulator tiles per wave
+// (320 of the 512 registers) at one workgroup per CU
+template <int TM>
+struct GcShape {
+  static constexpr int Tiles = TM * (TM + 1) / 2;
+  static constexpr int TW = (Tiles + 3) / 4;   // tiles per wave
+  static constexpr int KP = 16 * TM;           // padded filter count of a staged row
+  static constexpr int LD = KP + 1;            // staged row stride (complex)
+  static constexpr int WGS = TM <= 7 ? 2 : 1;  // workgroups per CU
+};
+constexpr int kGcMaxTM = 12;
 constexpr int kGcPC = 16;                   // patches per staged chunk
-constexpr int kGcKP = 16 * kGcTM;           // padded filter count of a staged row
-constexpr int kGcLD = kGcKP + 1;            // staged row stride (complex)
 constexpr int kGcTS = 17;                   // column stride (complex) of an LDS tile
 constexpr int kGcTSZ = 16 * kGcTS;          // complex per LDS tile
 constexpr int kGcHPT = 8;                   // right-hand-side entries of h per thread
@@ -63,15 +70,16 @@ __device__ __forceinline__ void gc_tile(int t, int& I, int& J) {
 // step and filter 16 T + (l & 15) of tile row/column T).  Tile coordinates are
 // wave-uniform runtime values: operands are loaded per tile from LDS, so no
 // register array is indexed at run time.
+template <int TM>
 __device__ __forceinline__ void gram_kstep(const cpx<double>* row, int w, int Tn,
-                                           d4 (&gr)[kGcTW], d4 (&gi)[kGcTW]) {
+                                           d4 (&gr)[GcShape<TM>::TW], d4 (&gi)[GcShape<TM>::TW]) {
   const int lane = threadIdx.x & 63;
 #pragma unroll
-  for (int s = 0; s < kGcTW; ++s) {
+  for (int s = 0; s < GcShape<TM>::TW; ++s) {
     const int t = w + 4 * s;
     int I, J;
     gc_tile(t, I, J);
-    if (t < kGcTiles && I < Tn) {
+    if (t < GcShape<TM>::Tiles && I < Tn) {
       const cpx<double> a = row[16 * I + (lane & 15)];
       const cpx<double> b = row[16 * J + (lane & 15)];
       gr[s] = mfma(a.x, b.x, gr[s]);
@@ -94,16 +102,18 @@ __device__ __forceinline__ void tile_to_lds(cpx<double>* dst, const d4& re, cons
 // trailing update of wave w's tiles (i, k), k > j: A_ik -= L_ij L_kj^H, the panel
 // tiles L_.j in P (P[i * kGcTSZ + col * kGcTS + row]); then the tiles of column
 // j + 1 to the next panel buffer Pn
+template <int TM>
 __device__ __forceinline__ void trail_step(const cpx<double>* P, cpx<double>* Pn, int j, int w,
-                                           int Tn, d4 (&gr)[kGcTW], d4 (&gi)[kGcTW]) {
+                                           int Tn, d4 (&gr)[GcShape<TM>::TW],
+                                           d4 (&gi)[GcShape<TM>::TW]) {
   const int lane = threadIdx.x & 63;
   const int row = lane & 15, c4 = lane >> 4;
 #pragma unroll
-  for (int s = 0; s < kGcTW; ++s) {
+  for (int s = 0; s < GcShape<TM>::TW; ++s) {
     const int t = w + 4 * s;
     int I, J;
     gc_tile(t, I, J);
-    if (t < kGcTiles && I < Tn && J > j) {
+    if (t < GcShape<TM>::Tiles && I < Tn && J > j) {
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) {
         const int col = 4 * kk + c4;
@@ -119,27 +129,30 @@ __device__ __forceinline__ void trail_step(const cpx<double>* P, cpx<double>* Pn
   }
 }
 
+template <int TM>
 __device__ __forceinline__ void first_panel(cpx<double>* P, int w, int Tn,
-                                            const d4 (&gr)[kGcTW], const d4 (&gi)[kGcTW]) {
+                                            const d4 (&gr)[GcShape<TM>::TW],
+                                            const d4 (&gi)[GcShape<TM>::TW]) {
 #pragma unroll
-  for (int s = 0; s < kGcTW; ++s) {
+  for (int s = 0; s < GcShape<TM>::TW; ++s) {
     const int t = w + 4 * s;
     int I, J;
     gc_tile(t, I, J);
-    if (t < kGcTiles && I < Tn && J == 0) tile_to_lds(P + I * kGcTSZ, gr[s], gi[s]);
+    if (t < GcShape<TM>::Tiles && I < Tn && J == 0) tile_to_lds(P + I * kGcTSZ, gr[s], gi[s]);
   }
 }
 
 // rho on the diagonal (exactly real), identity on the padding rows K..16 Tn - 1
-__device__ __forceinline__ void fix_diag(int w, int K, int Tn, double rho, d4 (&gr)[kGcTW],
-                                         d4 (&gi)[kGcTW]) {
+template <int TM>
+__device__ __forceinline__ void fix_diag(int w, int K, int Tn, double rho,
+                                         d4 (&gr)[GcShape<TM>::TW], d4 (&gi)[GcShape<TM>::TW]) {
   const int lane = threadIdx.x & 63;
 #pragma unroll
-  for (int s = 0; s < kGcTW; ++s) {
+  for (int s = 0; s < GcShape<TM>::TW; ++s) {
     const int t = w + 4 * s;
     int I, J;
     gc_tile(t, I, J);
-    if (t < kGcTiles && I < Tn && I == J) {
+    if (t < GcShape<TM>::Tiles && I < Tn && I == J) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int rr = (lane >> 4) + 4 * r, cc = lane & 15;
@@ -152,7 +165,8 @@ __device__ __forceinline__ void fix_diag(int w, int K, int Tn, double rho, d4 (&
   }
 }
 
-__global__ __launch_bounds__(kGcNT, 2) void k_gram_chol_mf(const cpx<double>* __restrict__ Zh,
+template <int TM>
+__global__ __launch_bounds__(kGcNT, GcShape<TM>::WGS) void k_gram_chol_mf(const cpx<double>* __restrict__ Zh,
                                                            const cpx<double>* __restrict__ Bh,
                                                            cpx<double>* __restrict__ L,
                                                            cpx<double>* __restrict__ h, int F,
@@ -160,6 +174,8 @@ __global__ __launch_bounds__(kGcNT, 2) void k_gram_chol_mf(const cpx<double>* __
   const int per = gridDim.x >> 3;
   const int f = (blockIdx.x & 7) * per + (blockIdx.x >> 3);   // XCD-aware: neighbours share L2
   if (f >= F) return;
+  using S = GcShape<TM>;
+  constexpr int kGcTW = S::TW, kGcKP = S::KP, kGcLD = S::LD, kGcTM = TM;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   cpx<double>* sA = reinterpret_cast<cpx<double>*>(smem);      // [2][kGcPC][kGcLD]
   cpx<double>* sB = sA + 2 * kGcPC * kGcLD;                    // [2][kGcPC][NV]
@@ -215,7 +231,7 @@ __global__ __launch_bounds__(kGcNT, 2) void k_gram_chol_mf(const cpx<double>* __
     for (int kk = 0; kk < kGcPC / 4; ++kk) {
       const cpx<double>* row = a + (4 * kk + (lane >> 4)) * kGcLD;
 #ifndef CCSC_ABL_NOGRAM
-      gram_kstep(row, wave, Tn, gr, gi);
+      gram_kstep<TM>(row, wave, Tn, gr, gi);
 #endif
     }
     const cpx<double>* b = sB + buf * kGcPC * NV;
@@ -237,12 +253,12 @@ __global__ __launch_bounds__(kGcNT, 2) void k_gram_chol_mf(const cpx<double>* __
     const int q = tid + i * kGcNT;
     if (q < KV) h[(int64_t)f * KV + q] = hacc[i];
   }
-  fix_diag(wave, K, Tn, rho, gr, gi);
+  fix_diag<TM>(wave, K, Tn, rho, gr, gi);
 
   // ---- blocked Cholesky over the tile columns ----
   cpx<double>* Pbuf = reinterpret_cast<cpx<double>*>(smem);   // [2][kGcTM][kGcTSZ]
   cpx<double>* Lf = L + (int64_t)f * (K * (K + 1) / 2);
-  first_panel(Pbuf, wave, Tn, gr, gi);
+  first_panel<TM>(Pbuf, wave, Tn, gr, gi);
 #ifdef CCSC_ABL_NOCHOL
   Tn = 0;   // ablation build: skip the factorisation (timing only)
 #endif
@@ -253,7 +269,7 @@ __global__ __launch_bounds__(kGcNT, 2) void k_gram_chol_mf(const cpx<double>* __
     // Panel j (POTRF of tile (j, j) + TRSM of the tiles below) in one left-looking
     // sweep over its 16 columns, every wave on its own: lanes 0..15 hold the rows of
     // tile (j, j) (all four waves redundantly, so no wave waits for another), lanes
-    // 16..39 up to 24 of the panel's other rows.  Column c of row r:
+    // 16..16 + RW - 1 up to RW = 4 (TM - 1) of the panel's other rows.  Column c of row r:
     //   s = a[r][c] - sum_{k < c} L[r][k] conj(L[c][k]);  L[c][c] = sqrt(s of row c),
     //   L[r][c] = s / L[c][c]  (the POTRF and TRSM formulas coincide),
     // L[c][k] read back as LDS broadcasts from the wave's own copy Lw of the diagonal
@@ -261,13 +277,15 @@ __global__ __launch_bounds__(kGcNT, 2) void k_gram_chol_mf(const cpx<double>* __
     {
       cpx<double>* Lw = Pbuf + 2 * kGcTM * kGcTSZ + wave * kGcTSZ;
       const bool diag = lane < 16;
-      const int q = wave * 24 + lane - 16;
+      constexpr int RW = 4 * (TM - 1);   // panel rows below the diagonal tile per wave (<= 48)
+      static_assert(16 + RW <= 64, "panel rows per wave");
+      const int q = wave * RW + lane - 16;
       const int ti = diag ? j : j + 1 + (q >> 4);
       const int row = diag ? lane : (q & 15);
 #ifdef CCSC_ABL_NOTRSM
       const bool mine = diag;
 #else
-      const bool mine = diag || (lane < 40 && ti < Tn);
+      const bool mine = diag || (lane < 16 + RW && ti < Tn);
 #endif
       cpx<double> x[16];
 #pragma unroll
@@ -331,26 +349,43 @@ __global__ __launch_bounds__(kGcNT, 2) void k_gram_chol_mf(const cpx<double>* __
     }
     __syncthreads();   // the panel L_.j is in P
 #ifndef CCSC_ABL_NOTRAIL
-    if (j + 1 < Tn) trail_step(P, Pn, j, wave, Tn, gr, gi);
+    if (j + 1 < Tn) trail_step<TM>(P, Pn, j, wave, Tn, gr, gi);
 #endif
   }
 }
 
-bool gram_chol_mf_ok(int K, int NV) { return K <= kGcKP && K * NV <= kGcHPT * kGcNT && NV <= 16; }
+static int gc_tm(int K) { const int t = (K + 15) / 16; return t <= 7 ? 7 : t <= 8 ? 8 : t <= 10 ? 10 : 12; }
 
-size_t gram_chol_mf_smem(int NV) {
-  const size_t stage = (size_t)2 * kGcPC * kGcLD * 16 + (size_t)2 * kGcPC * NV * 16;
-  const size_t chol = (size_t)(2 * kGcTM + 4) * kGcTSZ * 16;   // two panels + the waves' L_jj
+bool gram_chol_mf_ok(int K, int NV) {
+  return K <= 16 * kGcMaxTM && K * NV <= kGcHPT * kGcNT && NV <= 16;
+}
+
+size_t gram_chol_mf_smem(int NV, int K) {
+  const int tm = gc_tm(K);
+  const size_t stage = (size_t)2 * kGcPC * (16 * tm + 1) * 16 + (size_t)2 * kGcPC * NV * 16;
+  const size_t chol = (size_t)(2 * tm + 4) * kGcTSZ * 16;   // two panels + the waves' L_jj
   return stage > chol ? stage : chol;
+}
+
+template <int TM>
+static void gram_chol_mf_go(const cpx<double>* Zh, const cpx<double>* Bh, cpx<double>* L,
+                            cpx<double>* h, int F, int K, int ni, double rho, int NV,
+                            hipStream_t st) {
+  const int grid = ((F + 7) / 8) * 8;
+  hipLaunchKernelGGL(k_gram_chol_mf<TM>, dim3(grid), dim3(kGcNT), gram_chol_mf_smem(NV, K), st,
+                     Zh, Bh, L, h, F, K, ni, rho, NV);
 }
 
 hipError_t launch_gram_chol_mf(const cpx<double>* Zh, const cpx<double>* Bh, cpx<double>* L,
                                cpx<double>* h, int F, int K, int ni, double rho, int NV,
                                hipStream_t st) {
   if (!gram_chol_mf_ok(K, NV)) return hipErrorInvalidValue;
-  const int grid = ((F + 7) / 8) * 8;
-  hipLaunchKernelGGL(k_gram_chol_mf, dim3(grid), dim3(kGcNT), gram_chol_mf_smem(NV), st, Zh, Bh,
-                     L, h, F, K, ni, rho, NV);
+  switch (gc_tm(K)) {
+    case 7: gram_chol_mf_go<7>(Zh, Bh, L, h, F, K, ni, rho, NV, st); break;
+    case 8: gram_chol_mf_go<8>(Zh, Bh, L, h, F, K, ni, rho, NV, st); break;
+    case 10: gram_chol_mf_go<10>(Zh, Bh, L, h, F, K, ni, rho, NV, st); break;
+    default: gram_chol_mf_go<12>(Zh, Bh, L, h, F, K, ni, rho, NV, st); break;
+  }
   return hipGetLastError();
 }
 

@@ -232,6 +232,83 @@ __device__ __forceinline__ void sst(void* base, uint32_t boff, V v) {
   zst<V>(base, boff, v);
 #endif
 }
+// Buffer-descriptor forms of the slice loop's global accesses (CCSC_ZL_BUF): the
+// wave-uniform base goes into a descriptor, the lane's byte offset into voffset and
+// the register's constant offset into soffset (an SGPR), so no per-access 64-bit
+// VGPR address arithmetic is issued (tools/gpu_ab_zl.sh).
+#ifndef CCSC_ZL_BUF
+#define CCSC_ZL_BUF 1
+#endif
+#ifndef CCSC_ZL_BUF_F
+#define CCSC_ZL_BUF_F CCSC_ZL_BUF
+#endif
+#ifndef CCSC_ZL_BUF_W
+#define CCSC_ZL_BUF_W CCSC_ZL_BUF
+#endif
+#ifndef CCSC_ZL_BUF_S
+#define CCSC_ZL_BUF_S CCSC_ZL_BUF
+#endif
+#if CCSC_ZL_BUF
+typedef unsigned int zl_u4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t zrsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+#ifndef CCSC_ZL_BUF_AUX
+#define CCSC_ZL_BUF_AUX 2
+#endif
+constexpr int kZlNT = CCSC_ZL_BUF_AUX;   // cache policy bit: nontemporal (gfx950 NT = SLC)
+template <typename V, int AUX>
+__device__ __forceinline__ V bld(const void* base, uint32_t bytes, uint32_t voff, uint32_t soff) {
+  const zl_u4 u = __builtin_amdgcn_raw_buffer_load_b128(zrsrc(base, bytes), voff, soff, AUX);
+  V v;
+  __builtin_memcpy(&v, &u, 16);
+  return v;
+}
+template <typename V, int AUX>
+__device__ __forceinline__ void bst(void* base, uint32_t bytes, uint32_t voff, uint32_t soff, V v) {
+  zl_u4 u;
+  __builtin_memcpy(&u, &v, 16);
+  __builtin_amdgcn_raw_buffer_store_b128(u, zrsrc(base, bytes), voff, soff, AUX);
+}
+#endif
+// spectrum (F complex) access: lane offset + register offset
+template <typename V>
+__device__ __forceinline__ V fld(const void* base, uint32_t lane, uint32_t reg) {
+#if CCSC_ZL_BUF && CCSC_ZL_BUF_F && !defined(CCSC_ABL_NODK)
+  return bld<V, 0>(base, zl::F * 16, lane, reg);
+#else
+  return dld<V>(base, lane + reg);
+#endif
+}
+template <typename V>
+__device__ __forceinline__ V wld(const void* base, uint32_t lane, uint32_t reg) {
+#if CCSC_ZL_BUF && CCSC_ZL_BUF_W
+  return bld<V, 0>(base, zl::F * 16, lane, reg);
+#else
+  return zld<V>(base, lane + reg);
+#endif
+}
+// state slice (P reals) access, nontemporal
+template <typename V>
+__device__ __forceinline__ V sld2(const void* base, uint32_t lane, uint32_t reg) {
+#if CCSC_ZL_BUF && CCSC_ZL_BUF_S && CCSC_ZL_NT && !defined(CCSC_ABL_NOSTATE) && !defined(CCSC_ABL_NOSTLOAD)
+  return bld<V, kZlNT>(base, zl::P * 8, lane, reg);
+#else
+  return sld<V>(base, lane + reg);
+#endif
+}
+// (state stores stay global stores: the buffer-store form of this in-place update -- the
+// descriptor built from the same base the slice was loaded through -- failed the mode-2
+// parity cases on the GPU while the buffer-load form passes: tools/gpu_var_test.sh)
+template <typename V>
+__device__ __forceinline__ void sst2(void* base, uint32_t lane, uint32_t reg, V v) {
+#if defined(CCSC_ZL_BUF_SS) && CCSC_ZL_BUF && CCSC_ZL_BUF_S && CCSC_ZL_NT && !defined(CCSC_ABL_NOSTATE) && !defined(CCSC_ABL_NOSTSTORE)
+  bst<V, kZlNT>(base, zl::P * 8, lane, reg, v);
+#else
+  sst<V>(base, lane + reg, v);
+#endif
+}
+
 // an opaque copy of a lane index: per-lane address math is redone where it is used
 // instead of being hoisted out of the slice loop into (spilled) registers
 __device__ __forceinline__ int fresh(int v) {
@@ -339,8 +416,8 @@ __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn
 #pragma unroll
       for (int k1 = 0; k1 < 10; ++k1)
 #if CCSC_ZL_WLDS
-        b[k1] = cmulc(dld<cpx<T>>(dk, bo + k1 * 616 * 16),
-                      wl ? sW[k1 * 385 + c * 11 + sb] : zld<cpx<T>>(Wp, bo + k1 * 616 * 16));
+        b[k1] = cmulc(fld<cpx<T>>(dk, bo, k1 * 616 * 16),
+                      wl ? sW[k1 * 385 + c * 11 + sb] : wld<cpx<T>>(Wp, bo, k1 * 616 * 16));
 #else
         b[k1] = cmulc(zld<cpx<T>>(dk, bo + k1 * 616 * 16), zld<cpx<T>>(Wp, bo + k1 * 616 * 16));
 #endif
@@ -367,11 +444,11 @@ __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn
         // each corr value is consumed as the last inverse stage forms it ----
         V2 av[11];
 #pragma unroll
-        for (int n2 = 0; n2 < 11; ++n2) av[n2] = sld<V2>(A + sl, po + n2 * 550 * 16);
+        for (int n2 = 0; n2 < 11; ++n2) av[n2] = sld2<V2>(A + sl, po, n2 * 550 * 16);
         V2 zo[kCmp ? 11 : 1];
         if constexpr (kCmp) {
 #pragma unroll
-          for (int n2 = 0; n2 < 11; ++n2) zo[n2] = sld<V2>(Zt + sl, po + n2 * 550 * 16);
+          for (int n2 = 0; n2 < 11; ++n2) zo[n2] = sld2<V2>(Zt + sl, po, n2 * 550 * 16);
         }
         // lanes that own their elements (not a clamped duplicate) count in the norms
         const T own = (s < 10 && lane < 55) ? (T)1 : (T)0;
@@ -389,12 +466,12 @@ __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn
               nd += own * (ex * ex + ey * ey);
               nz += own * (zn.x * zn.x + zn.y * zn.y);
             }
-            sst<V2>(Zt + sl, po + n2 * 550 * 16, zn);
+            sst2<V2>(Zt + sl, po, n2 * 550 * 16, zn);
           }
           if constexpr (MODE == 2) {
             a.x = sx + corr.x;
             a.y = sy + corr.y;
-            sst<V2>(Ao + sl, po + n2 * 550 * 16, a);
+            sst2<V2>(Ao + sl, po, n2 * 550 * 16, a);
             zc[n2] = {fma((T)-2, clamp_t(a.x, theta), a.x), fma((T)-2, clamp_t(a.y, theta), a.y)};
             if constexpr (kForm) {   // c_t+1 - c_t and c_t+1 of the lanes' own elements
               const T dx = zc[n2].x - ctx, dy = zc[n2].y - cty;
@@ -480,7 +557,7 @@ __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn
       const cpx<T>* dk = dhat + (int64_t)k * zl::F;
       const uint32_t bo = (uint32_t)(c * 11 + s9) * 16u;
       fwd_line<T, zl::RS>(col, Ey, s9, [&](int k1, cpx<T> cb) {
-        acc[k1] = cadd(acc[k1], cmul(dld<cpx<T>>(dk, bo + k1 * 616 * 16), cb));
+        acc[k1] = cadd(acc[k1], cmul(fld<cpx<T>>(dk, bo, k1 * 616 * 16), cb));
       });
     }
   }
