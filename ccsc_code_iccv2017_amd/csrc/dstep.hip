@@ -329,7 +329,10 @@ constexpr int kDsJB = CCSC_DS_JB;
 #ifndef CCSC_DS_BWRED
 #define CCSC_DS_BWRED 0
 #endif
-constexpr bool kDsBwRed = CCSC_DS_BWRED;   // A/B: reduction backward for every NVB
+constexpr bool kDsBwRed = CCSC_DS_BWRED;
+#ifndef CCSC_DS_NV8
+#define CCSC_DS_NV8 1   // A/B: 8 right-hand sides per factor sweep when NV > 4 (K <= 128)
+#endif   // A/B: reduction backward for every NVB
 
 // x[u] for a wave-uniform u < RPL (unrolled selects: no runtime register indexing)
 template <typename T, int RPL>
@@ -535,8 +538,10 @@ hipError_t launch_dsolve(const cpx<T>* L, const cpx<T>* h, const cpx<T>* Ch, cpx
     else if (NV <= 4) dsolve_go<T, 1, 4>(grid, st, L, h, Ch, Dh, F, K, rho, fgroups, NV);
     else dsolve_go<T, 1, 8>(grid, st, L, h, Ch, Dh, F, K, rho, fgroups, NV);
   } else if (K <= 128) {
+    // many right-hand sides (L23's W = 31 wavelengths): 8 per sweep over the factor
     if (NV == 1) dsolve_go<T, 2, 1>(grid, st, L, h, Ch, Dh, F, K, rho, fgroups, NV);
-    else dsolve_go<T, 2, 4>(grid, st, L, h, Ch, Dh, F, K, rho, fgroups, NV);
+    else if (NV <= 4 || !CCSC_DS_NV8) dsolve_go<T, 2, 4>(grid, st, L, h, Ch, Dh, F, K, rho, fgroups, NV);
+    else dsolve_go<T, 2, 8>(grid, st, L, h, Ch, Dh, F, K, rho, fgroups, NV);
   } else if (K <= 192) {
     if (NV == 1) dsolve_go<T, 3, 1>(grid, st, L, h, Ch, Dh, F, K, rho, fgroups, NV);
     else dsolve_go<T, 3, 4>(grid, st, L, h, Ch, Dh, F, K, rho, fgroups, NV);
