@@ -297,13 +297,14 @@ __device__ __forceinline__ V sld2(const void* base, uint32_t lane, uint32_t reg)
   return sld<V>(base, lane + reg);
 #endif
 }
-// (state stores stay global stores: the buffer-store form of this in-place update -- the
-// descriptor built from the same base the slice was loaded through -- failed the mode-2
-// parity cases on the GPU while the buffer-load form passes: tools/gpu_var_test.sh)
+// (state stores stay global stores by default: a buffer store carrying the register offset
+// in soffset failed the mode-2 parity cases on the GPU -- with either cache policy and with a
+// larger range -- while the same store with the whole offset in voffset passes, and then it
+// costs the same per-store VGPR add as the global store: tools/gpu_var_test.sh)
 template <typename V>
 __device__ __forceinline__ void sst2(void* base, uint32_t lane, uint32_t reg, V v) {
 #if defined(CCSC_ZL_BUF_SS) && CCSC_ZL_BUF && CCSC_ZL_BUF_S && CCSC_ZL_NT && !defined(CCSC_ABL_NOSTATE) && !defined(CCSC_ABL_NOSTSTORE)
-  bst<V, kZlNT>(base, zl::P * 8, lane, reg, v);
+  bst<V, kZlNT>(base, zl::P * 8, lane + reg, 0, v);
 #else
   sst<V>(base, lane + reg, v);
 #endif
