@@ -430,6 +430,13 @@ struct Session2D {
   // st3 beside block j's Gram/Cholesky, filling that kernel's last partial round
   hipStream_t st3 = nullptr;
   hipEvent_t ev_s = nullptr, ev_z = nullptr, ev_gz[2] = {nullptr, nullptr};
+  // 110 grid, tol = 0: a z-phase's launches split over two streams (patches [0, np/2) on st,
+  // the rest on st3, idle during the z-phase), so each stream's next launch starts as soon as
+  // its own half is done and fills the other's partial last round of workgroups (a C2 launch
+  // is 39.06 rounds of one workgroup per CU); the halves couple only at the phase ends
+  bool zsplit_open = false;
+  hipEvent_t zsp_a = nullptr;
+  int zsp_n = 0;
   DevBuf Zh2;
   int64_t N, nbl, b0, np;
   bool owner0;
@@ -477,7 +484,7 @@ struct Session2D {
 
   // profiling
   bool prof = false;
-  struct Rec { int id; hipEvent_t a, b; };
+  struct Rec { int id; hipEvent_t a, b; int n = 1; };   // n launches between a and b
   std::vector<Rec> recs;
   std::vector<hipEvent_t> pool;
   int64_t k_launch[5] = {0, 0, 0, 0, 0};
@@ -510,7 +517,7 @@ struct Session2D {
       float ms = 0;
       HIPCHK(hipEventSynchronize(rc.b));
       HIPCHK(hipEventElapsedTime(&ms, rc.a, rc.b));
-      k_launch[rc.id] += 1;
+      k_launch[rc.id] += rc.n;
       k_ms[rc.id] += ms;
       pool.push_back(rc.a);
       pool.push_back(rc.b);
@@ -830,6 +837,28 @@ struct Session2D {
   double* fpart() { return znorm.as<double>() + 2 * np; }
   // one z-iteration over the local patches (dP:147-157; 4D L4:163-167; 3D L3:164-178).
   // The other z-steps leave the test of the produced iterate in znorm when tol_on.
+  bool zsplit_ok(bool tol_on) const {
+    const char* e = std::getenv("CCSC_ZSPLIT2");   // A/B: CCSC_ZSPLIT2=0 keeps one stream
+    const bool on = !(e && e[0] == '0');
+    return on && zl_on && !tol_on && zmode == 2 && st3 && np >= 1024;
+  }
+  // both halves of a split z-phase done before anything else reads the state on st
+  void zsplit_join() {
+    if (!zsplit_open) return;
+    hipEvent_t e = get_event(), b = get_event();
+    HIPCHK(hipEventRecord(e, st3));
+    HIPCHK(hipStreamWaitEvent(st, e, 0));
+    HIPCHK(hipEventRecord(b, st));
+    pool.push_back(e);
+    if (prof) {
+      recs.push_back(Rec{0, zsp_a, b, zsp_n});
+    } else {
+      pool.push_back(zsp_a);
+      pool.push_back(b);
+    }
+    zsplit_open = false;
+  }
+
   ZTests zstep_iter(bool tol_on) {
     const auto* twc = tw.as<cpx<double>>();
     if (is4) {
@@ -862,6 +891,29 @@ struct Session2D {
       // d-phase, or a materialised state) it stores the z it starts from in `yz`, and the
       // next launch measures that iterate against it (Cmp, one launch late)
       const int mode = zmode == 2 ? 2 : 0;
+      if (zsplit_ok(tol_on)) {
+        if (!zsplit_open) {
+          zsp_a = get_event();
+          HIPCHK(hipEventRecord(zsp_a, st));
+          HIPCHK(hipStreamWaitEvent(st3, zsp_a, 0));
+          zsplit_open = true;
+          zsp_n = 0;
+        }
+        const int64_t na = np / 2;
+        const int64_t zo = na * K * (int64_t)P, wo = na * (int64_t)F;
+        HIPCHK(launch_zline<double>(z.as<double>(), z.as<double>(), z.as<double>(), yz.as<double>(),
+                                    W.as<cpx<double>>(), Bhs.as<cpx<double>>(), dws,
+                                    dhs.as<cpx<double>>(), sdens.as<double>(), na, K, theta,
+                                    p.rho_z, 2, st, 0, nullptr, nullptr, nullptr));
+        HIPCHK(launch_zline<double>(z.as<double>() + zo, z.as<double>() + zo, z.as<double>() + zo,
+                                    yz.as<double>() + zo, W.as<cpx<double>>() + wo,
+                                    Bhs.as<cpx<double>>() + wo, dws, dhs.as<cpx<double>>(),
+                                    sdens.as<double>(), np - na, K, theta, p.rho_z, 2, st3, 0,
+                                    nullptr, nullptr, nullptr));
+        ++zsp_n;
+        dws = dhs.as<cpx<double>>();
+        return ZTests{};
+      }
       const bool same = mode == 2 && dws == dhs.as<cpx<double>>();
       int tolv = 0;
       if (tol_on) {
@@ -1179,7 +1231,10 @@ struct Session2D {
     bool zbreak = false;
     for (int iz = 0; iz < p.max_it_z; ++iz) {
       ZTests zt_done;
-      timed(0, [&] { zt_done = zstep_iter(tol_on); });
+      if (zsplit_ok(tol_on))
+        zt_done = zstep_iter(tol_on);   // timed as one phase record by zsplit_join
+      else
+        timed(0, [&] { zt_done = zstep_iter(tol_on); });
       ++nz;
       if (zt_done.lagged && z_test(iz - 1, zpart(), np) < p.tol) {   // dP:165-167 for iz - 1
         zl_rollback();
@@ -1197,6 +1252,7 @@ struct Session2D {
         zd = z_test(iz, znorm.as<double>(), np * K * Tn);
       }
       if (want_oz) {
+        zsplit_join();
         const double o = objective_timed(dhat.as<cpx<double>>());
         if (verbose_refresh_z()) obj_z = o;
         if (p.trace_objective) tr_oz[(size_t)it * p.max_it_z + iz] = o;
@@ -1206,6 +1262,7 @@ struct Session2D {
         break;
       }
     }
+    zsplit_join();
     if (zl_tol && !zbreak && zt == ZT_PREV) {   // the last iteration's test
       zl_finalize();
       z_test(nz - 1, zpart(), np);
