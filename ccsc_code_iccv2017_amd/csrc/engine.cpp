@@ -430,7 +430,7 @@ struct Session2D {
   // st3 beside block j's Gram/Cholesky, filling that kernel's last partial round
   hipStream_t st3 = nullptr;
   hipEvent_t ev_s = nullptr, ev_z = nullptr, ev_gz[2] = {nullptr, nullptr};
-  // 110 grid, tol = 0: a z-phase's launches split over two streams (patches [0, np/2) on st,
+  // 110 grid, tol = 0, >= 512 patches: a z-phase's launches split over two streams (patches [0, np/2) on st,
   // the rest on st3, idle during the z-phase), so each stream's next launch starts as soon as
   // its own half is done and fills the other's partial last round of workgroups (a C2 launch
   // is 39.06 rounds of one workgroup per CU); the halves couple only at the phase ends
@@ -840,7 +840,7 @@ struct Session2D {
   bool zsplit_ok(bool tol_on) const {
     const char* e = std::getenv("CCSC_ZSPLIT2");   // A/B: CCSC_ZSPLIT2=0 keeps one stream
     const bool on = !(e && e[0] == '0');
-    return on && zl_on && !tol_on && zmode == 2 && st3 && np >= 1024;
+    return on && zl_on && !tol_on && zmode == 2 && st3 && np >= 512;
   }
   // both halves of a split z-phase done before anything else reads the state on st
   void zsplit_join() {

@@ -665,7 +665,7 @@ __global__ __launch_bounds__(zl::NT) void k_zhat_line(const T* __restrict__ A,
       cpx<T> zc[11];
 #pragma unroll
       for (int n2 = 0; n2 < 11; ++n2) {
-        const V2 a = zld<V2>(A + sl, po + n2 * 550 * 16);
+        const V2 a = sld2<V2>(A + sl, po, n2 * 550 * 16);
         zc[n2] = {fma((T)-2, clamp_t(a.x, theta), a.x), fma((T)-2, clamp_t(a.y, theta), a.y)};
       }
       const int s5 = fresh(sb);
@@ -698,7 +698,7 @@ __global__ __launch_bounds__(zl::NT) void k_zhat_line(const T* __restrict__ A,
       const uint32_t bo = (uint32_t)(c * 11 + s9) * 16u;
       cpx<T>* out = dst + (p * K + k) * (int64_t)zl::F + c;
       fwd_line<T, zl::RS>(col, Ey, s9, [&](int k1, cpx<T> cb) {
-        const cpx<T> q = cmulc(zld<cpx<T>>(dk, bo + k1 * 616 * 16), zld<cpx<T>>(Wp, bo + k1 * 616 * 16));
+        const cpx<T> q = cmulc(fld<cpx<T>>(dk, bo, k1 * 616 * 16), wld<cpx<T>>(Wp, bo, k1 * 616 * 16));
         out[zl::elem_b(s9, k1) * zl::Xh] = {fma((T)0.5, cb.x, sc * q.x), fma((T)0.5, cb.y, sc * q.y)};
       });
     }
