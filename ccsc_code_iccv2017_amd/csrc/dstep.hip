@@ -545,6 +545,15 @@ hipError_t launch_dsolve(const cpx<T>* L, const cpx<T>* h, const cpx<T>* Ch, cpx
   } else if (K <= 192) {
     if (NV == 1) dsolve_go<T, 3, 1>(grid, st, L, h, Ch, Dh, F, K, rho, fgroups, NV);
     else dsolve_go<T, 3, 4>(grid, st, L, h, Ch, Dh, F, K, rho, fgroups, NV);
+  } else if (K <= 256) {   // factors of gramchol_big.hip
+    if (NV == 1) dsolve_go<T, 4, 1>(grid, st, L, h, Ch, Dh, F, K, rho, fgroups, NV);
+    else dsolve_go<T, 4, 4>(grid, st, L, h, Ch, Dh, F, K, rho, fgroups, NV);
+  } else if (K <= 320) {
+    if (NV == 1) dsolve_go<T, 5, 1>(grid, st, L, h, Ch, Dh, F, K, rho, fgroups, NV);
+    else dsolve_go<T, 5, 4>(grid, st, L, h, Ch, Dh, F, K, rho, fgroups, NV);
+  } else if (K <= 400) {
+    if (NV == 1) dsolve_go<T, 7, 1>(grid, st, L, h, Ch, Dh, F, K, rho, fgroups, NV);
+    else dsolve_go<T, 7, 4>(grid, st, L, h, Ch, Dh, F, K, rho, fgroups, NV);
   } else {
     return hipErrorInvalidValue;
   }

@@ -305,7 +305,11 @@ static void check_supported(const ccsc_problem& p, Geom* Gout) {
   if (p.variant != CCSC_HS23 && (int64_t)p.K * p.views[0] * p.views[1] > 2048)
     throw Err(CCSC_E_UNSUPPORTED, "K * views > 2048 exceeds the gram kernel's RHS budget");
   if (p.precision != CCSC_FP64) throw Err(CCSC_E_UNSUPPORTED, "only CCSC_FP64 is built");
-  if (p.K > 192) throw Err(CCSC_E_UNSUPPORTED, "K > 192 exceeds the gram kernel's tile budget");
+  // K <= 192: the register-resident MFMA factor (gramchol.hip); 192 < K <= 400: the
+  // HBM-resident Gram + left-looking Cholesky of gramchol_big.hip (consensus learners)
+  if (p.K > 400) throw Err(CCSC_E_UNSUPPORTED, "K > 400 exceeds the d-solve's rows per lane");
+  if (p.K > 192 && p.variant == CCSC_HS23)
+    throw Err(CCSC_E_UNSUPPORTED, "the 2-3D learner's factor holds K <= 192");
   if (p.dfactor == CCSC_DFACTOR_WOODBURY && (p.variant == CCSC_HS23 || !woodbury_ok(p.K, p.ni)))
     throw Err(CCSC_E_UNSUPPORTED, "the Woodbury D-factor needs ni <= 8 and ni K + ni^2 <= K (K + 1) / 2 "
                                   "(consensus learners only)");
@@ -347,9 +351,9 @@ static bool zline_usable(const Grid2D& G) {
 // memory plan shared by ccsc_plan_bytes and the session
 struct Plan2D {
   int64_t np, nbl, b0;
-  size_t z, yz, cbuf, W, dhw, D, yD, Bhat, b, L, h, Ch, Dh, Zh, E, zl, misc;
+  size_t z, yz, cbuf, W, dhw, D, yD, Bhat, b, L, h, Ch, Dh, Zh, E, zl, big, misc;
   size_t total() const {
-    return z + yz + cbuf + W + dhw + D + yD + Bhat + b + L + h + Ch + Dh + Zh + E + zl + misc;
+    return z + yz + cbuf + W + dhw + D + yD + Bhat + b + L + h + Ch + Dh + Zh + E + zl + big + misc;
   }
 };
 
@@ -383,6 +387,8 @@ static Plan2D plan2d(const ccsc_problem& p, const Geom& g, int rank, int nranks)
   m.Ch = m.nbl * K * NV * F * 16;
   m.Dh = m.Ch;
   m.Zh = (size_t)p.ni * K * F * 16;
+  // K > 192 (gramchol_big.hip): the block's code spectra transposed frequency-major
+  m.big = (K > 192 && p.dfactor != CCSC_DFACTOR_WOODBURY) ? m.Zh : 0;
   // 4D: view correlations E; 3D: spectra of the z-step's plane/t transforms, in the
   // t-minor tile order when k_tsolve3 runs (padded to whole tiles: sized for TC = 4),
   // with B^, the filter spectrum and sden in that order (misc)
@@ -423,6 +429,8 @@ struct Session2D {
   bool woodbury;   // D-factor in Woodbury form (p.dfactor; AUTO: woodbury_fits, ni << K)
   bool gram_mf;    // Gram + Cholesky on the matrix cores (gramchol.hip; CCSC_GRAM_MF=0: VALU form)
   bool dtile = false;   // tile d-solve on a factor with inverted diagonal tiles (dstep.hip)
+  bool gram_big = false;   // K > 192: HBM-resident Gram + Cholesky (gramchol_big.hip), X its workspace
+  DevBuf Xbig;
   // the diagonal-tile inversion of block j runs on st2 beside block j+1's precompute R2C
   hipStream_t st2 = nullptr;
   hipEvent_t ev_g = nullptr, ev_i = nullptr;
@@ -582,6 +590,7 @@ struct Session2D {
     {
       const char* ev = std::getenv("CCSC_GRAM_MF");
       gram_mf = gram_chol_mf_ok(K, NV) && !(ev && ev[0] == '0');
+      gram_big = !woodbury && K > 192 && gram_big_ok(K, NV);
       // tile d-solve (one read of the factor per solve) on the MFMA factor with inverted
       // diagonal tiles; CCSC_DS_TILE=0 keeps the two-sweep k_dsolve
       const char* et = std::getenv("CCSC_DS_TILE");
@@ -672,6 +681,7 @@ struct Session2D {
     L.alloc(m.L);
     h.alloc(m.h);
     Zh.alloc(m.Zh);
+    if (gram_big) Xbig.alloc(m.big);
     dhat.alloc((size_t)KG * F * 16);
     dtmp.alloc((size_t)KG * F * 16);
     sden.alloc((size_t)F * 8);
@@ -1113,6 +1123,8 @@ struct Session2D {
         cpx<double>* hj = h.as<cpx<double>>() + (size_t)jl * F * NV * K;
         if (woodbury)
           HIPCHK(launch_gram_wb<double>(Zc, Bj, Lj, hj, F, K, ni, p.rho_d, NV, st));
+        else if (gram_big)
+          HIPCHK(launch_gram_big(Zc, Bj, Xbig.as<cpx<double>>(), Lj, hj, F, K, ni, p.rho_d, NV, st));
         else if (gram_mf) {
           HIPCHK(launch_gram_chol_mf(Zc, Bj, Lj, hj, F, K, ni, p.rho_d, NV, st));
           if (dtile) {

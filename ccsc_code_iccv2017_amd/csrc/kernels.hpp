@@ -110,6 +110,13 @@ bool gram_chol_mf_ok(int K, int NV);
 hipError_t launch_gram_chol_mf(const cpx<double>* Zh, const cpx<double>* Bh, cpx<double>* L,
                                cpx<double>* h, int F, int K, int ni, double rho, int NV,
                                hipStream_t st);
+// The same outputs for 192 < K <= 400 (gramchol_big.hip): the block's code spectra
+// transposed into X ([F][ni][K], ni K F complex of workspace), the Gram on the matrix
+// cores into the packed slots of L, then a left-looking Cholesky in place.
+bool gram_big_ok(int K, int NV);
+hipError_t launch_gram_big(const cpx<double>* Zh, const cpx<double>* Bh, cpx<double>* X,
+                           cpx<double>* L, cpx<double>* h, int F, int K, int ni, double rho, int NV,
+                           hipStream_t st);
 // x_{f,uv} = (L L^H)^{-1} (h_{f,uv} + rho * C_{f,uv}) for every (block, f, view);
 // C and Dh are [blk][K][NV][F].
 template <typename T>

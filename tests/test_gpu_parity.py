@@ -61,7 +61,14 @@ def _case(variant, sb, psf, K, n, ni, seed):
                                            # K > 112: the 8-tile (K = 128, two-sweep d-solve)
                                            # and 12-tile (K = 170, RPL = 3) MFMA factor
                                            ((12, 12), 5, 128, 256, 128),
-                                           ((12, 12), 5, 170, 170, 170)])
+                                           ((12, 12), 5, 170, 170, 170),
+                                           # K > 192: the HBM-resident Gram + left-looking
+                                           # Cholesky (gramchol_big.hip), d-solve RPL = 4, 5, 7;
+                                           # K = 400 = 25 tiles, the largest supported (few
+                                           # patches per block keep the oracle in seconds)
+                                           ((12, 12), 5, 200, 24, 12),
+                                           ((12, 12), 5, 260, 6, 3),
+                                           ((12, 12), 5, 400, 4, 2)])
 def test_learn_2d_matches_oracle(gpu_ctx, variant, sb, psf, K, n, ni):
     from ccsc_code_iccv2017_amd import learners as E
     b, d0, z0 = _case(variant, sb, psf, K, n, ni, seed=7)
@@ -247,12 +254,12 @@ def test_dfactor_woodbury_rejected_when_blocks_too_large(gpu_ctx):
 
 
 def test_k_above_the_factor_budget_rejected(gpu_ctx):
-    """K <= 192 runs (the 12-tile MFMA factor); larger K is a clean CCSC_E_UNSUPPORTED."""
+    """K <= 400 runs (K > 192: gramchol_big.hip); larger K is a clean CCSC_E_UNSUPPORTED."""
     from ccsc_code_iccv2017_amd import _lib as L
     from ccsc_code_iccv2017_amd import learners as E
-    b, d0, z0 = _case("dz", (6, 6), 3, 193, 2, 1, seed=4)
+    b, d0, z0 = _case("dz", (6, 6), 3, 401, 2, 1, seed=4)
     with pytest.raises(L.CCSCError) as ei:
-        E.admm_learn_conv2D_large_dzParallel(b, [3, 3, 193], 1.0, 1.0, 1, 0.0, "none",
+        E.admm_learn_conv2D_large_dzParallel(b, [3, 3, 401], 1.0, 1.0, 1, 0.0, "none",
                                              {"d": d0, "z": z0}, ni=1, ctx=gpu_ctx)
     assert ei.value.code == L.CCSC_E_UNSUPPORTED
 
