@@ -108,6 +108,9 @@ def cpu_baseline(args):
     }
 
 
+ZLINE_WAVES_PER_PATCH = 12
+
+
 def pmc_traffic(n_local):
     """HBM bytes per launch of the dominant z-step kernel from the committed rocprofv3
     PMC passes (FETCH_SIZE doubled for 16-B streaming loads on gfx950 and WRITE_SIZE,
@@ -130,7 +133,11 @@ def pmc_traffic(n_local):
     sq = sq_limits(k)
     if "FETCH_SIZE" not in k or "WRITE_SIZE" not in k:
         return None, os.path.relpath(PMC_SUMMARY, ROOT), name, stale, sq
-    per = (2.0 * k["FETCH_SIZE"] + k["WRITE_SIZE"]) * 1024.0 * n_local / d.get("n_local", n_local)
+    # patches per profiled dispatch: one 12-wave workgroup per patch (zline.hip), so a
+    # two-stream z-phase's half launches (rocprofv3 serialises them under --pmc) count as
+    # halves; without the SQ pass, the profile's whole patch count
+    disp = k["SQ_WAVES"] / ZLINE_WAVES_PER_PATCH if k.get("SQ_WAVES") else d.get("n_local", n_local)
+    per = (2.0 * k["FETCH_SIZE"] + k["WRITE_SIZE"]) * 1024.0 * n_local / disp
     return per, os.path.relpath(PMC_SUMMARY, ROOT), name, stale, sq
 
 
