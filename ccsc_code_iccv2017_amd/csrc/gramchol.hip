@@ -227,11 +227,14 @@ __global__ __launch_bounds__(kGcNT, GcShape<TM>::WGS) void k_gram_chol_mf(const 
     const int buf = c & 1;
     if (c + 1 < nch) fetch((c + 1) * kGcPC);
     const cpx<double>* a = sA + buf * kGcPC * kGcLD;
+    // k-steps past the last patch (the zero padding of a partial last chunk: ni = 100 is
+    // 6.25 chunks) are skipped -- adding their zero products changes nothing
+    const int kvalid = (ni - c * kGcPC + 3) >> 2;
 #pragma unroll
     for (int kk = 0; kk < kGcPC / 4; ++kk) {
       const cpx<double>* row = a + (4 * kk + (lane >> 4)) * kGcLD;
 #ifndef CCSC_ABL_NOGRAM
-      gram_kstep<TM>(row, wave, Tn, gr, gi);
+      if (kk < kvalid) gram_kstep<TM>(row, wave, Tn, gr, gi);
 #endif
     }
     const cpx<double>* b = sB + buf * kGcPC * NV;
@@ -240,8 +243,9 @@ __global__ __launch_bounds__(kGcNT, GcShape<TM>::WGS) void k_gram_chol_mf(const 
       const int q = tid + i * kGcNT;   // q = uv * K + k
       if (q < KV) {
         const int uv = q / K, k = q - uv * K;
+        const int pv = min(kGcPC, ni - c * kGcPC);
 #pragma unroll 4
-        for (int pp = 0; pp < kGcPC; ++pp)
+        for (int pp = 0; pp < pv; ++pp)
           hacc[i] = cadd(hacc[i], cmulc(a[pp * kGcLD + k], b[pp * NV + uv]));
       }
     }

@@ -86,7 +86,8 @@ typedef struct ccsc_problem {
   int32_t views[2];         /* 4D: U, V (angular views; kernel_size(3:4));
                                2-3D: W, 1 (wavelengths, kernel_size(3)); else 1,1      */
   int64_t n;                /* number of patches (size(b, end))                     */
-  int32_t K;                /* number of filters (kernel_size(end))                 */
+  int32_t K;                /* number of filters (kernel_size(end)); K <= 400 (2-3D:
+                               K <= 192), larger K returns CCSC_E_UNSUPPORTED         */
   int32_t psf;              /* psf_s = kernel_size(1), odd                          */
   double lambda_residual;   /* objective weight only (dP:21, Q-note)                */
   double lambda_prior;      /* lambda: soft threshold = lambda / theta_div          */
