@@ -86,6 +86,24 @@ def test_supported_reports_reasons(L):
     assert rc == L.CCSC_E_UNSUPPORTED and b"radix" in eb.value
 
 
+def test_filter_count_limits(L):
+    """K <= 192: the register-resident MFMA factor; 192 < K <= 400: gramchol_big.hip, whose
+    frequency-major code-spectra workspace (ni K F complex) joins the device plan; K > 400
+    and the 2-3D learner past K = 192 are CCSC_E_UNSUPPORTED with a reason."""
+    from ccsc_code_iccv2017_amd.learners import plan_bytes
+    eb = L.errbuf()
+    for K, ok in [(192, True), (193, True), (400, True), (401, False)]:
+        p = _problem(L, 1, n=200, K=K)
+        rc = L.lib().ccsc_supported(C.byref(p), eb, len(eb))
+        assert (rc == 0) == ok, (K, eb.value)
+        if not ok:
+            assert rc == L.CCSC_E_UNSUPPORTED and b"K > 400" in eb.value
+    # the big-K workspace: plan(193) - plan(192) exceeds the ni K F complex of X alone
+    F = 110 * 56
+    grow = plan_bytes(_problem(L, 1, n=200, K=193), 0, 1) - plan_bytes(_problem(L, 1, n=200, K=192), 0, 1)
+    assert grow > 100 * 193 * F * 16
+
+
 @pytest.mark.parametrize("nranks,expect", [(1, [100]), (2, [50, 50]), (4, [25] * 4),
                                            (8, [13, 13, 13, 13, 12, 12, 12, 12])])
 def test_block_sharding_is_contiguous(L, nranks, expect):
