@@ -1091,7 +1091,12 @@ struct Session2D {
     HIPCHK(hipEventRecord(e0, st));
 
     // ---- D precompute (dP:95-99) ----
-    const bool ovz = zmode == 2 && zhat_line && st3;
+    // A/B: CCSC_PRE_OVERLAP=0 runs every block's R2C on st, in series with the Gram
+    static const bool pre_overlap = [] {
+      const char* e = std::getenv("CCSC_PRE_OVERLAP");
+      return !(e && e[0] == '0');
+    }();
+    const bool ovz = zmode == 2 && zhat_line && st3 && pre_overlap;
     if (ovz) {   // st3's R2C passes read the state the z-phase left on st
       HIPCHK(hipEventRecord(ev_s, st));
       HIPCHK(hipStreamWaitEvent(st3, ev_s, 0));
