@@ -46,6 +46,9 @@ constexpr int kGcHPT = 8;                   // right-hand-side entries of h per 
 #ifndef CCSC_GC_RL
 #define CCSC_GC_RL 1
 #endif
+#ifndef CCSC_GC_NEWTON2   // A/B: a second Newton step on v_rsq_f64's 1/sqrt of the pivot
+#define CCSC_GC_NEWTON2 0
+#endif
 
 __device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
@@ -299,14 +302,17 @@ __global__ __launch_bounds__(kGcNT, GcShape<TM>::WGS) void k_gram_chol_mf(const 
       // right-looking in registers: once column c is final, every row r loses
       // L[r][c] conj(L[c2][c]) from its column c2 > c, L[c2][c] broadcast from lane c2 by
       // v_readlane -- no LDS round trip on the column-to-column chain; 1/sqrt of the
-      // pivot by v_rsq_f64 and two Newton steps instead of sqrt and a division
+      // pivot by v_rsq_f64 and one Newton step (error ~1.5 e0^2; a second one measured
+      // 1.4% of the kernel, CCSC_GC_NEWTON2) instead of sqrt and a division
 #pragma unroll
       for (int c = 0; c < 16; ++c) {
         const double a = rdl(x[c].x, c);
         double y = __builtin_amdgcn_rsq(a);
         const double hh = 0.5 * a;
         y = fma(y, fma(-hh * y, y, 0.5), y);
+#if CCSC_GC_NEWTON2
         y = fma(y, fma(-hh * y, y, 0.5), y);
+#endif
         x[c] = (lane == c) ? cpx<double>{a * y, 0.0} : cscale(x[c], y);
 #pragma unroll
         for (int c2 = c + 1; c2 < 16; ++c2) {
