@@ -180,7 +180,9 @@ def limiter(frac_dram, sq):
 
 def step_alg_bytes(n, K, ni, P, F, mid, miz, s=8, V=1):
     """algorithmic bytes of one outer iteration (precompute + max_it_d
-    d-iterations + max_it_z z-iterations), c = 2 s, N = n / ni blocks."""
+    d-iterations + max_it_z z-iterations), c = 2 s, N = n / ni blocks.  Its z-iteration
+    counts every stage's operands through HBM (prox, R2C, solve, C2R), which the fused
+    z-steps never move, so it is a staged model, not a floor."""
     c = 2 * s
     N = n // ni
     s_app = min(c * F * K * (K + 1) // 2, c * F * (ni * K + ni * (ni + 1) // 2))
@@ -188,6 +190,131 @@ def step_alg_bytes(n, K, ni, P, F, mid, miz, s=8, V=1):
     d_it = N * (4 * s * P * V * K + 5 * c * F * V * K + s_app)
     pre = N * (c * F * K * ni + c * F * V * ni + s_app + c * F * V * K)
     return pre + mid * d_it + miz * z_it
+
+
+def step_compulsory_bytes(n, K, ni, P, F, mid, miz, woodbury, V=1, four_d=False, s=8):
+    """Compulsory HBM bytes of one outer iteration of a consensus learner: every kernel
+    class reads its inputs once and writes its outputs once, with the z-iteration fused
+    (DESIGN.md §7):
+      z-iteration  the state a = z + y read and written once per (patch, filter) slice
+                   (2 s P), plus per patch the z-solve's own operands: w read + written and
+                   B^ read (3 c F; the closed form of dP:278-303), or for 4D the view
+                   correlation E per slice (c F, L4:310-347);
+      precompute   per block the R2C of the state into Z^ (ni K (s P + c F)), the Gram's
+                   reads of Z^ and B^ and its writes of the factor and h (dP:221-237);
+      d-iteration  per block §8(d)'s stages (dual update + R2C, d-solve over the factor,
+                   C2R): 4 s P V K + 5 c F V K + the factor.
+    The factor is K(K+1)/2 packed per f (Cholesky) or ni K + ni(ni+1)/2 (Woodbury)."""
+    c = 2 * s
+    N = n // ni
+    fac = c * F * (ni * K + ni * (ni + 1) // 2) if woodbury else c * F * (K * (K + 1) // 2)
+    pre = N * (ni * K * (s * P + c * F) + c * F * K * ni + c * F * V * ni + fac + c * F * V * K)
+    d_it = N * (4 * s * P * V * K + 5 * c * F * V * K + fac)
+    z_it = n * K * 2 * s * P + (n * K * c * F if four_d else 3 * n * c * F)
+    return pre + mid * d_it + miz * z_it
+
+
+def hs23_compulsory_bytes(n, K, W, P, F, mid, miz, s=8):
+    """Compulsory bytes of one outer iteration of the 2-3D learner (L23:86-226, C3): the
+    precompute fft2(z) + Gram (L23:100, 289-295), then per inner iteration (each of the
+    max_it_d D- and max_it_z Z-iterations, objective included: L23:132,195) the synthesis
+    sum_k d^_k z^_k (reads z^ and d^), the masked data prox/dual on the W-channel side
+    (its spectrum in, d{1} and M.*b read, d{1} written, xi1 out: 2 c F + 3 s P per
+    channel), the variable's prox/dual (3 s P + c F per variable slice), the solve's
+    right-hand side reads, its output spectrum and the C2R of the variable (c F + s P),
+    and the objective's synthesis (z^, d^ again)."""
+    c = 2 * s
+    Kp = K * (K + 1) // 2
+    pre = n * K * (s * P + c * F) + n * K * c * F + c * F * Kp
+    synth = n * K * c * F + W * K * c * F
+    data = n * W * (2 * c * F + 3 * s * P)
+    d_it = (synth + data + W * K * (3 * s * P + c * F) + n * K * c * F + n * W * c * F
+            + c * F * Kp + W * K * (2 * c * F + s * P) + synth)
+    z_it = (synth + data + n * K * (3 * s * P + c * F) + n * W * c * F
+            + n * K * (2 * c * F + s * P) + synth)
+    return pre + mid * d_it + miz * z_it
+
+
+# the other BASELINE.json configs (C2 is the headline workload above): name, variant, b
+# shape, kernel size, lambda, synthetic data kind (SURVEY.md §8d sizes; C4/C5 take n = 64)
+CONFIGS = [
+    ("C1", "2D dParallel, K=100 11x11, n=1000 100x100 patches, 10 blocks", "DPAR",
+     (100, 100, 1000), [11, 11, 100], 1.0, "normal"),
+    ("C3", "2-3D hyperspectral (admm_learn), K=100 11x11x31, n=64 100x100x31 cubes", "HS23",
+     (100, 100, 31, 64), [11, 11, 31, 100], 1.0, "uniform"),
+    ("C4", "3D video, K=49 11x11x11, n=64 64x64x32 clips (ni=8, Woodbury)", "L3D",
+     (64, 64, 32, 64), [11, 11, 11, 49], 0.1, "normal"),
+    ("C5", "4D light field, K=49 11x11x5x5, n=64 64x64 5x5-view patches (ni=8)", "L4D",
+     (64, 64, 5, 5, 64), [11, 11, 5, 5, 49], 1.0, "normal"),
+]
+
+
+def config_bytes(p, b_shape, ks):
+    """(§8(d) bytes, compulsory bytes) of one outer iteration of a resolved problem."""
+    from ccsc_code_iccv2017_amd import _lib as L
+    r = ks[0] // 2
+    X, Y = b_shape[0] + 2 * r, b_shape[1] + 2 * r
+    Xh = X // 2 + 1
+    n, K, mid, miz = p.n, p.K, p.max_it_d, p.max_it_z
+    if p.variant == L.CCSC_HS23:
+        W = b_shape[2]
+        return None, hs23_compulsory_bytes(n, K, W, X * Y, Xh * Y, mid, miz)
+    T = b_shape[2] + 2 * r if p.variant == L.CCSC_L3D else 1
+    V = p.views[0] * p.views[1]
+    P, F = X * Y * T, Xh * Y * T
+    wb = p.dfactor == L.DFACTOR["woodbury"]
+    return (step_alg_bytes(n, K, p.ni, P, F, mid, miz, V=V),
+            step_compulsory_bytes(n, K, p.ni, P, F, mid, miz, wb, V=V,
+                                  four_d=p.variant == L.CCSC_L4D))
+
+
+def run_config(ctx, key, label, variant, b_shape, ks, lam, kind, steps=1):
+    """One untimed warm-up outer iteration, then `steps` timed ones (objective excluded
+    where the learner allows it; C3 evaluates it every inner iteration, as the
+    reference's rollback test needs), synchronised through the session's own sync."""
+    from ccsc_code_iccv2017_amd import learners as E
+    from ccsc_code_iccv2017_amd import _lib as L
+    rng = np.random.default_rng(7)
+    b = rng.random(b_shape) if kind == "uniform" else rng.standard_normal(b_shape)
+    var = getattr(L, "CCSC_" + variant)
+    p = E.make_problem(var, b_shape, ks, 1.0, lam, steps + 1, 0.0, "none", seed=11)
+    sm = 0.5 * rng.random(b_shape) if variant == "HS23" else None
+    s = E.Session(ctx, p, b, smooth_init=sm)
+    try:
+        s.step(1)
+        t0 = time.perf_counter()
+        s.step(steps)
+        dt = (time.perf_counter() - t0) / steps
+        q = s.p
+    finally:
+        s.close()
+    n = b_shape[-1]
+    s8d, comp = config_bytes(q, b_shape, ks)
+    return {
+        "workload": label,
+        "s_per_outer_iteration": dt,
+        "patch_iters_per_s": n / dt,
+        "s8d_bytes": s8d,
+        "frac_s8d": s8d / dt / 1e9 / HBM_PEAK_GBS if s8d else None,
+        "compulsory_bytes": comp,
+        "frac_compulsory": comp / dt / 1e9 / HBM_PEAK_GBS,
+        "max_it_d": q.max_it_d, "max_it_z": q.max_it_z, "ni": q.ni,
+        "dfactor": "woodbury" if q.dfactor == L.DFACTOR["woodbury"] else "cholesky",
+    }
+
+
+def configs_leg(local):
+    """Every other BASELINE.json config on this GPU (rank 0, N = 1): seconds per outer
+    iteration, patch-iters/s and the step-level byte fractions."""
+    from ccsc_code_iccv2017_amd import learners as E
+    out = {}
+    with E.Context(local) as ctx:
+        for key, label, variant, shape, ks, lam, kind in CONFIGS:
+            t0 = time.perf_counter()
+            out[key] = run_config(ctx, key, label, variant, shape, ks, lam, kind)
+            log(f"config {key}: {out[key]['s_per_outer_iteration']:.4f} s per outer iteration "
+                f"({time.perf_counter() - t0:.1f} s with setup)")
+    return out
 
 
 def main():
@@ -201,6 +328,8 @@ def main():
                     help="inner/outer tol (the reference driver's 1e-3, learn_kernels_2D_large.m:24;"
                          " the metric is defined at tol = 0: fixed inner counts)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-configs", action="store_true",
+                    help="skip the C1/C3/C4/C5 timings (one warm-up + one timed outer iteration each)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -268,7 +397,7 @@ def main():
         dt = float(t.item())
 
     comm_ranks, transport = ctx.comm_ranks()
-    launches, zms, zbytes = sess.kernel_stats(0)
+    launches, zms, _ = sess.kernel_stats(0)
     kstats = {}
     for kid, name in enumerate(["zstep", "gram_chol", "dsolve", "dual_r2c", "c2r_dout"]):
         n_, ms_, by_ = sess.kernel_stats(kid)
@@ -300,7 +429,7 @@ def main():
     compulsory = n_local * (K * 2 * 8 * Pg + 3 * 16 * Fg)
     achieved = compulsory / t_launch / 1e9 if launches else 0.0
     frac_dram = traffic / t_launch / 1e9 / HBM_PEAK_GBS if (traffic and launches) else None
-    step_bytes = step_alg_bytes(args.n, K, ni, Pg, Fg, p.max_it_d, p.max_it_z)
+    step_comp = step_compulsory_bytes(args.n, K, ni, Pg, Fg, p.max_it_d, p.max_it_z, False)
     step_s = dt / max(done_steps, 1)
     result = {
         "objective_start": obj_start,
@@ -345,22 +474,26 @@ def main():
             "avg_launch_ms": avg_ms,
             "frac_dram": frac_dram,
             "sq": sq,
-            # SURVEY.md §8(d)'s staged z-iteration model (n K (4sP + 4cF) + n c F): it
-            # counts every stage's operands through HBM, which the fused kernel never
-            # moves, so its fraction exceeds 1 -- kept for continuity, not the roofline
-            "s8d_bytes_per_launch": zbytes,
-            "frac_s8d": zbytes / t_launch / 1e9 / HBM_PEAK_GBS if launches else None,
-            # whole outer iteration: §8(d) bytes of every stage / step time / node peak
-            "step_alg_bytes": step_bytes,
-            "step_frac_s8d": step_bytes / step_s / 1e9 / (HBM_PEAK_GBS * world),
+            # whole outer iteration: every kernel class's compulsory bytes (its inputs read
+            # once, its outputs written once; step_compulsory_bytes) / step time / node peak
+            "step_compulsory_bytes": step_comp,
+            "step_frac": step_comp / step_s / 1e9 / (HBM_PEAK_GBS * world),
         },
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    result["configs"] = None
+    result["cpu_baseline"] = None
+    if rank == 0 and world == 1:
         sess.close()
         ctx.close()
-        result["cpu_baseline"] = cpu_baseline(args)
-    else:
-        result["cpu_baseline"] = None
+        if not args.no_configs:
+            result["configs"] = configs_leg(local)
+        if not args.no_cpu_baseline:
+            cb = cpu_baseline(args)
+            if result["configs"]:   # the GPU on the same config (C1) beside the CPU number
+                g1 = result["configs"]["C1"]["patch_iters_per_s"]
+                cb["gpu_same_config"] = {"config": "C1", "value": g1, "unit": "patch-iters/s",
+                                         "gpu_over_cpu": g1 / cb["value"]}
+            result["cpu_baseline"] = cb
     if rank == 0:
         print(json.dumps(result), flush=True)
     sess.close()

@@ -22,7 +22,7 @@ CCSC_E_STATE = -6
 CCSC_DPAR, CCSC_DZPAR, CCSC_L3D, CCSC_L4D, CCSC_HS23 = 0, 1, 2, 3, 4
 ABI_VERSION = 6
 VERBOSE = {"none": 0, "brief": 1, "all": 2}
-CCSC_FP64, CCSC_FP32 = 0, 1
+CCSC_FP64 = 0
 DFACTOR = {"auto": 0, "cholesky": 1, "woodbury": 2}
 TRANSPORT = {0: "none", 1: "rccl", 2: "host"}
 

@@ -33,10 +33,7 @@ __host__ __device__ __forceinline__ T cabs2(cpx<T> a) { return a.x * a.x + a.y *
 // Block size of every slice-resident kernel: 16 waves of 64 lanes (one
 // workgroup per CU holds a whole fp64 slice in LDS, so the waves of that one
 // workgroup are all the latency hiding the CU gets).
-#ifndef CCSC_NT
-#define CCSC_NT 1024
-#endif
-constexpr int kNT = CCSC_NT;
+constexpr int kNT = 1024;
 // Butterflies per FFT pass that the threads hold in registers at once (the
 // in-place pass needs every butterfly of the pass live between its read and
 // write barriers); MAXB = kMaxButterflies / kNT per thread.

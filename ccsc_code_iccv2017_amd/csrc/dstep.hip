@@ -32,14 +32,8 @@ __device__ __forceinline__ int pk_off(int j, int K) { return j * K - (j * (j - 1
 // form spent its time in LDS latency chains (measured 2.9 of 4.2 ms per block
 // launch at K = 100).
 // ---------------------------------------------------------------------------
-#ifndef CCSC_CHOL_NB
-#define CCSC_CHOL_NB 8
-#endif
-#ifndef CCSC_CHOL_T
-#define CCSC_CHOL_T 2
-#endif
-constexpr int kCholNB = CCSC_CHOL_NB;
-constexpr int kCholT = CCSC_CHOL_T;
+constexpr int kCholNB = 8;
+constexpr int kCholT = 2;
 
 // broadcast of lane `l` (wave-uniform) through v_readlane: a scalar-register
 // hop of a few cycles, where a shuffle is an LDS-crossbar round trip
@@ -218,9 +212,6 @@ __global__ __launch_bounds__(kGramNT) void k_gram_chol(const cpx<T>* __restrict_
   for (int i = 0; i < kGramHPT; ++i) hacc[i] = {(T)0, (T)0};
   const int KV = K * NV;
 
-#ifdef CCSC_ABL_NOGRAM
-  ni = 0;  // ablation build: skip the Gram accumulation (timing only)
-#endif
   for (int p0 = 0; p0 < ni; p0 += kGramPC) {
     const int pc = min(kGramPC, ni - p0);
     __syncthreads();
@@ -281,9 +272,7 @@ __global__ __launch_bounds__(kGramNT) void k_gram_chol(const cpx<T>* __restrict_
   }
   __syncthreads();
 
-#ifndef CCSC_ABL_NOCHOL
   chol_blocked(sG, K);
-#endif
   cpx<T>* Lf = L + (int64_t)f * Kp;
   for (int q = tid; q < Kp; q += kGramNT) Lf[q] = sG[q];
 }
@@ -322,17 +311,7 @@ __device__ __forceinline__ cpx<T> shfl_c(cpx<T> v, int src) {
 // instead of NV times.  The factor's columns are read in blocks of kDsJB per
 // wave (one load batch per block, address-independent of the solve) so their
 // latency is paid once per block instead of once per column.
-#ifndef CCSC_DS_JB
-#define CCSC_DS_JB 6
-#endif
-constexpr int kDsJB = CCSC_DS_JB;
-#ifndef CCSC_DS_BWRED
-#define CCSC_DS_BWRED 0
-#endif
-constexpr bool kDsBwRed = CCSC_DS_BWRED;
-#ifndef CCSC_DS_NV8
-#define CCSC_DS_NV8 1   // A/B: 8 right-hand sides per factor sweep when NV > 4 (K <= 128)
-#endif   // A/B: reduction backward for every NVB
+constexpr int kDsJB = 6;
 
 // x[u] for a wave-uniform u < RPL (unrolled selects: no runtime register indexing)
 template <typename T, int RPL>
@@ -428,7 +407,7 @@ __global__ __launch_bounds__(256) void k_dsolve(const cpx<T>* __restrict__ L,
   // reductions dominate and the column-axpy form below is faster; with one the
   // latter's per-lane column walk (64 lines per load) costs more than the
   // reductions (C2: 22 vs 42 ms per launch, with shuffle reductions).
-  if constexpr (NVB == 1 || kDsBwRed) {
+  if constexpr (NVB == 1) {
   for (int j1 = K - 1; j1 >= 0; j1 -= kDsJB) {
     cpx<T> lc[kDsJB][RPL];
     T dg[kDsJB];
@@ -508,22 +487,10 @@ __global__ __launch_bounds__(256) void k_dsolve(const cpx<T>* __restrict__ L,
   }  // view groups
 }
 
-// A/B knob: CCSC_DS_LDS_KB reserves that much (unused) LDS per workgroup, capping the
-// workgroups per CU and so the factor bytes in flight between a (block, f)'s forward
-// and backward sweep (the reuse distance of the second read of L).
-static size_t dsolve_lds_bytes() {
-  static const size_t v = [] {
-    const char* e = std::getenv("CCSC_DS_LDS_KB");
-    const int kb = e ? std::atoi(e) : 0;
-    return (size_t)std::min(std::max(kb, 0), 160) * 1024;
-  }();
-  return v;
-}
-
 template <typename T, int RPL, int NVB>
 static void dsolve_go(dim3 grid, hipStream_t st, const cpx<T>* L, const cpx<T>* h,
                       const cpx<T>* Ch, cpx<T>* Dh, int F, int K, T rho, int fgroups, int NV) {
-  hipLaunchKernelGGL((k_dsolve<T, RPL, NVB>), grid, dim3(256), dsolve_lds_bytes(), st, L, h, Ch,
+  hipLaunchKernelGGL((k_dsolve<T, RPL, NVB>), grid, dim3(256), 0, st, L, h, Ch,
                      Dh, F, K, rho, fgroups, NV);
 }
 
@@ -540,7 +507,7 @@ hipError_t launch_dsolve(const cpx<T>* L, const cpx<T>* h, const cpx<T>* Ch, cpx
   } else if (K <= 128) {
     // many right-hand sides (L23's W = 31 wavelengths): 8 per sweep over the factor
     if (NV == 1) dsolve_go<T, 2, 1>(grid, st, L, h, Ch, Dh, F, K, rho, fgroups, NV);
-    else if (NV <= 4 || !CCSC_DS_NV8) dsolve_go<T, 2, 4>(grid, st, L, h, Ch, Dh, F, K, rho, fgroups, NV);
+    else if (NV <= 4) dsolve_go<T, 2, 4>(grid, st, L, h, Ch, Dh, F, K, rho, fgroups, NV);
     else dsolve_go<T, 2, 8>(grid, st, L, h, Ch, Dh, F, K, rho, fgroups, NV);
   } else if (K <= 192) {
     if (NV == 1) dsolve_go<T, 3, 1>(grid, st, L, h, Ch, Dh, F, K, rho, fgroups, NV);

@@ -50,11 +50,6 @@ static int64_t generic_tasks(int n, int nlines, int p) {
   return (int64_t)nlines * (n / p) * (((p - 1) / 2 + kGenericQP - 1) / kGenericQP);
 }
 
-static bool pfa_disabled() {   // CCSC_FFT_PFA=0: the generic pass (A/B)
-  const char* e = std::getenv("CCSC_FFT_PFA");
-  return e && e[0] == '0';
-}
-
 static bool plan1d(int n, int nlines, Plan1D& out) {
   Plan1D best{};
   best.npass = 99;
@@ -106,7 +101,7 @@ static bool plan1d(int n, int nlines, Plan1D& out) {
       best.rad[rest.npass] = p;
       // 2 * kPfaM: the prime-factor pass with immediate roots (fft_pass_pfa)
       best.pfa = (n == 2 * kPfaM && p == kPfaM && best.npass == 2 &&
-                  pfa_slots(nlines, kPfaM, kPfaQP) <= kNT && !pfa_disabled());
+                  pfa_slots(nlines, kPfaM, kPfaQP) <= kNT);
       break;
     }
   }
@@ -276,7 +271,7 @@ static void resolve_problem(ccsc_problem& p) {
                                   std::to_string(p.ni) + "); the reference floors n/ni silently (Q13)");
   if (p.verbose < CCSC_VERBOSE_NONE || p.verbose > CCSC_VERBOSE_ALL)
     throw Err(CCSC_E_INVALID, "bad verbose");
-  if (p.precision != CCSC_FP64 && p.precision != CCSC_FP32) throw Err(CCSC_E_INVALID, "bad precision");
+  if (p.precision != CCSC_FP64) throw Err(CCSC_E_INVALID, "precision must be CCSC_FP64 (double, as the reference)");
   if (p.dfactor < CCSC_DFACTOR_AUTO || p.dfactor > CCSC_DFACTOR_WOODBURY)
     throw Err(CCSC_E_INVALID, "bad dfactor");
   // AUTO resolves to the form the consensus learners will run (observable through
@@ -304,7 +299,6 @@ static void check_supported(const ccsc_problem& p, Geom* Gout) {
   // (the 2-3D learner forms its right-hand sides with the per-bin GEMM, not in the gram kernel)
   if (p.variant != CCSC_HS23 && (int64_t)p.K * p.views[0] * p.views[1] > 2048)
     throw Err(CCSC_E_UNSUPPORTED, "K * views > 2048 exceeds the gram kernel's RHS budget");
-  if (p.precision != CCSC_FP64) throw Err(CCSC_E_UNSUPPORTED, "only CCSC_FP64 is built");
   // K <= 192: the register-resident MFMA factor (gramchol.hip); 192 < K <= 400: the
   // HBM-resident Gram + left-looking Cholesky of gramchol_big.hip (consensus learners)
   if (p.K > 400) throw Err(CCSC_E_UNSUPPORTED, "K > 400 exceeds the d-solve's rows per lane");
@@ -342,11 +336,8 @@ using namespace ccsc;
 
 namespace ccsc {
 
-// the register-line z-step serves the 110 grid (A/B switch: CCSC_ZLINE=0 keeps k_zsplit)
-static bool zline_usable(const Grid2D& G) {
-  const char* ev = std::getenv("CCSC_ZLINE");
-  return zline_grid(G) && !(ev && ev[0] == '0');
-}
+// the register-line z-step serves the 110 grid (k_zsplit every other 2D grid)
+static bool zline_usable(const Grid2D& G) { return zline_grid(G); }
 
 // memory plan shared by ccsc_plan_bytes and the session
 struct Plan2D {
@@ -409,6 +400,44 @@ static Plan2D plan2d(const ccsc_problem& p, const Geom& g, int rank, int nranks)
 
 static const char* kKernelNames[5] = {"zstep", "gram_chol", "dsolve", "dual_r2c", "c2r_dout"};
 
+// Wait for a non-blocking communicator's pending call (ncclInProgress); with `abort`,
+// give up as soon as the group aborted (the enqueue may be waiting on a failed rank).
+static void wait_comm(ncclComm_t c, const std::atomic<bool>* abort) {
+  ncclResult_t st = ncclInProgress;
+  for (;;) {
+    NCCLCHK(ncclCommGetAsyncError(c, &st));
+    if (st != ncclInProgress) break;
+    if (abort && abort->load())
+      throw Err(CCSC_E_RCCL, "host communicator aborted: another rank of this context failed");
+    std::this_thread::yield();
+  }
+  if (st != ncclSuccess)
+    throw Err(CCSC_E_RCCL, std::string("RCCL communicator error: ") + ncclGetErrorString(st));
+}
+
+// The communicators of a device-list context (rank i on devices[i]), created
+// non-blocking so that no collective call can stall inside RCCL: abort_group relies on
+// it to abort them only while no rank is inside a call.
+static void init_group_comms(std::vector<ncclComm_t>& comms, const int32_t* devices, int nd) {
+  ncclUniqueId id;
+  NCCLCHK(ncclGetUniqueId(&id));
+  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+  cfg.blocking = 0;
+  auto ok = [](ncclResult_t r) { return r == ncclSuccess || r == ncclInProgress; };
+  if (!ok(ncclGroupStart())) throw Err(CCSC_E_RCCL, "ncclGroupStart failed");
+  for (int i = 0; i < nd; ++i) {
+    HIPCHK(hipSetDevice(devices[i]));
+    const ncclResult_t r = ncclCommInitRankConfig(&comms[i], nd, id, i, &cfg);
+    if (!ok(r)) {
+      ncclGroupEnd();
+      throw Err(CCSC_E_RCCL, std::string("ncclCommInitRankConfig failed: ") + ncclGetErrorString(r));
+    }
+  }
+  const ncclResult_t r = ncclGroupEnd();
+  if (!ok(r)) throw Err(CCSC_E_RCCL, std::string("ncclGroupEnd failed: ") + ncclGetErrorString(r));
+  for (int i = 0; i < nd; ++i) wait_comm(comms[i], nullptr);
+}
+
 // ---------------------------------------------------------------------------
 // Session: 2D consensus learners (dP / dZ)
 // ---------------------------------------------------------------------------
@@ -427,7 +456,7 @@ struct Session2D {
   int NV, KG;   // views, filter slices per block (K * NV)
   bool is4, is3;
   bool woodbury;   // D-factor in Woodbury form (p.dfactor; AUTO: woodbury_fits, ni << K)
-  bool gram_mf;    // Gram + Cholesky on the matrix cores (gramchol.hip; CCSC_GRAM_MF=0: VALU form)
+  bool gram_mf;    // Gram + Cholesky on the matrix cores (gramchol.hip; else the VALU form)
   bool dtile = false;   // tile d-solve on a factor with inverted diagonal tiles (dstep.hip)
   bool gram_big = false;   // K > 192: HBM-resident Gram + Cholesky (gramchol_big.hip), X its workspace
   DevBuf Xbig;
@@ -464,7 +493,6 @@ struct Session2D {
   // in state order, W the last w in bin-slot order solved with dws (dhs or dhws);
   // Bhs / dhs / sdens: B^, the current filter spectrum and sden in bin-slot order.
   bool zl_on = false;
-  bool zhat_line = true;   // D-precompute spectra on the lanes (CCSC_ZHAT_LINE=0: k_zhat_split)
   DevBuf Bhs, dhs, dhws, sdens;
   const cpx<double>* dws = nullptr;
   // tol > 0 with the register-line z-step: what `yz` holds (state order) while the
@@ -478,7 +506,7 @@ struct Session2D {
   Grid2D gt2{};            //     its t plan (K * tsolve_tc lines) and twiddles
   DevBuf twt2;
   DevBuf BhatT, dhatT, sdenT;   // B^, the filter spectrum, sden in k_tsolve3's tile order
-  int tsolve_ppw = 16;          // patches per k_tsolve3 workgroup (CCSC_TSOLVE3_PPW)
+  int tsolve_ppw = 16;          // patches per k_tsolve3 workgroup
 
   // host-side log
   int outer_done = 0;
@@ -588,8 +616,7 @@ struct Session2D {
     NV = p.views[0] * p.views[1];
     KG = K * NV;
     {
-      const char* ev = std::getenv("CCSC_GRAM_MF");
-      gram_mf = gram_chol_mf_ok(K, NV) && !(ev && ev[0] == '0');
+      gram_mf = gram_chol_mf_ok(K, NV);
       gram_big = !woodbury && K > 192 && gram_big_ok(K, NV);
       // tile d-solve (one read of the factor per solve) on the MFMA factor with inverted
       // diagonal tiles; CCSC_DS_TILE=0 keeps the two-sweep k_dsolve
@@ -628,14 +655,11 @@ struct Session2D {
       odz.alloc((size_t)P * 8);
       // fused t-FFT + z-solve (k_tsolve3): TC x' columns per workgroup; C4 (74x74x42,
       // K = 49) measured 0.432 s per outer iteration at TC = 2, 0.456 at TC = 4 and with
-      // the three-kernel form (CCSC_TSOLVE3=0), 0.587 at TC = 1
-      const char* ev = std::getenv("CCSC_TSOLVE3");
-      const char* etc = std::getenv("CCSC_TSOLVE3_TC");
-      if (const char* ep = std::getenv("CCSC_TSOLVE3_PPW")) tsolve_ppw = std::max(1, std::atoi(ep));
-      if (!(ev && ev[0] == '0')) {
+      // the three-kernel form, 0.587 at TC = 1; the three-kernel form serves what k_tsolve3
+      // cannot hold
+      {
         std::string why2;
         for (int tc : {2, 4, 1}) {
-          if (etc && std::atoi(etc) > 0 && tc != std::atoi(etc)) continue;
           Grid2D Gt2{};
           if (!tsolve3_ok(Tn, K, tc) || !make_gridt(Tn, K * tc, Gt2, why2)) continue;
           if (tsolve3_smem_bytes(Gt2, K, tc, sizeof(double)) > 160 * 1024) continue;
@@ -657,10 +681,6 @@ struct Session2D {
     if (m.W) W.alloc(m.W);
     if (m.dhw) dhatw.alloc(m.dhw);
     zl_on = m.zl != 0;
-    {
-      const char* ev = std::getenv("CCSC_ZHAT_LINE");
-      zhat_line = !(ev && ev[0] == '0');
-    }
     if (zl_on) {
       Zh2.alloc(m.Zh);
       HIPCHK(hipStreamCreateWithFlags(&st3, hipStreamNonBlocking));
@@ -776,16 +796,22 @@ struct Session2D {
     if (g && g->aborted.load())
       throw Err(CCSC_E_RCCL, "host communicator aborted: another rank of this context failed");
     if (!ctx->comm) throw Err(CCSC_E_STATE, "multi-rank context without a communicator");
-    rccl();
+    const ncclResult_t r = rccl();
+    // a device-list group's communicators are non-blocking (init_group_comms): the enqueue
+    // may still be connecting; wait for it here, giving up once the group aborted, so no
+    // rank stays inside RCCL on a communicator abort_group is about to abort
+    if (r == ncclInProgress) wait_comm(ctx->comm, g ? &g->aborted : nullptr);
+    else if (r != ncclSuccess)
+      throw Err(CCSC_E_RCCL, std::string("RCCL collective failed: ") + ncclGetErrorString(r));
   }
   void allreduce(double* buf, size_t count) {
     collective(CCSC_COMM_ALLREDUCE_SUM, buf, count, [&] {
-      NCCLCHK(ncclAllReduce(buf, buf, count, ncclDouble, ncclSum, ctx->comm, st));
+      return ncclAllReduce(buf, buf, count, ncclDouble, ncclSum, ctx->comm, st);
     });
   }
   void bcast0(double* buf, size_t count) {
     collective(CCSC_COMM_BCAST0, buf, count, [&] {
-      NCCLCHK(ncclBroadcast(buf, buf, count, ncclDouble, 0, ctx->comm, st));
+      return ncclBroadcast(buf, buf, count, ncclDouble, 0, ctx->comm, st);
     });
   }
   void pair_to_host(double* out2) {
@@ -1091,12 +1117,9 @@ struct Session2D {
     HIPCHK(hipEventRecord(e0, st));
 
     // ---- D precompute (dP:95-99) ----
-    // A/B: CCSC_PRE_OVERLAP=0 runs every block's R2C on st, in series with the Gram
-    static const bool pre_overlap = [] {
-      const char* e = std::getenv("CCSC_PRE_OVERLAP");
-      return !(e && e[0] == '0');
-    }();
-    const bool ovz = zmode == 2 && zhat_line && st3 && pre_overlap;
+    // 110 grid: block j+1's R2C on st3 beside block j's Gram on st (same-box A/B at
+    // 8ff8b2a: 949 vs 957.7 ms per C2 step in series, profiles/r03j/preov_ab.txt)
+    const bool ovz = zmode == 2 && st3;
     if (ovz) {   // st3's R2C passes read the state the z-phase left on st
       HIPCHK(hipEventRecord(ev_s, st));
       HIPCHK(hipStreamWaitEvent(st3, ev_s, 0));
@@ -1110,7 +1133,7 @@ struct Session2D {
                                         K, theta, st3));
         HIPCHK(hipEventRecord(ev_z, st3));
         HIPCHK(hipStreamWaitEvent(st, ev_z, 0));
-      } else if (zmode == 2 && zhat_line)
+      } else if (zmode == 2)
         HIPCHK(launch_zhat_line<double>(z.as<double>() + (size_t)jl * ni * K * P,
                                         W.as<cpx<double>>() + (size_t)jl * ni * F, dws,
                                         Zh.as<cpx<double>>(), ni, K, theta, st));
@@ -1627,13 +1650,9 @@ struct SessionHS {
     // z_hat = fft2(z) (L23:100) and v_D{1} = H z of the first d-iteration (L23:108)
     objective_fresh();
     // opt_f = (Z_f' Z_f + rho I)^-1 as a Cholesky factor per bin (L23:290)
-    if (K > 128)   // beyond the LDS-resident VALU factor: the matrix-core kernel (no RHS here)
-      HIPCHK(launch_gram_chol_mf(Zh.as<cpx<double>>(), Zh.as<cpx<double>>(), L.as<cpx<double>>(),
-                                 h.as<cpx<double>>(), F, K, n, p.rho_d, 0, st));
-    else
-      HIPCHK(launch_gram_chol<double>(Zh.as<cpx<double>>(), Zh.as<cpx<double>>(),
-                                      L.as<cpx<double>>(), h.as<cpx<double>>(), F, K, n, p.rho_d,
-                                      0, st));
+    // on the matrix cores (gramchol.hip, K <= 192; no right-hand side here: NV = 0)
+    HIPCHK(launch_gram_chol_mf(Zh.as<cpx<double>>(), Zh.as<cpx<double>>(), L.as<cpx<double>>(),
+                               h.as<cpx<double>>(), F, K, n, p.rho_d, 0, st));
     for (int id = 0; id < p.max_it_d; ++id) {                                    // L23:102
       // c = 1: masked data split (L23:112, 117, 120-121)
       HIPCHK(launch_hs_data_r2c<double>(v.as<double>(), eD.as<double>(), bdev.as<double>(),
@@ -1787,16 +1806,19 @@ struct ccsc_session {
 
 namespace ccsc {
 // One rank of a multi-device context failed: mark the group aborted (once, whichever
-// threads fail), wake the in-process exchange, let collectives already past their
-// abort check finish enqueueing, then abort every RCCL communicator so the other
-// ranks' collectives waiting on the failed rank return (see CommGroup).
+// threads fail), wake the in-process exchange, wait until no rank is inside a collective
+// call, then abort every RCCL communicator so the other ranks' kernels waiting on the
+// failed rank return (see CommGroup).  The wait has no time limit and needs none: the
+// group's communicators are non-blocking (init_group_comms), so an enqueue returns at
+// once and collective()'s poll loop leaves as soon as `aborted` is set -- a communicator
+// is never aborted (freed) while another thread is inside RCCL with it, and a rank that
+// enters collective() later sees `aborted` (set before the wait) before it reads `comm`.
 static void abort_group(ccsc_ctx* ctx) {
   CommGroup* g = ctx->grp.get();
   std::lock_guard<std::mutex> lk(g->mu);
   if (g->aborted.exchange(true)) return;
   if (ctx->hg) ctx->hg->abort();
-  for (int i = 0; i < 2000 && g->inflight.load() > 0; ++i)
-    std::this_thread::sleep_for(std::chrono::microseconds(50));
+  while (g->inflight.load() > 0) std::this_thread::sleep_for(std::chrono::microseconds(50));
   for (ccsc_ctx* u : ctx->subs)
     if (u->comm) {
       ncclCommAbort(u->comm);
@@ -1817,7 +1839,7 @@ static void reset_group(ccsc_ctx* ctx) {
     for (int i = 0; i < nd; ++i) ctx->hg_ranks[i] = HostGroupRank{ctx->hg.get(), i};
   } else {
     std::vector<ncclComm_t> comms(nd, nullptr);
-    NCCLCHK(ncclCommInitAll(comms.data(), nd, ctx->devices.data()));
+    init_group_comms(comms, ctx->devices.data(), nd);
     for (int i = 0; i < nd; ++i) ctx->subs[i]->comm = comms[i];
     HIPCHK(hipSetDevice(ctx->device));
   }
@@ -2078,7 +2100,7 @@ ccsc_ctx* ccsc_create_multi(const int32_t* devices, int32_t ndev, char* err, siz
       }
       if (distinct) {
         std::vector<ncclComm_t> comms(ndev, nullptr);
-        NCCLCHK(ncclCommInitAll(comms.data(), ndev, devices));
+        init_group_comms(comms, devices, ndev);
         for (int i = 0; i < ndev; ++i) c->subs[i]->comm = comms[i];
       }
       for (int i = 0; i < ndev; ++i) {

@@ -22,10 +22,6 @@
 
 #include "common.hpp"
 
-// DFT of size 2 M (M odd) as a prime-factor split (dft_sink); -DCCSC_DFT_PFA=0 for A/B
-#ifndef CCSC_DFT_PFA
-#define CCSC_DFT_PFA 1
-#endif
 
 #include <utility>
 
@@ -127,7 +123,6 @@ __device__ __forceinline__ void dft_sink(cpx<T> (&v)[R], Sink&& sink) {
     sink(2, csub(a0, b0));
     sink(1, cadd(a1, b1i));
     sink(3, csub(a1, b1i));
-#if CCSC_DFT_PFA
   } else if constexpr (R % 4 == 2 && R > 2) {
     // R = 2 M, M odd: prime-factor (Good-Thomas) split, no twiddles -- input
     // n = (M n1 + 2 n2) mod R, output k = (M k1 + (M + 1) k2) mod R; M two-point
@@ -142,7 +137,6 @@ __device__ __forceinline__ void dft_sink(cpx<T> (&v)[R], Sink&& sink) {
     });
     dft_sink<T, M, SIGN>(e, [&](int k2, cpx<T> val) { sink(((M + 1) * k2) % R, val); });
     dft_sink<T, M, SIGN>(o, [&](int k2, cpx<T> val) { sink((M + (M + 1) * k2) % R, val); });
-#endif
   } else {
     constexpr int H = (R - 1) / 2;
     constexpr bool EVEN = (R % 2) == 0;

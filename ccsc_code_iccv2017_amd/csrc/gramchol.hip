@@ -43,12 +43,6 @@ constexpr int kGcPC = 16;                   // patches per staged chunk
 constexpr int kGcTS = 17;                   // column stride (complex) of an LDS tile
 constexpr int kGcTSZ = 16 * kGcTS;          // complex per LDS tile
 constexpr int kGcHPT = 8;                   // right-hand-side entries of h per thread
-#ifndef CCSC_GC_RL
-#define CCSC_GC_RL 1
-#endif
-#ifndef CCSC_GC_NEWTON2   // A/B: a second Newton step on v_rsq_f64's 1/sqrt of the pivot
-#define CCSC_GC_NEWTON2 0
-#endif
 
 __device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
@@ -236,9 +230,7 @@ __global__ __launch_bounds__(kGcNT, GcShape<TM>::WGS) void k_gram_chol_mf(const 
 #pragma unroll
     for (int kk = 0; kk < kGcPC / 4; ++kk) {
       const cpx<double>* row = a + (4 * kk + (lane >> 4)) * kGcLD;
-#ifndef CCSC_ABL_NOGRAM
       if (kk < kvalid) gram_kstep<TM>(row, wave, Tn, gr, gi);
-#endif
     }
     const cpx<double>* b = sB + buf * kGcPC * NV;
 #pragma unroll
@@ -266,53 +258,39 @@ __global__ __launch_bounds__(kGcNT, GcShape<TM>::WGS) void k_gram_chol_mf(const 
   cpx<double>* Pbuf = reinterpret_cast<cpx<double>*>(smem);   // [2][kGcTM][kGcTSZ]
   cpx<double>* Lf = L + (int64_t)f * (K * (K + 1) / 2);
   first_panel<TM>(Pbuf, wave, Tn, gr, gi);
-#ifdef CCSC_ABL_NOCHOL
-  Tn = 0;   // ablation build: skip the factorisation (timing only)
-#endif
   for (int j = 0; j < Tn; ++j) {
     cpx<double>* P = Pbuf + (j & 1) * kGcTM * kGcTSZ;
     cpx<double>* Pn = Pbuf + ((j + 1) & 1) * kGcTM * kGcTSZ;
     __syncthreads();   // column j's tiles are in P
-    // Panel j (POTRF of tile (j, j) + TRSM of the tiles below) in one left-looking
-    // sweep over its 16 columns, every wave on its own: lanes 0..15 hold the rows of
-    // tile (j, j) (all four waves redundantly, so no wave waits for another), lanes
-    // 16..16 + RW - 1 up to RW = 4 (TM - 1) of the panel's other rows.  Column c of row r:
+    // Panel j (POTRF of tile (j, j) + TRSM of the tiles below) in one sweep over its 16
+    // columns, every wave on its own: lanes 0..15 hold the rows of tile (j, j) (all four
+    // waves redundantly, so no wave waits for another), lanes 16..16 + RW - 1 up to
+    // RW = 4 (TM - 1) of the panel's other rows.  Column c of row r:
     //   s = a[r][c] - sum_{k < c} L[r][k] conj(L[c][k]);  L[c][c] = sqrt(s of row c),
-    //   L[r][c] = s / L[c][c]  (the POTRF and TRSM formulas coincide),
-    // L[c][k] read back as LDS broadcasts from the wave's own copy Lw of the diagonal
-    // tile (written by lanes 0..15 one column earlier), the pivot by v_readlane.
+    //   L[r][c] = s / L[c][c]  (the POTRF and TRSM formulas coincide).
     {
-      cpx<double>* Lw = Pbuf + 2 * kGcTM * kGcTSZ + wave * kGcTSZ;
       const bool diag = lane < 16;
       constexpr int RW = 4 * (TM - 1);   // panel rows below the diagonal tile per wave (<= 48)
       static_assert(16 + RW <= 64, "panel rows per wave");
       const int q = wave * RW + lane - 16;
       const int ti = diag ? j : j + 1 + (q >> 4);
       const int row = diag ? lane : (q & 15);
-#ifdef CCSC_ABL_NOTRSM
-      const bool mine = diag;
-#else
       const bool mine = diag || (lane < 16 + RW && ti < Tn);
-#endif
       cpx<double> x[16];
 #pragma unroll
       for (int c = 0; c < 16; ++c)
         x[c] = mine ? P[ti * kGcTSZ + c * kGcTS + row] : cpx<double>{1.0, 0.0};
-#if !defined(CCSC_ABL_NOPOTRF) && CCSC_GC_RL
       // right-looking in registers: once column c is final, every row r loses
       // L[r][c] conj(L[c2][c]) from its column c2 > c, L[c2][c] broadcast from lane c2 by
       // v_readlane -- no LDS round trip on the column-to-column chain; 1/sqrt of the
       // pivot by v_rsq_f64 and one Newton step (error ~1.5 e0^2; a second one measured
-      // 1.4% of the kernel, CCSC_GC_NEWTON2) instead of sqrt and a division
+      // 1.4% of the kernel, profiles/r03j/gram_newton_ab.txt) instead of sqrt and a division
 #pragma unroll
       for (int c = 0; c < 16; ++c) {
         const double a = rdl(x[c].x, c);
         double y = __builtin_amdgcn_rsq(a);
         const double hh = 0.5 * a;
         y = fma(y, fma(-hh * y, y, 0.5), y);
-#if CCSC_GC_NEWTON2
-        y = fma(y, fma(-hh * y, y, 0.5), y);
-#endif
         x[c] = (lane == c) ? cpx<double>{a * y, 0.0} : cscale(x[c], y);
 #pragma unroll
         for (int c2 = c + 1; c2 < 16; ++c2) {
@@ -321,29 +299,6 @@ __global__ __launch_bounds__(kGcNT, GcShape<TM>::WGS) void k_gram_chol_mf(const 
           x[c2].y -= x[c].y * lx - x[c].x * ly;
         }
       }
-#elif !defined(CCSC_ABL_NOPOTRF)
-#pragma unroll
-      for (int c = 0; c < 16; ++c) {
-        cpx<double> s0 = x[c], s1 = {0.0, 0.0};
-#pragma unroll
-        for (int k0 = 0; k0 < c; k0 += 4) {
-          asm volatile("" ::: "memory");   // at most four broadcast reads in flight
-#pragma unroll
-          for (int k = k0; k < k0 + 4 && k < c; ++k) {
-            const cpx<double> l = Lw[k * kGcTS + c];   // L[c][k]
-            cpx<double>& acc = (k & 1) ? s1 : s0;
-            acc.x -= x[k].x * l.x + x[k].y * l.y;
-            acc.y -= x[k].y * l.x - x[k].x * l.y;
-          }
-        }
-        const cpx<double> sc = cadd(s0, s1);
-        const double d = sqrt(rdl(sc.x, c));
-        x[c] = (lane == c) ? cpx<double>{d, 0.0} : cscale(sc, 1.0 / d);
-        if (diag) Lw[c * kGcTS + lane] = x[c];
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // column c visible to the wave
-        __builtin_amdgcn_wave_barrier();
-      }
-#endif
       const int gr_ = 16 * ti + row;
       if (mine && (!diag || wave == 0) && gr_ < K) {
 #pragma unroll
@@ -358,9 +313,7 @@ __global__ __launch_bounds__(kGcNT, GcShape<TM>::WGS) void k_gram_chol_mf(const 
       }
     }
     __syncthreads();   // the panel L_.j is in P
-#ifndef CCSC_ABL_NOTRAIL
     if (j + 1 < Tn) trail_step<TM>(P, Pn, j, wave, Tn, gr, gi);
-#endif
   }
 }
 
@@ -373,7 +326,7 @@ bool gram_chol_mf_ok(int K, int NV) {
 size_t gram_chol_mf_smem(int NV, int K) {
   const int tm = gc_tm(K);
   const size_t stage = (size_t)2 * kGcPC * (16 * tm + 1) * 16 + (size_t)2 * kGcPC * NV * 16;
-  const size_t chol = (size_t)(2 * tm + 4) * kGcTSZ * 16;   // two panels + the waves' L_jj
+  const size_t chol = (size_t)2 * tm * kGcTSZ * 16;   // two column panels
   return stage > chol ? stage : chol;
 }
 

@@ -41,10 +41,7 @@ struct ColGeom {
 // hold up to kLineGT generic-radix tasks per thread across a pass barrier.
 constexpr int kLineNT = 256;
 constexpr int kLineGT = 4;
-#ifndef CCSC_LINE_BS
-#define CCSC_LINE_BS 1
-#endif
-constexpr int kLineBS = CCSC_LINE_BS;   // native-pass butterflies per thread: maxb_for_radix * BS
+constexpr int kLineBS = 1;   // native-pass butterflies per thread: maxb_for_radix * BS
 
 constexpr int kRowParts = 5;   // partial sums per row workgroup (see RowArgs)
 

@@ -105,11 +105,8 @@ static void add_twiddles(Plan1D& p, std::vector<cpx<double>>& t) {
   }
 }
 
-// LDS budget of one line-kernel workgroup (four or more per CU); CCSC_LINE_LDS_KB overrides
-static size_t line_lds() {
-  const char* e = std::getenv("CCSC_LINE_LDS_KB");
-  return (e && std::atoi(e) > 0) ? (size_t)std::atoi(e) * 1024 : (size_t)40 * 1024;
-}
+// LDS budget of one line-kernel workgroup (four or more per CU)
+static size_t line_lds() { return (size_t)40 * 1024; }
 
 static int twiddle_count(const Plan1D& p) {
   int n = 0, Ns = 1;

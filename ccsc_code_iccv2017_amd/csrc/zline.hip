@@ -50,29 +50,27 @@
 
 
 // Measured on the C2 slice (n = 1000, ms per launch): 7.98 plain, 7.75 nontemporal state,
-// 8.56 resident w alone, 7.17 both (tools/gpu_ab_zl.sh); a next-slice state prefetch by the
-// idle wave (LDS-DMA) and w held in registers (49 spills) were slower.  -D...=0 for A/B.
-#ifndef CCSC_ZL_NT
-#define CCSC_ZL_NT 1
-#endif
-#ifndef CCSC_ZL_WLDS
-#define CCSC_ZL_WLDS 1
-#endif
-
-// timing-only ablations (wrong results; tools/gpu_ab_zl.sh): CCSC_ABL_NODK replaces the
-// per-slice filter-spectrum loads (dcorr_k, dhat_k: L2 hits) by register constants,
-// CCSC_ABL_NOSTATE drops the state stream (HBM; _NOSTLOAD / _NOSTSTORE only its loads /
-// stores), CCSC_ABL_NOBAR the workgroup barriers
+// 8.56 resident w alone, 7.17 both (round 2); a next-slice state prefetch by the idle wave
+// (LDS-DMA) and w held in registers (49 spills) were slower.
 
 namespace ccsc {
 
-#if CCSC_ZL_WLDS
 constexpr int kZlWL = 7;   // waves whose w bins stay in LDS (35 columns x 110 bins, 61.6 KB)
 constexpr size_t kZlWBytes = (size_t)kZlWL * 5 * zl::Y * 16;
-#else
-constexpr size_t kZlWBytes = 0;
-#endif
-constexpr size_t kZlSmem = zl::kSmem + kZlWBytes;
+// Per-lane LDS address tables (uint32 byte offsets, rows of kZlTR entries), filled once per
+// workgroup: the T addresses of the slice loop depend only on the lane's line position and
+// the register index, but cost 4 - 13 integer VALU instructions each to form (mod-110
+// wraps, the Hermitian fold, the even/odd column placement) -- read from the tables they
+// cost one add (~180 VALU instructions per wave and slice less).
+//   kLutP1 [sa][n2]  row  (11 sa + 10 n2) mod 110 of T, times RS * 16   (P1 sink)
+//   kLutP3 [s][k1]   column tcol(fold(x)) * 16 of x = (xb(s) + 11 k1) mod 110, bit 0 set
+//                    when x > 55 (conjugate: the Hermitian half, P3)
+//   kLutP7 [n1][n2]  (kZlWR wv + zoff(n1 >> 1)) * 16, wv = (n1 + n2) mod 11  (P7 rows)
+constexpr int kZlTR = 12;
+constexpr int kLutP1 = 0, kLutP3 = 10 * kZlTR, kLutP7 = kLutP3 + 11 * kZlTR;
+constexpr int kLutN = kLutP7 + 10 * kZlTR;
+constexpr size_t kZlLutOff = zl::kSmem + kZlWBytes;
+constexpr size_t kZlSmem = kZlLutOff + (size_t)kLutN * 4;
 static_assert(kZlSmem <= 160 * 1024, "z-step LDS");
 
 // clamp(a, -theta, theta): the prox and the dual update of a z-iteration are
@@ -83,30 +81,9 @@ __device__ __forceinline__ T clamp_t(T a, T theta) {
   return fmax(-theta, fmin(a, theta));
 }
 
-
-#ifdef CCSC_ABL_LDSLIN
-// timing-only ablation (wrong results): every LDS access of the slice loop goes to a
-// lane-linear, conflict-free slot (register r of wave w: slot lane + 64 (r mod 16) + 1024 (w mod 6))
-template <typename T>
-__device__ __forceinline__ cpx<T>& ablx(int r) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  return reinterpret_cast<cpx<T>*>(smem)[(threadIdx.x & 63) + 64 * (r & 15) + 1024 * ((threadIdx.x >> 6) % 6)];
-}
-#define LX(expr, r) ablx<T>(r)
-#else
-#define LX(expr, r) (expr)
-#endif
-
-// CCSC_ABL_NODFT (timing only, wrong results): the line DFTs of the slice loop pass their
-// inputs through unchanged (no butterfly arithmetic)
 template <typename T, int R, int SIGN, typename Sink>
 __device__ __forceinline__ void zdft(cpx<T> (&v)[R], Sink&& sink) {
-#ifdef CCSC_ABL_NODFT
-#pragma unroll
-  for (int q = 0; q < R; ++q) sink(q, v[q]);
-#else
   dft_sink<T, R, SIGN>(v, sink);
-#endif
 }
 
 __device__ __forceinline__ void wave_lds_fence() {
@@ -125,11 +102,11 @@ __device__ __forceinline__ void wave_lds_fence() {
 template <typename T, int ES, typename Sink>
 __device__ __forceinline__ void fwd_line(cpx<T> (&v)[11], cpx<T>* E, int s, Sink&& sink) {
   const int sa = min(s, 9);
-  zdft<T, 11, -1>(v, [&](int k2, cpx<T> val) { LX(E[(sa * 11 + k2) * ES], k2) = val; });
+  zdft<T, 11, -1>(v, [&](int k2, cpx<T> val) { E[(sa * 11 + k2) * ES] = val; });
   wave_lds_fence();
   cpx<T> in[10];
 #pragma unroll
-  for (int n1 = 0; n1 < 10; ++n1) in[n1] = LX(E[(n1 * 11 + s) * ES], n1);
+  for (int n1 = 0; n1 < 10; ++n1) in[n1] = E[(n1 * 11 + s) * ES];
   zdft<T, 10, -1>(in, sink);
 }
 
@@ -137,24 +114,16 @@ __device__ __forceinline__ void fwd_line(cpx<T> (&v)[11], cpx<T>* E, int s, Sink
 // -> layout A (out[n2], lane n1 = s < 10).
 template <typename T, int ES, typename Sink>
 __device__ __forceinline__ void inv_line(cpx<T> (&in)[10], cpx<T>* E, int s, Sink&& sink) {
-  zdft<T, 10, +1>(in, [&](int n1, cpx<T> val) { LX(E[(n1 * 11 + s) * ES], n1) = val; });
+  zdft<T, 10, +1>(in, [&](int n1, cpx<T> val) { E[(n1 * 11 + s) * ES] = val; });
   wave_lds_fence();
   const int sa = min(s, 9);
   cpx<T> v[11];
 #pragma unroll
-  for (int k2 = 0; k2 < 11; ++k2) v[k2] = LX(E[(sa * 11 + k2) * ES], k2);
+  for (int k2 = 0; k2 < 11; ++k2) v[k2] = E[(sa * 11 + k2) * ES];
   zdft<T, 11, +1>(v, sink);
 }
 
-__device__ __forceinline__ void zl_sync() {
-#ifdef CCSC_ABL_NOBAR
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-#else
-  lds_sync();
-#endif
-}
+__device__ __forceinline__ void zl_sync() { lds_sync(); }
 
 // (e mod 110) for 0 <= e < 220
 __device__ __forceinline__ int mod110(int e) { return e >= 110 ? e - 110 : e; }
@@ -176,87 +145,66 @@ __device__ __forceinline__ int xoff(int l) { return 110 * l + (l < 2 ? 0 : l == 
 __device__ __forceinline__ int zoff(int l) { return 110 * l + (l < 1 ? 0 : l < 4 ? 5 + l : 11); }
 constexpr int kZlWR = 10 * zl::RS;   // complex slots of a wave's ten T rows
 
+// the z-step's LDS as bytes (32-bit offsets: no 64-bit address arithmetic)
+template <typename T>
+__device__ __forceinline__ cpx<T>& lds_cpx_at(uint32_t byte_off) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  return *reinterpret_cast<cpx<T>*>(smem + byte_off);
+}
+// row r (kZlTR entries, 16-B aligned) of an address table
+__device__ __forceinline__ void lut_row(int table, int r, uint32_t (&e)[kZlTR]) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+  const u4* q = reinterpret_cast<const u4*>(smem + kZlLutOff + (size_t)(table + r * kZlTR) * 4);
+#pragma unroll
+  for (int i = 0; i < kZlTR / 4; ++i) {
+    const u4 v = q[i];
+    e[4 * i] = v.x;
+    e[4 * i + 1] = v.y;
+    e[4 * i + 2] = v.z;
+    e[4 * i + 3] = v.w;
+  }
+}
+__device__ void fill_luts() {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint32_t* lut = reinterpret_cast<uint32_t*>(smem + kZlLutOff);
+  for (int q = threadIdx.x; q < kLutN; q += blockDim.x) {
+    uint32_t v = 0;
+    if (q < kLutP3) {
+      const int sa = q / kZlTR, n2 = q % kZlTR;
+      v = (uint32_t)(((11 * sa + 10 * n2) % 110) * zl::RS * 16);
+    } else if (q < kLutP7) {
+      const int s = (q - kLutP3) / kZlTR, k1 = (q - kLutP3) % kZlTR;
+      const int x = ((s ? 110 - 10 * s : 0) + 11 * k1) % 110;
+      const bool hi = x >= zl::Xh;
+      v = (uint32_t)(tcol(hi ? zl::X - x : x) * 16) | (hi ? 1u : 0u);
+    } else {
+      const int n1 = (q - kLutP7) / kZlTR, n2 = (q - kLutP7) % kZlTR;
+      v = (uint32_t)((kZlWR * ((n1 + n2) % 11) + zoff(n1 >> 1)) * 16);
+    }
+    lut[q] = v;
+  }
+}
+
 // 16-B global access at a 32-bit byte offset from a wave-uniform base (saddr form:
 // SGPR base + one VGPR offset, no 64-bit VGPR address per access).
 template <typename V>
 __device__ __forceinline__ V zld(const void* base, uint32_t boff) {
   return *reinterpret_cast<const V*>(reinterpret_cast<const char*>(base) + boff);
 }
-// the per-slice filter-spectrum loads (dcorr_k, dhat_k)
-template <typename V>
-__device__ __forceinline__ V dld(const void* base, uint32_t boff) {
-#ifdef CCSC_ABL_NODK
-  V v;
-  v.x = 1e-3 * (double)(boff & 255);
-  v.y = 1e-3;
-  (void)base;
-  return v;
-#else
-  return zld<V>(base, boff);
-#endif
-}
 template <typename V>
 __device__ __forceinline__ void zst(void* base, uint32_t boff, V v) {
   *reinterpret_cast<V*>(reinterpret_cast<char*>(base) + boff) = v;
 }
-// state stream (read once, written once per launch): CCSC_ZL_NT marks it nontemporal so it
-// does not evict the re-read spectra (w, dcorr, dhat) from L2
-typedef double nt_d2 __attribute__((ext_vector_type(2)));
-template <typename V>
-__device__ __forceinline__ V sld(const void* base, uint32_t boff) {
-#if defined(CCSC_ABL_NOSTATE) || defined(CCSC_ABL_NOSTLOAD)
-  V s;
-  s.x = 1e-3 * (double)(boff & 255);
-  s.y = -s.x;
-  (void)base;
-  return s;
-#elif CCSC_ZL_NT
-  const nt_d2 r = __builtin_nontemporal_load(
-      reinterpret_cast<const nt_d2*>(reinterpret_cast<const char*>(base) + boff));
-  V v;
-  v.x = r.x;
-  v.y = r.y;
-  return v;
-#else
-  return zld<V>(base, boff);
-#endif
-}
-template <typename V>
-__device__ __forceinline__ void sst(void* base, uint32_t boff, V v) {
-#if defined(CCSC_ABL_NOSTATE) || defined(CCSC_ABL_NOSTSTORE)
-  if (v.x == 12345.678) zst<V>(base, boff, v);   // keeps the value live, never stores
-#elif CCSC_ZL_NT
-  const nt_d2 r = {v.x, v.y};
-  __builtin_nontemporal_store(r, reinterpret_cast<nt_d2*>(reinterpret_cast<char*>(base) + boff));
-#else
-  zst<V>(base, boff, v);
-#endif
-}
-// Buffer-descriptor forms of the slice loop's global accesses (CCSC_ZL_BUF): the
-// wave-uniform base goes into a descriptor, the lane's byte offset into voffset and
-// the register's constant offset into soffset (an SGPR), so no per-access 64-bit
-// VGPR address arithmetic is issued (tools/gpu_ab_zl.sh).
-#ifndef CCSC_ZL_BUF
-#define CCSC_ZL_BUF 1
-#endif
-#ifndef CCSC_ZL_BUF_F
-#define CCSC_ZL_BUF_F CCSC_ZL_BUF
-#endif
-#ifndef CCSC_ZL_BUF_W
-#define CCSC_ZL_BUF_W CCSC_ZL_BUF
-#endif
-#ifndef CCSC_ZL_BUF_S
-#define CCSC_ZL_BUF_S CCSC_ZL_BUF
-#endif
-#if CCSC_ZL_BUF
+// Buffer-descriptor forms of the slice loop's global loads: the wave-uniform base goes
+// into a descriptor, the lane's byte offset into voffset and the register's constant
+// offset into soffset (an SGPR), so no per-access 64-bit VGPR address arithmetic is
+// issued (6.75 -> 6.55 ms at n = 1000, round 3).
 typedef unsigned int zl_u4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t zrsrc(const void* base, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
 }
-#ifndef CCSC_ZL_BUF_AUX
-#define CCSC_ZL_BUF_AUX 2
-#endif
-constexpr int kZlNT = CCSC_ZL_BUF_AUX;   // cache policy bit: nontemporal (gfx950 NT = SLC)
+constexpr int kZlNT = 2;   // cache policy bit: nontemporal (gfx950 NT = SLC)
 template <typename V, int AUX>
 __device__ __forceinline__ V bld(const void* base, uint32_t bytes, uint32_t voff, uint32_t soff) {
   const zl_u4 u = __builtin_amdgcn_raw_buffer_load_b128(zrsrc(base, bytes), voff, soff, AUX);
@@ -264,50 +212,29 @@ __device__ __forceinline__ V bld(const void* base, uint32_t bytes, uint32_t voff
   __builtin_memcpy(&v, &u, 16);
   return v;
 }
-template <typename V, int AUX>
-__device__ __forceinline__ void bst(void* base, uint32_t bytes, uint32_t voff, uint32_t soff, V v) {
-  zl_u4 u;
-  __builtin_memcpy(&u, &v, 16);
-  __builtin_amdgcn_raw_buffer_store_b128(u, zrsrc(base, bytes), voff, soff, AUX);
-}
-#endif
 // spectrum (F complex) access: lane offset + register offset
 template <typename V>
 __device__ __forceinline__ V fld(const void* base, uint32_t lane, uint32_t reg) {
-#if CCSC_ZL_BUF && CCSC_ZL_BUF_F && !defined(CCSC_ABL_NODK)
   return bld<V, 0>(base, zl::F * 16, lane, reg);
-#else
-  return dld<V>(base, lane + reg);
-#endif
 }
 template <typename V>
 __device__ __forceinline__ V wld(const void* base, uint32_t lane, uint32_t reg) {
-#if CCSC_ZL_BUF && CCSC_ZL_BUF_W
   return bld<V, 0>(base, zl::F * 16, lane, reg);
-#else
-  return zld<V>(base, lane + reg);
-#endif
 }
-// state slice (P reals) access, nontemporal
+// The state stream (read once, written once per launch) is nontemporal, so it does not
+// evict the re-read spectra (w, dcorr, dhat) from L2.  State slice (P reals) loads:
 template <typename V>
 __device__ __forceinline__ V sld2(const void* base, uint32_t lane, uint32_t reg) {
-#if CCSC_ZL_BUF && CCSC_ZL_BUF_S && CCSC_ZL_NT && !defined(CCSC_ABL_NOSTATE) && !defined(CCSC_ABL_NOSTLOAD)
   return bld<V, kZlNT>(base, zl::P * 8, lane, reg);
-#else
-  return sld<V>(base, lane + reg);
-#endif
 }
-// (state stores stay global stores by default: a buffer store carrying the register offset
-// in soffset failed the mode-2 parity cases on the GPU -- with either cache policy and with a
-// larger range -- while the same store with the whole offset in voffset passes, and then it
-// costs the same per-store VGPR add as the global store: tools/gpu_var_test.sh)
+// state stores stay global stores: a buffer store carrying the register offset in soffset
+// failed the mode-2 parity cases on the GPU (round 3), while the same store with the whole
+// offset in voffset passes and then costs the same per-store VGPR add as a global store
+typedef double nt_d2 __attribute__((ext_vector_type(2)));
 template <typename V>
 __device__ __forceinline__ void sst2(void* base, uint32_t lane, uint32_t reg, V v) {
-#if defined(CCSC_ZL_BUF_SS) && CCSC_ZL_BUF && CCSC_ZL_BUF_S && CCSC_ZL_NT && !defined(CCSC_ABL_NOSTATE) && !defined(CCSC_ABL_NOSTSTORE)
-  bst<V, kZlNT>(base, zl::P * 8, lane + reg, 0, v);
-#else
-  sst<V>(base, lane + reg, v);
-#endif
+  const nt_d2 r = {v.x, v.y};
+  __builtin_nontemporal_store(r, reinterpret_cast<nt_d2*>(reinterpret_cast<char*>(base) + lane + reg));
 }
 
 // an opaque copy of a lane index: per-lane address math is redone where it is used
@@ -348,7 +275,7 @@ __device__ __forceinline__ int fresh(int v) {
 // untouched.
 constexpr int kZtStore = kZlTolStore, kZtCmp = kZlTolCmp, kZtForm = kZlTolForm;
 template <typename T, int MODE, int TOL>
-__global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn, const T* Yn,
+__global__ __launch_bounds__(zl::NT) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_zline(const T* A, T* Ao, const T* Zn, const T* Yn,
                                                   cpx<T>* __restrict__ W,
                                                   const cpx<T>* __restrict__ Bs,
                                                   const cpx<T>* __restrict__ dcorr,
@@ -375,7 +302,6 @@ __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn
   const bool xwave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6) < 11;
   T nd = (T)0, nz = (T)0;   // kCmp: ||z_cur - z_prev||^2, ||z_cur||^2 of the lanes' own elements
   T fd = (T)0, fz = (T)0;   // kForm: ||z_t+1 - z_t||^2, ||z_t+1||^2 (element, then bin terms)
-#if CCSC_ZL_WLDS
   // w is the same for every slice of the patch: the y-lines of waves 0..kZlWL-1 (columns
   // 0..5 kZlWL - 1) keep their bins in the LDS left over beside T, each lane its own ten
   // (slot k1 * 385 + c * 11 + k2; written and read back by the same lane, so no barrier)
@@ -390,7 +316,9 @@ __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn
       for (int k1 = 0; k1 < 10; ++k1) sW[k1 * 385 + c * 11 + sb] = zld<cpx<T>>(Wp, bo + k1 * 616 * 16);
     }
   }
-#endif
+
+  fill_luts();
+  __syncthreads();
 
   for (int k = 0; k < K; ++k) {
     // lane roles, recomputed per slice from an opaque thread index (see fresh())
@@ -406,44 +334,61 @@ __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn
     const int64_t sl = (p * K + k) * zl::P;
     cpx<T> zc[11];   // c = u - y of the row pair (x-lines, layout A) for the R2C
     const uint32_t po = (uint32_t)(j * 10 + fresh(sa)) * 16u;   // pair n2 at po + n2*550*16
+    V2 av[11];   // the state a of row pair j (layout A), mode 2
     if constexpr (MODE >= 2) {
       // ---- P1: y-C2R of conj(dcorr_k) w from bins to T[y][c] ----
       const cpx<T>* dk = dcorr + (int64_t)k * zl::F;
       const uint32_t bo = (uint32_t)(c * 11 + sb) * 16u;
-#if CCSC_ZL_WLDS
       const bool wl = __builtin_amdgcn_readfirstlane(wave) < kZlWL;
-#endif
-      cpx<T> b[10];
+      // every operand load first, then the products (sched_barrier): interleaved, the
+      // scheduler waits for each load pair in turn -- ten L2 round trips per wave
+      cpx<T> b[10], wv[10];
+      if (wl) {
 #pragma unroll
-      for (int k1 = 0; k1 < 10; ++k1)
-#if CCSC_ZL_WLDS
-        b[k1] = cmulc(fld<cpx<T>>(dk, bo, k1 * 616 * 16),
-                      wl ? sW[k1 * 385 + c * 11 + sb] : wld<cpx<T>>(Wp, bo, k1 * 616 * 16));
-#else
-        b[k1] = cmulc(zld<cpx<T>>(dk, bo + k1 * 616 * 16), zld<cpx<T>>(Wp, bo + k1 * 616 * 16));
-#endif
-      inv_line<T, zl::RS>(b, Ey, sb, [&](int n2, cpx<T> val) {
-        LX(sT[mod110(11 * sa + 10 * n2) * zl::RS + tcol(c)], n2 + 5) = val;
-      });
+        for (int k1 = 0; k1 < 10; ++k1) {
+          b[k1] = fld<cpx<T>>(dk, bo, k1 * 616 * 16);
+          wv[k1] = sW[k1 * 385 + c * 11 + sb];
+        }
+      } else {
+#pragma unroll
+        for (int k1 = 0; k1 < 10; ++k1) {
+          b[k1] = fld<cpx<T>>(dk, bo, k1 * 616 * 16);
+          wv[k1] = wld<cpx<T>>(Wp, bo, k1 * 616 * 16);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int k1 = 0; k1 < 10; ++k1) b[k1] = cmulc(b[k1], wv[k1]);
+      uint32_t r1[kZlTR];   // T rows of the column's elements (layout A of the y-line)
+      lut_row(kLutP1, fresh(sa), r1);
+      const uint32_t cb1 = (uint32_t)tcol(c) * 16u;
+      inv_line<T, zl::RS>(b, Ey, sb, [&](int n2, cpx<T> val) { lds_cpx_at<T>(r1[n2] + cb1) = val; });
       zl_sync();   // P2
       if (xwave) {
         // ---- P3: x-C2R of row pair j: Z(x) = R_2j(x) + i R_2j+1(x), Hermitian ext. ----
         const int s3 = fresh(sb);
-        const int xb = s3 ? 110 - 10 * s3 : 0;   // elem_b(k2, 0)
-        cpx<T> zb[10];
-        const cpx<T>* r0 = sT + 2 * j * zl::RS;
+        cpx<T> zb[10], zr[10];
+        uint32_t e3[kZlTR];   // column of x = elem_b(s3, k1) (+ 1: conjugate, x > 55)
+        lut_row(kLutP3, s3, e3);
+        const uint32_t r0 = (uint32_t)(2 * j * zl::RS) * 16u;
+        // the 20 reads first, then the rebuild (as P7: no pairwise lgkmcnt waits)
 #pragma unroll
         for (int k1 = 0; k1 < 10; ++k1) {
-          const int x = mod110(xb + 11 * k1);
-          const bool hi = x >= zl::Xh;
-          const int cc = tcol(hi ? zl::X - x : x);
-          const cpx<T> a = LX(r0[cc], 2 * k1), bb = LX(r0[zl::RS + cc], 2 * k1 + 1);
-          const T sg = hi ? (T)-1 : (T)1;   // conjugate both rows above Xh
-          zb[k1] = {fma(-sg, bb.y, a.x), fma(sg, a.y, bb.x)};
+          const uint32_t o = r0 + (e3[k1] & ~15u);
+          zb[k1] = lds_cpx_at<T>(o);
+          zr[k1] = lds_cpx_at<T>(o + zl::RS * 16);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int k1 = 0; k1 < 10; ++k1) {
+          // conjugate both rows above Xh: flip the sign bits of their imaginary parts
+          const uint32_t m = e3[k1] << 31;
+          const T ay = __hiloint2double(__double2hiint(zb[k1].y) ^ (int)m, __double2loint(zb[k1].y));
+          const T by = __hiloint2double(__double2hiint(zr[k1].y) ^ (int)m, __double2loint(zr[k1].y));
+          zb[k1] = {zb[k1].x - by, ay + zr[k1].x};
         }
         // ---- P4: state (row 2j, row 2j+1) at x = elem_a(n1, n2), in flight under the C2R;
         // each corr value is consumed as the last inverse stage forms it ----
-        V2 av[11];
 #pragma unroll
         for (int n2 = 0; n2 < 11; ++n2) av[n2] = sld2<V2>(A + sl, po, n2 * 550 * 16);
         V2 zo[kCmp ? 11 : 1];
@@ -529,25 +474,33 @@ __global__ __launch_bounds__(zl::NT) void k_zline(const T* A, T* Ao, const T* Zn
     if (xwave) {
       const int s5 = fresh(sb);
       cpx<T>* r0 = sT + kZlWR * min(wave, 10) + zoff(l);   // Z_j in layout-B slot order (zslot)
-      fwd_line<T, 1>(zc, Ex, s5, [&](int k1, cpx<T> val) { LX(r0[k1 * 11 + s5], k1 + 3) = val; });
+      fwd_line<T, 1>(zc, Ex, s5, [&](int k1, cpx<T> val) { r0[k1 * 11 + s5] = val; });
     }
     zl_sync();   // P6
     // ---- P7: column c, rows y = n1 + 10 n2: two-for-one separation ----
     cpx<T> col[11];
     {
       const int n1 = fresh(sa);
-      const int zc1 = zslot(c), zc2 = zslot((c == 0) ? 0 : zl::X - c);
+      const uint32_t a1 = (uint32_t)zslot(c) * 16u, a2 = (uint32_t)zslot((c == 0) ? 0 : zl::X - c) * 16u;
       // even rows: z1 + conj z2; odd rows: (z1 - conj z2) / i (row parity = n1's) -- twice
       // the row spectra: the 1/2 is applied once to the patch's accumulated bins
       const bool odd = n1 & 1;
+      // row y = (11 n1 + 10 n2) mod 110: pair y >> 1 is line n1 >> 1 of wave (n1 + n2) mod 11
+      uint32_t e7[kZlTR];
+      lut_row(kLutP7, n1, e7);
+      // all 22 reads first, then the arithmetic: the scheduler otherwise interleaves them
+      // pairwise with a full lgkmcnt wait each (eleven LDS round trips per wave)
+      cpx<T> z1[11], z2[11];
 #pragma unroll
       for (int n2 = 0; n2 < 11; ++n2) {
-        // row y = (11 n1 + 10 n2) mod 110: pair y >> 1 is line n1 >> 1 of wave (n1 + n2) mod 11
-        const int wv = n1 + n2 >= 11 ? n1 + n2 - 11 : n1 + n2;
-        const cpx<T>* r0 = sT + kZlWR * wv + zoff(n1 >> 1);
-        const cpx<T> z1 = LX(r0[zc1], n2), z2 = LX(r0[zc2], n2 + 11);
-        const T ex = z1.x + z2.x, ey = z1.y - z2.y;
-        const T ox = z1.y + z2.y, oy = z2.x - z1.x;
+        z1[n2] = lds_cpx_at<T>(e7[n2] + a1);
+        z2[n2] = lds_cpx_at<T>(e7[n2] + a2);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int n2 = 0; n2 < 11; ++n2) {
+        const T ex = z1[n2].x + z2[n2].x, ey = z1[n2].y - z2[n2].y;
+        const T ox = z1[n2].y + z2[n2].y, oy = z2[n2].x - z1[n2].x;
         col[n2] = {odd ? ox : ex, odd ? oy : ey};
       }
     }

@@ -136,11 +136,7 @@ __global__ __launch_bounds__(NT) void k_zsplit(const T* A, T* Ao, const T* __res
           lds_cpx_store(S.slice + y * RS + 2 * (f - y * GO::Xh(Gd)), 1, cmulc(dv[i], wv[i]));
         }
       }
-#ifndef CCSC_ABL_NOC2R
       GO::c2r(S.slice, Gd, S.tw, tid);
-#else
-      lds_sync();
-#endif
     }
     asm volatile("" : "+v"(tid));  // elementwise index math after the C2R, not live across it
     if (vec) {
@@ -192,11 +188,7 @@ __global__ __launch_bounds__(NT) void k_zsplit(const T* A, T* Ao, const T* __res
     }
     if (GO::Yp(Gd) != GO::Y(Gd))
       for (int x = tid; x < RS; x += NT) S.slice[Yd * RS + x] = (T)0;
-#ifndef CCSC_ABL_NOR2C
     GO::r2c(S.slice, Gd, S.tw, tid);
-#else
-    lds_sync();
-#endif
     // next slice's state: issued after the R2C, when this slice's stores (whose
     // data registers the loads overwrite) have drained; it lands under the
     // accumulation and the next C2R
@@ -325,15 +317,9 @@ __global__ __launch_bounds__(kNT) void k_zhat_split(const T* __restrict__ A,
 // VGPRs per lane for the transform, the accumulator bins and the one-slice
 // state prefetch (16 waves cap a lane at 128 and spill); the wave-local line
 // transforms of the 110 grid need 11 (x) and 12 (y) waves.
-#ifndef CCSC_ZS_NT
-#define CCSC_ZS_NT 768
-#endif
-#ifndef CCSC_ZS_NBR
-#define CCSC_ZS_NBR 6
-#endif
-constexpr int kZsNT = CCSC_ZS_NT;
+constexpr int kZsNT = 768;
 constexpr int kZsNB = (Grid110::F + kZsNT - 1) / kZsNT;
-constexpr int kZsNBR = CCSC_ZS_NBR < kZsNB ? CCSC_ZS_NBR : kZsNB;
+constexpr int kZsNBR = 6 < kZsNB ? 6 : kZsNB;
 constexpr int kZsNBL = kZsNB - kZsNBR;
 
 size_t zsplit_smem_bytes(const Grid2D& G) {

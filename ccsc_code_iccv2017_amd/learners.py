@@ -155,7 +155,9 @@ def make_problem(variant, b_shape, kernel_size, lambda_residual, lambda_prior, m
     p.rho_d = float(rho_d or 0)
     p.rho_z = float(rho_z or 0)
     p.theta_div = float(theta_div or 0)
-    p.precision = L.CCSC_FP64 if precision == "fp64" else L.CCSC_FP32
+    if precision != "fp64":
+        raise ValueError("precision must be 'fp64' (the reference computes in double)")
+    p.precision = L.CCSC_FP64
     p.trace_objective = 1 if trace_objective else 0
     p.seed = int(seed)
     if dfactor not in L.DFACTOR:

@@ -66,8 +66,11 @@ extern "C" {
 #define CCSC_VERBOSE_BRIEF 1
 #define CCSC_VERBOSE_ALL 2
 
+/* arithmetic and storage precision: double only, as the reference computes (MATLAB
+ * double; the 4D driver's single-precision b, learn_kernels_4D_extract_patches.m:46,
+ * is widened on input).  A reduced-precision storage mode was declared in earlier
+ * rounds and never built; it is not part of the ABI. */
 #define CCSC_FP64 0
-#define CCSC_FP32 1
 
 /* form of the per-frequency D-step factor (precompute_H_hat_D, dP:221-237).
  * AUTO: Woodbury when blocks hold few patches (ni <= 8 and 4 ni <= K), else the
@@ -101,7 +104,7 @@ typedef struct ccsc_problem {
   double rho_d;             /* dP:98,111                                            */
   double rho_z;             /* dP:153                                               */
   double theta_div;         /* soft threshold = lambda_prior / theta_div (dP:150)   */
-  int32_t precision;        /* CCSC_FP64 (reference precision) or CCSC_FP32         */
+  int32_t precision;        /* CCSC_FP64 (the only value; others: CCSC_E_INVALID)   */
   int32_t trace_objective;  /* 1: evaluate the objective after every inner iter     */
   uint64_t seed;            /* device RNG seed for d0/z0 when not supplied          */
   int32_t dfactor;          /* CCSC_DFACTOR_* (0 = AUTO)                            */

@@ -222,7 +222,8 @@ def _want_obj(verbose, which):
 
 
 def _new_trace():
-    return {"obj_d": [], "obj_z": [], "d_diff": [], "z_diff": [], "D1": [], "n_d": [], "n_z": []}
+    return {"obj_d": [], "obj_z": [], "d_diff": [], "z_diff": [], "D1": [], "n_d": [], "n_z": [],
+            "U": []}
 
 
 # ----------------------------------------------------------------------------
@@ -535,6 +536,7 @@ def learn_3d(b, kernel_size, lambda_residual, lambda_prior, max_it, tol, verbose
         trace["obj_d"].append(od)
         trace["d_diff"].append(zd)
         trace["n_d"].append(len(zd))
+        trace["U"].append(u_D2)                                   # the projected consensus
         dhat_flat, dTd = precompute_H_hat_Z(d_hat, ss)            # L3:161
         oz, zz = [], []
         for i_z in range(max_it_z):                               # L3:164

@@ -7,8 +7,8 @@ holds at any size:
     plan fits one MI355X, the iteration-0 objective matches its closed-form expectation
     for random init (1/2 n 10^4 121 K + lambda E|z| n K X Y), and the
     objective is finite and decreases over outer iterations (dZ:165, :174-175);
-  * C1-shaped learning (2D dParallel, K = 100, ni = 100) run for the reference driver's
-    20 outer iterations (learn_kernels_2D_large.m:23) at a reduced n: the learned
+  * C1 (2D dParallel, K = 100, n = 1000, ni = 100 -> 10 blocks) run for the reference
+    driver's 20 outer iterations (learn_kernels_2D_large.m:23): the learned
     filters sit on the unit sphere like the reference's shipped ones
     (2D/Filters/Filters_ours_2D_large.mat, tests/golden/reference_filter_norms.json:
     the constraint dP:212-213 is active at convergence; block 1's local filters D{1},
@@ -51,20 +51,31 @@ def test_c2_fullsize_objective_properties(gpu_ctx):
     assert np.all(np.isfinite(d_res))
 
 
-def test_c1_shape_filters_reach_unit_sphere(gpu_ctx):
+def test_c1_fullsize_20_iterations(gpu_ctx):
+    """C1 at full size (2D dParallel, K = 100 11x11, n = 1000, ni = 100 -> 10 blocks) for
+    the reference driver's 20 outer iterations: the iteration-0 objective matches its
+    closed form for the random init, the objective decreases, and the learned filters
+    sit on the unit sphere (1000 patches take the two-stream z-phase, engine.cpp
+    zsplit_ok)."""
     from ccsc_code_iccv2017_amd import learners as E
     from ccsc_code_iccv2017_amd import synth
-    n, K, psf = 200, 100, 11
+    n, K, psf = 1000, 100, 11
     b = synth.images_2d(n, device="cuda:0", seed=2017)
+    d0 = np.random.default_rng(8).standard_normal((psf, psf, K))
     d_res, _, _, it = E.admm_learn_conv2D_large_dParallel(b, [psf, psf, K], 1.0, 1.0, 20, 0.0,
-                                                          "brief", None, ctx=gpu_ctx,
+                                                          "brief", {"d": d0}, ctx=gpu_ctx,
                                                           want_z=False, want_DZ=False, seed=7)
-    norms = np.sqrt((d_res ** 2).sum(axis=(0, 1)))
     oz = it["obj_vals_z"]
     assert np.all(np.isfinite(oz)) and oz[-1] < oz[1] < oz[0]
-    print("filter norms: min %.6f max %.6f" % (norms.min(), norms.max()))
-    # measured on MI355X (round 2): 0.9982 .. 0.9996 -- block 1's local d-solve output sits
-    # just inside the sphere its consensus projection lies on; the reference's shipped 2D
-    # filters (learned from n = 5 patches) span 0.9998 .. 1.0001
+    X = 100 + 2 * (psf // 2)
+    expect0 = (0.5 * (n * 100 * 100 * float((d0 ** 2).sum()) + float((b ** 2).sum()))
+               + math.sqrt(2 / math.pi) * n * K * X * X)
+    assert abs(oz[0] / expect0 - 1) < 2e-3, (oz[0], expect0)
+    norms = np.sqrt((d_res ** 2).sum(axis=(0, 1)))
+    print("C1 objective %.6e -> %.6e; filter norms: min %.6f max %.6f"
+          % (oz[0], oz[-1], norms.min(), norms.max()))
+    # block 1's local d-solve output sits just inside the sphere its consensus projection
+    # lies on (round 2, n = 200: 0.9982 .. 0.9996); the reference's shipped 2D filters
+    # (learned from n = 5 patches) span 0.9998 .. 1.0001
     assert np.all(np.abs(norms - 1.0) < 2.5e-3), (norms.min(), norms.max())
     assert np.mean(np.abs(norms - 1.0)) < 1e-3

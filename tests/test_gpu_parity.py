@@ -330,22 +330,24 @@ def test_zline_tol_matches_port(gpu_ctx, variant, verbose):
     assert _rel(d_e, O.crop_filters(port.D[0], 2, 5)) < 1e-7
 
 
-def test_zline_two_stream_phase_is_exact(gpu_ctx, monkeypatch):
-    """With tol = 0 and >= 1024 patches on the 110 grid the engine splits every z-launch of a
+@pytest.mark.parametrize("variant", ["dZ", "dP"])
+def test_zline_two_stream_phase_is_exact(gpu_ctx, monkeypatch, variant):
+    """With tol = 0 and >= 512 patches on the 110 grid the engine splits every z-launch of a
     phase over two streams (patches [0, np/2) and the rest, engine.cpp zsplit_ok); the
     per-patch arithmetic is the same kernel's, so the result equals the one-stream run
-    bit for bit."""
+    bit for bit -- for dZ (the bench workload) and dP (C1's 1000 patches take this path)."""
     from ccsc_code_iccv2017_amd import learners as E
     K, n, ni = 3, 1024, 512
     rng = np.random.default_rng(1024)
     b = rng.standard_normal((100, 100, n))
     d0 = rng.standard_normal((11, 11, K))
-    z0 = rng.standard_normal((110, 110, K, ni))
+    z0 = rng.standard_normal((110, 110, K, ni if variant == "dZ" else n))
+    learn = (E.admm_learn_conv2D_large_dzParallel if variant == "dZ"
+             else E.admm_learn_conv2D_large_dParallel)
     out = {}
     for flag in ("1", "0"):
         monkeypatch.setenv("CCSC_ZSPLIT2", flag)
-        out[flag] = E.admm_learn_conv2D_large_dzParallel(
-            b, [11, 11, K], 1.0, 1.0, 2, 0.0, "none", {"d": d0, "z": z0}, ni=ni, max_it_d=2,
-            max_it_z=3, ctx=gpu_ctx)
+        out[flag] = learn(b, [11, 11, K], 1.0, 1.0, 2, 0.0, "none", {"d": d0, "z": z0}, ni=ni,
+                          max_it_d=2, max_it_z=3, ctx=gpu_ctx)
     assert np.array_equal(out["1"][0], out["0"][0])
     assert np.array_equal(out["1"][1], out["0"][1])

@@ -169,6 +169,8 @@ def test_hs_golden_fixture_regression():
     ((8, 7), 2, 3, 2, 2, 0.05, 30),      # rollback at outer iteration 2 (Q16)
     ((20, 20), 31, 11, 100, 2, 1.0, 1),  # C3's W = 31, K = 100, 11x11 filters
     ((100, 100), 31, 11, 8, 2, 1.0, 1),  # C3's 110 x 110 grid
+    ((20, 20), 31, 11, 120, 2, 1.0, 1),  # 112 < K <= 128: TM = 8 MFMA factor
+    ((20, 20), 31, 11, 150, 2, 1.0, 1),  # 128 < K <= 192: TM = 10, three rows per lane
 ])
 def test_learn_hs23_matches_oracle(gpu_ctx, sb, W, psf, K, n, lam, max_it):
     from ccsc_code_iccv2017_amd import learners as E

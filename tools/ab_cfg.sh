@@ -9,5 +9,5 @@ mkdir -p gpurun_out/ab
 for v in "$@"; do
   cp $d/libccsc_$v.so ccsc_code_iccv2017_amd/libccsc.so
   timeout -k 10 300 python -u tools/bench_configs.py --steps 1 --configs ${CONFIGS:-C1,C3,C4,C5} > gpurun_out/ab/$v.cfg.json 2> gpurun_out/ab/$v.cfg.err || exit 1
-  [ -n "$SKIP_BENCH" ] || timeout -k 10 300 python bench.py --n 1000 --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/ab/$v.json 2> gpurun_out/ab/$v.err || exit 1
+  [ -n "$SKIP_BENCH" ] || timeout -k 10 300 python bench.py --n 1000 --steps 2 --warmup 1 --no-cpu-baseline --no-configs > gpurun_out/ab/$v.json 2> gpurun_out/ab/$v.err || exit 1
 done
