@@ -759,14 +759,28 @@ hipError_t launch_invert_diag(cpx<double>* L, int F, int K, hipStream_t st) {
 // One wave per f, lanes over k (RPL rows per lane); row p of M / L_M lives in
 // lane p.
 // ---------------------------------------------------------------------------
+// The spectra the Woodbury kernels read and write are [.][k][..][F] (lanes over k stride
+// F), so a wave's access touches one 16-B piece of K lines: the kWbWG waves of a workgroup
+// take consecutive f (the neighbouring pieces of the same lines), and consecutive
+// workgroups of one XCD (ids i, i + 8, ...) the next f's, so the lines are read and
+// written whole from one L2 instead of piecewise from several.
+constexpr int kWbWG = 8;
+__device__ __forceinline__ int xcd_group(int ntot) {
+  const int per = (int)((gridDim.x + 7) >> 3);
+  const int g = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+  return g < ntot ? g : -1;
+}
+
 template <typename T, int RPL>
-__global__ __launch_bounds__(256) void k_gram_wb(const cpx<T>* __restrict__ Zh,
-                                                 const cpx<T>* __restrict__ Bh,
-                                                 cpx<T>* __restrict__ L, cpx<T>* __restrict__ h,
-                                                 int F, int K, int ni, T rho, int NV, int Kp) {
+__global__ __launch_bounds__(64 * kWbWG) void k_gram_wb(const cpx<T>* __restrict__ Zh,
+                                                        const cpx<T>* __restrict__ Bh,
+                                                        cpx<T>* __restrict__ L,
+                                                        cpx<T>* __restrict__ h, int F, int K,
+                                                        int ni, T rho, int NV, int Kp) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int f = blockIdx.x * 4 + wave;
-  if (f >= F) return;
+  const int g = xcd_group((F + kWbWG - 1) / kWbWG);
+  const int f = g * kWbWG + wave;
+  if (g < 0 || f >= F) return;
   const cpx<T> zero = {(T)0, (T)0};
   cpx<T> a[kWbMaxNi][RPL];
 #pragma unroll
@@ -786,7 +800,7 @@ __global__ __launch_bounds__(256) void k_gram_wb(const cpx<T>* __restrict__ Zh,
     }
   // M[p][q] = rho delta_pq + sum_k A[p][k] conj(A[q][k]), q <= p (wave sums,
   // staged through LDS so that lane p picks up row p with static indices)
-  __shared__ cpx<T> sM[4][kWbMaxNi * kWbMaxNi];
+  __shared__ cpx<T> sM[kWbWG][kWbMaxNi * kWbMaxNi];
 #pragma unroll
   for (int p = 0; p < kWbMaxNi; ++p)
 #pragma unroll
@@ -849,16 +863,19 @@ __global__ __launch_bounds__(256) void k_gram_wb(const cpx<T>* __restrict__ Zh,
   }
 }
 
+// One wave per (block, f), kWbWG consecutive f per workgroup (see k_gram_wb).
 template <typename T, int RPL, int NVB>
-__global__ __launch_bounds__(256) void k_dsolve_wb(const cpx<T>* __restrict__ L,
-                                                   const cpx<T>* __restrict__ h,
-                                                   const cpx<T>* __restrict__ Ch,
-                                                   cpx<T>* __restrict__ Dh, int F, int K, T rho,
-                                                   int fgroups, int NV, int ni, int Kp) {
+__global__ __launch_bounds__(64 * kWbWG) void k_dsolve_wb(const cpx<T>* __restrict__ L,
+                                                          const cpx<T>* __restrict__ h,
+                                                          const cpx<T>* __restrict__ Ch,
+                                                          cpx<T>* __restrict__ Dh, int F, int K,
+                                                          T rho, int fgroups, int ntot, int NV,
+                                                          int ni, int Kp) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int blk = blockIdx.x / fgroups;
-  const int f = (blockIdx.x - blk * fgroups) * 4 + wave;
-  if (f >= F) return;
+  const int g = xcd_group(ntot);
+  const int blk = g / fgroups;
+  const int f = (g - blk * fgroups) * kWbWG + wave;
+  if (g < 0 || f >= F) return;
   const cpx<T> zero = {(T)0, (T)0};
   const cpx<T>* slot = L + ((int64_t)blk * F + f) * Kp;
   cpx<T> a[kWbMaxNi][RPL];
@@ -971,13 +988,13 @@ hipError_t launch_gram_wb(const cpx<T>* Zh, const cpx<T>* Bh, cpx<T>* L, cpx<T>*
                           int ni, T rho, int NV, hipStream_t st) {
   if (!woodbury_ok(K, ni)) return hipErrorInvalidValue;
   const int Kp = K * (K + 1) / 2;
-  const dim3 grid((unsigned)((F + 3) / 4));
+  const dim3 grid((unsigned)((((F + kWbWG - 1) / kWbWG + 7) / 8) * 8));   // whole XCD rounds
   if (K <= 64)
-    hipLaunchKernelGGL((k_gram_wb<T, 1>), grid, dim3(256), 0, st, Zh, Bh, L, h, F, K, ni, rho, NV,
-                       Kp);
+    hipLaunchKernelGGL((k_gram_wb<T, 1>), grid, dim3(64 * kWbWG), 0, st, Zh, Bh, L, h, F, K, ni,
+                       rho, NV, Kp);
   else
-    hipLaunchKernelGGL((k_gram_wb<T, 2>), grid, dim3(256), 0, st, Zh, Bh, L, h, F, K, ni, rho, NV,
-                       Kp);
+    hipLaunchKernelGGL((k_gram_wb<T, 2>), grid, dim3(64 * kWbWG), 0, st, Zh, Bh, L, h, F, K, ni,
+                       rho, NV, Kp);
   return hipGetLastError();
 }
 
@@ -985,8 +1002,9 @@ template <typename T, int RPL, int NVB>
 static void dsolve_wb_go(dim3 grid, hipStream_t st, const cpx<T>* L, const cpx<T>* h,
                          const cpx<T>* Ch, cpx<T>* Dh, int F, int K, T rho, int fgroups, int NV,
                          int ni) {
-  hipLaunchKernelGGL((k_dsolve_wb<T, RPL, NVB>), grid, dim3(256), 0, st, L, h, Ch, Dh, F, K, rho,
-                     fgroups, NV, ni, K * (K + 1) / 2);
+  const int ntot = (int)grid.y * fgroups;   // grid.y carries the block count (see launcher)
+  hipLaunchKernelGGL((k_dsolve_wb<T, RPL, NVB>), dim3(grid.x), dim3(64 * kWbWG), 0, st, L, h, Ch,
+                     Dh, F, K, rho, fgroups, ntot, NV, ni, K * (K + 1) / 2);
 }
 
 template <typename T>
@@ -994,8 +1012,9 @@ hipError_t launch_dsolve_wb(const cpx<T>* L, const cpx<T>* h, const cpx<T>* Ch, 
                             int nblocks, int F, int K, int ni, T rho, int NV, hipStream_t st) {
   if (nblocks <= 0) return hipSuccess;
   if (!woodbury_ok(K, ni)) return hipErrorInvalidValue;
-  const int fgroups = (F + 3) / 4;
-  const dim3 grid((unsigned)(nblocks * fgroups));
+  const int fgroups = (F + kWbWG - 1) / kWbWG;
+  const int n = nblocks * fgroups;
+  const dim3 grid((unsigned)(((n + 7) / 8) * 8), (unsigned)nblocks);   // whole XCD rounds
   if (K <= 64) {
     if (NV == 1) dsolve_wb_go<T, 1, 1>(grid, st, L, h, Ch, Dh, F, K, rho, fgroups, NV, ni);
     else dsolve_wb_go<T, 1, 4>(grid, st, L, h, Ch, Dh, F, K, rho, fgroups, NV, ni);

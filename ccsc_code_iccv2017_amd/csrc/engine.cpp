@@ -750,6 +750,8 @@ struct Session2D {
         HIPCHK(launch_randn<double>(z.as<double>(), (int64_t)(np * KP), p.seed,
                                     (uint64_t)(b0 * ni) * KP, st));
     }
+    // 3D / 4D: `yz` holds the z-step state a = z + y (kernels3d.hip, zstep.hip), y = 0
+    if (is4 || is3) HIPCHK(hipMemcpyAsync(yz.p, z.p, m.z, hipMemcpyDeviceToDevice, st));
     // dhat = fft2(d) of the initial filters (all blocks share d0, dP:41-42)
     fwd_embed(D.as<double>(), G.X, G.Y, Tn, 0, dhat.as<cpx<double>>(), KG);
     HIPCHK(hipStreamSynchronize(st));
@@ -895,16 +897,20 @@ struct Session2D {
     zsplit_open = false;
   }
 
-  ZTests zstep_iter(bool tol_on) {
+  // write_z: the 3D / 4D z-steps store z only for the iterations whose z is read (the last
+  // of the phase -- the D-precompute's -- the objective's, the tol test's); `yz` holds
+  // their state a = z + y (kernels3d.hip, zstep.hip)
+  ZTests zstep_iter(bool tol_on, bool write_z = true) {
     const auto* twc = tw.as<cpx<double>>();
     if (is4) {
       HIPCHK(launch_zstep_diag<double>(z.as<double>(), yz.as<double>(), E.as<cpx<double>>(),
                                        sden.as<double>(), np * K, twc, G, theta, p.rho_z,
-                                       znorm.as<double>(), tol_on, st));
+                                       znorm.as<double>(), tol_on, write_z || tol_on, st));
     } else if (is3) {
       cpx<double>* C = E.as<cpx<double>>();
       const auto* twtc = twt.as<cpx<double>>();
-      HIPCHK(launch_plane_fwd<double>(1, z.as<double>(), yz.as<double>(), nullptr, 0, 0, 0, 0,
+      // the state a = z + y lives in `yz` (modes 3, kernels3d.hip)
+      HIPCHK(launch_plane_fwd<double>(3, z.as<double>(), yz.as<double>(), nullptr, 0, 0, 0, 0,
                                       theta, 1, r, C, np * K, Tn, twc, G, st, tsolve_tc));
       if (tsolve_tc) {
         HIPCHK(launch_tsolve3<double>(C, BhatT.as<cpx<double>>(), dhatT.as<cpx<double>>(),
@@ -917,9 +923,10 @@ struct Session2D {
                                       sden.as<double>(), F, np, K, 1.0 / (double)P, st));
         HIPCHK(launch_tfft<double>(C, C, np * K, G.Y, G.F, +1, twtc, g.Gt, st));
       }
-      HIPCHK(launch_plane_inv<double>(1, C, z.as<double>(), nullptr, nullptr,
+      HIPCHK(launch_plane_inv<double>(3, C, z.as<double>(), nullptr, nullptr,
                                       tol_on ? znorm.as<double>() : nullptr, 0, 1.0, r, np * K,
-                                      Tn, twc, G, st, tsolve_tc));
+                                      Tn, twc, G, st, tsolve_tc, yz.as<double>(), theta,
+                                      write_z || tol_on));
     } else if (zl_on) {
       // register-line z-step (zline.hip): mode 0 reads (z, y) and leaves a in state order.
       // tol > 0: a launch whose starting w was solved with the current filters measures
@@ -1271,10 +1278,11 @@ struct Session2D {
     bool zbreak = false;
     for (int iz = 0; iz < p.max_it_z; ++iz) {
       ZTests zt_done;
+      const bool wz = want_oz || iz + 1 == p.max_it_z;
       if (zsplit_ok(tol_on))
-        zt_done = zstep_iter(tol_on);   // timed as one phase record by zsplit_join
+        zt_done = zstep_iter(tol_on, wz);   // timed as one phase record by zsplit_join
       else
-        timed(0, [&] { zt_done = zstep_iter(tol_on); });
+        timed(0, [&] { zt_done = zstep_iter(tol_on, wz); });
       ++nz;
       if (zt_done.lagged && z_test(iz - 1, zpart(), np) < p.tol) {   // dP:165-167 for iz - 1
         zl_rollback();

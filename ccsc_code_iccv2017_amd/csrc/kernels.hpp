@@ -38,9 +38,9 @@ hipError_t launch_objective(const T* z, const cpx<T>* dhat, const T* b, int sbx,
                             T* DZ, T* part, int64_t npatch, const cpx<T>* tw, const Grid2D& G,
                             int K, int NV, hipStream_t st);
 template <typename T>
-hipError_t launch_zstep_diag(T* z, T* yz, const cpx<T>* E, const T* sden, int64_t nslices,
+hipError_t launch_zstep_diag(T* z, T* as, const cpx<T>* E, const T* sden, int64_t nslices,
                              const cpx<T>* tw, const Grid2D& G, T theta, T rho, T* znorm,
-                             bool tol, hipStream_t st);
+                             bool tol, bool write_z, hipStream_t st);
 template <typename T>
 hipError_t launch_view_corr(const cpx<T>* dhat, const cpx<T>* Bhat, cpx<T>* E, int64_t npatch,
                             int F, int K, int NV, hipStream_t st);
@@ -175,7 +175,8 @@ hipError_t launch_tfft(const cpx<T>* src, cpx<T>* dst, int64_t nslices, int Yn, 
 template <typename T>
 hipError_t launch_plane_inv(int mode, const cpx<T>* src, T* dst, const T* yv, T* supp, T* norms,
                             int64_t nfirst, T scale, int r, int64_t nslices, int Tn,
-                            const cpx<T>* tw, const Grid2D& G, hipStream_t stream, int tc = 0);
+                            const cpx<T>* tw, const Grid2D& G, hipStream_t stream, int tc = 0,
+                            T* state = nullptr, T theta = 0, bool wz = true);
 // fused t-FFT + z-solve + inverse t-FFT over (patch, y, TC x' columns) tiles; Gt2 plans
 // the t lines of K * TC columns (make_gridt with Xh = K * TC); C, Bhat, dhat, sden in the
 // t-minor tile order of tile width TC; ppw patches per workgroup (the filter-spectrum

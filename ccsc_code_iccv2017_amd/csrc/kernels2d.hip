@@ -76,8 +76,9 @@ __global__ __launch_bounds__(kNT) void k_c2r_plain(const cpx<T>* __restrict__ sr
 // slice = jl*KG + g over the local blocks; g = k*NV + uv (KG = K*NV filter
 // slices per block: NV = 1 in 2D, the U*V views in 4D).
 // ---------------------------------------------------------------------------
-template <typename T>
-__global__ __launch_bounds__(kNT) void k_dual_r2c(const T* __restrict__ D, T* __restrict__ yD,
+template <typename T, int RM>
+__global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(slice_waves<RM>())))
+void k_dual_r2c(const T* __restrict__ D, T* __restrict__ yD,
                                                   const T* __restrict__ Usup,
                                                   cpx<T>* __restrict__ Ch,
                                                   const cpx<T>* __restrict__ twg, Grid2D G,
@@ -100,7 +101,7 @@ __global__ __launch_bounds__(kNT) void k_dual_r2c(const T* __restrict__ D, T* __
     S.slice[y * G.RS + x] = uv - yv;
   }
   zero_pad_row(S.slice, G);
-  slice_r2c<T, kMaxB>(S.slice, G, S.tw);
+  slice_r2c<T, kMaxB, RM>(S.slice, G, S.tw);
   cpx<T>* out = Ch + (int64_t)slice * G.F;
   for (int f = threadIdx.x; f < G.F; f += kNT) { const int o = bin_off(f, G); out[f] = {S.slice[o], S.slice[o + 1]}; }
 }
@@ -112,8 +113,9 @@ __global__ __launch_bounds__(kNT) void k_dual_r2c(const T* __restrict__ D, T* __
 // `nfirst` slices of the launch, or none) also accumulate ||D1 - D1_old||^2
 // and ||D1||^2 for the tol test (dP:125-131).
 // ---------------------------------------------------------------------------
-template <typename T>
-__global__ __launch_bounds__(kNT) void k_c2r_dout(const cpx<T>* __restrict__ Dh,
+template <typename T, int RM>
+__global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(slice_waves<RM>())))
+void k_c2r_dout(const cpx<T>* __restrict__ Dh,
                                                   T* __restrict__ D, const T* __restrict__ yD,
                                                   T* __restrict__ supp, T* __restrict__ dnorm,
                                                   int nfirst, const cpx<T>* __restrict__ twg,
@@ -129,7 +131,7 @@ __global__ __launch_bounds__(kNT) void k_c2r_dout(const cpx<T>* __restrict__ Dh,
     S.slice[o] = v.x;
     S.slice[o + 1] = v.y;
   }
-  slice_c2r<T, kMaxB>(S.slice, G, S.tw);
+  slice_c2r<T, kMaxB, RM>(S.slice, G, S.tw);
   const int P = G.X * G.Y;
   const int64_t off = (int64_t)slice * P;
   const bool first = slice < nfirst;
@@ -282,8 +284,12 @@ hipError_t launch_dual_r2c(const T* D, T* yD, const T* Usup, cpx<T>* Ch, int64_t
                            const cpx<T>* tw, const Grid2D& G, int K, int r, hipStream_t st) {
   if (nslices <= 0) return hipSuccess;
   const size_t sm = slice_smem_bytes(G, sizeof(T));
-  hipLaunchKernelGGL(k_dual_r2c<T>, dim3((unsigned)nslices), dim3(kNT), sm, st, D, yD, Usup,
-                     Ch, tw, G, K, r);
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3((unsigned)nslices), dim3(kNT), sm, st, D, yD, Usup, Ch, tw, G,
+                       K, r);
+  };
+  if (slice_fits(kRm74, G)) go(k_dual_r2c<T, kRm74>);   // the 74 grid (C5): 2 slices per CU
+  else go(k_dual_r2c<T, kRmAll>);
   return hipGetLastError();
 }
 
@@ -293,8 +299,12 @@ hipError_t launch_c2r_dout(const cpx<T>* Dh, T* D, const T* yD, T* supp, T* dnor
                            hipStream_t st) {
   if (nslices <= 0) return hipSuccess;
   const size_t sm = slice_smem_bytes(G, sizeof(T));
-  hipLaunchKernelGGL(k_c2r_dout<T>, dim3((unsigned)nslices), dim3(kNT), sm, st, Dh, D, yD, supp,
-                     dnorm, nfirst, tw, G, r, (T)1 / (T)(G.X * G.Y));
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3((unsigned)nslices), dim3(kNT), sm, st, Dh, D, yD, supp, dnorm,
+                       nfirst, tw, G, r, (T)1 / (T)(G.X * G.Y));
+  };
+  if (slice_fits(kRm74, G)) go(k_c2r_dout<T, kRm74>);
+  else go(k_c2r_dout<T, kRmAll>);
   return hipGetLastError();
 }
 

@@ -19,21 +19,15 @@ namespace ccsc {
 
 // ---- plane forward: prologue -> 2D R2C -> dst[(slice*T + t)*F2 + f] --------
 // mode 0: embed src sub-volume [st][sy][sx] at offset (o, o, o) (zero padding)
-// mode 1: z-step prox + dual on z, y (L3:168-172)
 // mode 2: D-step dual y += D - u, c = u - y (L3:121-123), u from the (2r+1)^3 support
+// mode 3: z-step on the state a = z + y in b (read only): u = a - clamp(a), y' = clamp(a),
+//         c = u - y' = a - 2 clamp(a); k_plane_inv mode 3 forms a' = z' + clamp(a)
 // index of bin (t, y, x') of a slice in the t-minor tile order
 __device__ __forceinline__ int64_t ttile_idx(int t, int f2, int Tn, int Xh, int tc, int ntile) {
   const int y = f2 / Xh, x = f2 - y * Xh;
   const int tile = x / tc, c = x - tile * tc;
   return ((int64_t)(y * ntile + tile) * Tn + t) * tc + c;
 }
-
-// Waves per SIMD a slice kernel of pass mask RM is compiled for: the masked 74-point
-// instantiations fit 64 VGPRs, so two 1024-thread workgroups (two planes) share a CU
-// and one's barriers and HBM waits overlap the other's passes; the all-radix build
-// needs ~95-127 VGPRs (one workgroup per CU).
-template <int RM>
-constexpr int slice_waves() { return RM == kRmAll ? 4 : 8; }
 
 template <typename T, int RM>
 __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(slice_waves<RM>())))
@@ -68,14 +62,9 @@ void k_plane_fwd(int mode, const T* __restrict__ a,
     for (int e = threadIdx.x; e < P; e += kNT) {
       const int y = e / G.X, x = e - y * G.X;
       T c;
-      if (mode == 1) {
-        const T zv = a[off + e], yv = b[off + e];
-        const T q = zv + yv;
-        const T qa = fabs(q);
-        const T uu = ((qa > theta) ? (T)1 - theta / qa : (T)0) * q;
-        const T yn = yv + zv - uu;
-        b[off + e] = yn;
-        c = uu - yn;
+      if (mode == 3) {   // the z-step (L3:168-172) on the state a = z + y
+        const T q = b[off + e];
+        c = fma((T)-2, fmax(-theta, fmin(q, theta)), q);
       } else {
         const int sxx = (x + r) % G.X, syy = (y + r) % G.Y;
         const T uv = (sxx < s && syy < s && st3 < s) ? u[(st3 * s + syy) * s + sxx] : (T)0;
@@ -128,8 +117,9 @@ void k_tfft(const cpx<T>* src, cpx<T>* dst, int Yn, int F2,
 
 // ---- plane inverse: src plane spectrum -> 2D C2R -> epilogue ----------------
 // mode 0: dst = plane * scale
-// mode 1: z-step: z = plane (1/P3 folded into the solve), tol norms vs old z
 // mode 2: D-step: D = plane * scale; support gather of D + y (L3:239-240), d-norms
+// mode 3: z-step on the state a (k_plane_fwd mode 3): a' = z' + clamp(a) into `state`,
+//         z' into dst only when wz (the iterations whose z is read), tol norms vs old z
 template <typename T, int RM>
 __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(slice_waves<RM>())))
 void k_plane_inv(int mode, const cpx<T>* __restrict__ src,
@@ -137,7 +127,7 @@ void k_plane_inv(int mode, const cpx<T>* __restrict__ src,
                                                    T* __restrict__ supp, T* __restrict__ norms,
                                                    int64_t nfirst, T scale, int r, int Tn,
                                                    const cpx<T>* __restrict__ twg, Grid2D G,
-                                                   int tc) {
+                                                   int tc, T* __restrict__ state, T theta, int wz) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   Smem<T> S = carve<T>(smem, G);
   load_twiddles(S.tw, twg, G.ntw);
@@ -155,7 +145,7 @@ void k_plane_inv(int mode, const cpx<T>* __restrict__ src,
   slice_c2r<T, kMaxB, RM>(S.slice, G, S.tw);
   const int P = G.X * G.Y;
   const int64_t off = (slice * Tn + t) * P;
-  const bool nrm = (mode == 1 && norms) || (mode == 2 && slice < nfirst);
+  const bool nrm = (mode == 3 && norms) || (mode == 2 && slice < nfirst);
   T acc_d = 0, acc_n = 0;
   for (int e = threadIdx.x; e < P; e += kNT) {
     const int y = e / G.X, x = e - y * G.X;
@@ -165,7 +155,13 @@ void k_plane_inv(int mode, const cpx<T>* __restrict__ src,
       acc_d += (v - o) * (v - o);
       acc_n += v * v;
     }
-    dst[off + e] = v;
+    if (mode == 3) {
+      const T q = state[off + e];
+      state[off + e] = v + fmax(-theta, fmin(q, theta));
+      if (wz) dst[off + e] = v;
+    } else {
+      dst[off + e] = v;
+    }
   }
   if (mode == 2) {
     const int s = 2 * r + 1;
@@ -413,11 +409,6 @@ size_t tfft_smem_bytes(const Grid2D& Gt, size_t tsize) {
   return (size_t)Gt.ntw * 2 * tsize + (size_t)Gt.Y * Gt.RS * tsize;
 }
 
-// the slice kernels' x passes run Yp/2 column-pair lines, the y passes Xh columns
-static bool slice_fits(int rm, const Grid2D& G) {
-  return rm_fits(rm, G.px, G.Yp / 2) && rm_fits(rm, G.py, G.Xh);
-}
-
 template <typename T>
 hipError_t launch_plane_fwd(int mode, const T* a, T* b, const T* usup, int sx, int sy, int st,
                             int o, T theta, int KG, int r, cpx<T>* dst, int64_t nslices, int Tn,
@@ -524,12 +515,14 @@ hipError_t launch_tsolve3(cpx<T>* C, const cpx<T>* Bhat, const cpx<T>* dhat, con
 template <typename T>
 hipError_t launch_plane_inv(int mode, const cpx<T>* src, T* dst, const T* yv, T* supp, T* norms,
                             int64_t nfirst, T scale, int r, int64_t nslices, int Tn,
-                            const cpx<T>* tw, const Grid2D& G, hipStream_t stream, int tc) {
+                            const cpx<T>* tw, const Grid2D& G, hipStream_t stream, int tc,
+                            T* state, T theta, bool wz) {
   if (nslices <= 0) return hipSuccess;
+  if (mode == 3 && (!state || (norms && !wz))) return hipErrorInvalidValue;
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3((unsigned)(nslices * Tn)), dim3(kNT),
                        slice_smem_bytes(G, sizeof(T)), stream, mode, src, dst, yv, supp, norms,
-                       nfirst, scale, r, Tn, tw, G, tc);
+                       nfirst, scale, r, Tn, tw, G, tc, state, theta, wz ? 1 : 0);
   };
   if (slice_fits(kRm74, G)) go(k_plane_inv<T, kRm74>);
   else go(k_plane_inv<T, kRmAll>);
@@ -573,7 +566,8 @@ template hipError_t launch_tfft<double>(const cpx<double>*, cpx<double>*, int64_
                                         const cpx<double>*, const Grid2D&, hipStream_t);
 template hipError_t launch_plane_inv<double>(int, const cpx<double>*, double*, const double*,
                                              double*, double*, int64_t, double, int, int64_t, int,
-                                             const cpx<double>*, const Grid2D&, hipStream_t, int);
+                                             const cpx<double>*, const Grid2D&, hipStream_t, int,
+                                             double*, double, bool);
 template hipError_t launch_tsolve3<double>(cpx<double>*, const cpx<double>*,
                                            const cpx<double>*, const double*, int64_t, int, int,
                                            int, int, double, const cpx<double>*, const Grid2D&,

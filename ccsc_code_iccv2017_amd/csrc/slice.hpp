@@ -5,6 +5,18 @@
 
 namespace ccsc {
 
+// Waves per SIMD a slice kernel of pass mask RM is compiled for: the masked 74-point
+// instantiations fit 64 VGPRs, so two 1024-thread workgroups (two slices) share a CU
+// and one's barriers and HBM waits overlap the other's passes; the all-radix build
+// needs ~95-127 VGPRs (one workgroup per CU).
+template <int RM>
+constexpr int slice_waves() { return RM == kRmAll ? 4 : 8; }
+
+// the slice kernels' x passes run Yp/2 column-pair lines, the y passes Xh columns
+__host__ inline bool slice_fits(int rm, const Grid2D& G) {
+  return rm_fits(rm, G.px, G.Yp / 2) && rm_fits(rm, G.py, G.Xh);
+}
+
 template <typename T>
 struct Smem {
   cpx<T>* tw;

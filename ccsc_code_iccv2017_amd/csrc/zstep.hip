@@ -11,15 +11,22 @@ namespace ccsc {
 // so one workgroup per (patch, filter) slice: prox + dual + R2C, scale, C2R.
 // E = sum_uv conj(d) B is precomputed once per outer iteration (k_view_corr);
 // sden = 1/((rho + s) X Y).  z stays real (Q8: the reference's imaginary part
-// is round-off).  Traffic per slice: read z, y, E; write y, z.
+// is round-off).
+// The slice state is a = z + y (the pre-threshold value, as the 2D z-step keeps it):
+// u = soft(a) = a - clamp(a), y' = a - u = clamp(a), c = u - y' = a - 2 clamp(a), and
+// after the solve a' = z' + y' = z' + clamp(a) -- a read once (re-read from L2 for the
+// last step) and written once per iteration; z' is stored only when WZ (the iteration
+// whose z the D-precompute, the objective or the tol test reads).  Traffic per slice:
+// read a, E; write a' (+ z').
 // ---------------------------------------------------------------------------
-template <typename T>
-__global__ __launch_bounds__(kNT) void k_zstep_diag(T* __restrict__ z, T* __restrict__ yz,
+template <typename T, int RM>
+__global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(slice_waves<RM>())))
+void k_zstep_diag(T* __restrict__ z, T* __restrict__ as,
                                                     const cpx<T>* __restrict__ E,
                                                     const T* __restrict__ sden,
                                                     const cpx<T>* __restrict__ twg, Grid2D G,
                                                     T theta, T rho, T* __restrict__ znorm,
-                                                    int TOL) {
+                                                    int TOL, int WZ) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   Smem<T> S = carve<T>(smem, G);
   load_twiddles(S.tw, twg, G.ntw);
@@ -27,19 +34,15 @@ __global__ __launch_bounds__(kNT) void k_zstep_diag(T* __restrict__ z, T* __rest
   const int P = G.X * G.Y;
   const int F = G.F;
   const int64_t off = slice * P;
+  theta = __builtin_canonicalize(theta);
   lds_sync();
   for (int e = threadIdx.x; e < P; e += kNT) {
     const int y = e / G.X, x = e - y * G.X;
-    const T zv = z[off + e], yv = yz[off + e];
-    const T a = zv + yv;
-    const T aa = fabs(a);
-    const T u = ((aa > theta) ? (T)1 - theta / aa : (T)0) * a;
-    const T yn = yv + zv - u;
-    yz[off + e] = yn;
-    S.slice[y * G.RS + x] = u - yn;
+    const T a = as[off + e];
+    S.slice[y * G.RS + x] = fma((T)-2, fmax(-theta, fmin(a, theta)), a);
   }
   zero_pad_row(S.slice, G);
-  slice_r2c<T, kMaxB>(S.slice, G, S.tw);
+  slice_r2c<T, kMaxB, RM>(S.slice, G, S.tw);
   const cpx<T>* Es = E + slice * F;
   for (int f = threadIdx.x; f < F; f += kNT) {
     T* q = S.slice + bin_off(f, G);
@@ -48,7 +51,7 @@ __global__ __launch_bounds__(kNT) void k_zstep_diag(T* __restrict__ z, T* __rest
     const T sc = sden[f];
     lds_cpx_store(q, 1, cpx<T>{(e.x + rho * c.x) * sc, (e.y + rho * c.y) * sc});
   }
-  slice_c2r<T, kMaxB>(S.slice, G, S.tw);
+  slice_c2r<T, kMaxB, RM>(S.slice, G, S.tw);
   T nd = 0, nz = 0;
   for (int e = threadIdx.x; e < P; e += kNT) {
     const int y = e / G.X, x = e - y * G.X;
@@ -58,7 +61,9 @@ __global__ __launch_bounds__(kNT) void k_zstep_diag(T* __restrict__ z, T* __rest
       nd += (zn - zo) * (zn - zo);
       nz += zn * zn;
     }
-    z[off + e] = zn;
+    const T a = as[off + e];
+    as[off + e] = zn + fmax(-theta, fmin(a, theta));
+    if (WZ) z[off + e] = zn;
   }
   if (TOL) {
     nd = block_sum(nd, S.red);
@@ -71,19 +76,26 @@ __global__ __launch_bounds__(kNT) void k_zstep_diag(T* __restrict__ z, T* __rest
 }
 
 template <typename T>
-hipError_t launch_zstep_diag(T* z, T* yz, const cpx<T>* E, const T* sden, int64_t nslices,
+hipError_t launch_zstep_diag(T* z, T* as, const cpx<T>* E, const T* sden, int64_t nslices,
                              const cpx<T>* tw, const Grid2D& G, T theta, T rho, T* znorm,
-                             bool tol, hipStream_t st) {
+                             bool tol, bool write_z, hipStream_t st) {
   if (nslices <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_zstep_diag<T>, dim3((unsigned)nslices), dim3(kNT),
-                     slice_smem_bytes(G, sizeof(T)), st, z, yz, E, sden, tw, G, theta, rho,
-                     znorm, tol ? 1 : 0);
+  if (tol && !write_z) return hipErrorInvalidValue;   // the test reads the z it replaces
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3((unsigned)nslices), dim3(kNT), slice_smem_bytes(G, sizeof(T)),
+                       st, z, as, E, sden, tw, G, theta, rho, znorm, tol ? 1 : 0, write_z ? 1 : 0);
+  };
+#ifndef ZS_TMP_ALL
+  if (slice_fits(kRm74, G)) go(k_zstep_diag<T, kRm74>);   // the 74 grid (C5): 2 slices per CU
+  else
+#endif
+  go(k_zstep_diag<T, kRmAll>);
   return hipGetLastError();
 }
 
 template hipError_t launch_zstep_diag<double>(double*, double*, const cpx<double>*,
                                               const double*, int64_t, const cpx<double>*,
                                               const Grid2D&, double, double, double*, bool,
-                                              hipStream_t);
+                                              bool, hipStream_t);
 
 }  // namespace ccsc

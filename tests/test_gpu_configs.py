@@ -136,7 +136,12 @@ def test_c4_fullsize_20_iterations(gpu_ctx):
     ref = np.array(_ref_norms("3D/Filters/3D_video_filters.mat")["norms"])
     print(f"C4 filter norms {norms.min():.6f} .. {norms.max():.6f} "
           f"(reference 3D {ref.min():.6f} .. {ref.max():.6f})")
-    assert np.all(np.abs(norms - 1) < 1e-2)
+    # d_res is block 1's local d-solve output D{1} (L3:141, 226-227), which leaves the
+    # sphere its projected consensus u lies on outward by the ADMM primal residual, a
+    # drift that grows over the outer iterations and with the block's data weight
+    # (test_c4_reduced_norm_offset_matches_oracle pins the same drift on the oracle at
+    # 1/9 the size: +0.016% after 20 iterations); at full C4 it measures +0.35 .. +0.40%
+    assert np.all(norms > 1.0) and np.all(norms < 1.006), (norms.min(), norms.max())
 
 
 def test_c5_fullsize_20_iterations(gpu_ctx):
@@ -186,4 +191,54 @@ def test_c3_fullsize_20_iterations(gpu_ctx):
     ref = np.array(_ref_norms("2-3D/Filters/2D-3D-Hyperspectral.mat")["norms"])
     print(f"C3 filter norms {norms.min():.6f} .. {norms.max():.6f} "
           f"(reference 2-3D {ref.min():.6f} .. {ref.max():.6f})")
-    assert np.all(np.abs(norms - 1) < 3e-2)
+    # d_res is the d-solve output d (L23:126, 231), not a projection: on this data the
+    # constraint split (rho = gamma_D ratio 5000, L23:93) holds it on the sphere to 1e-6
+    # (round 3: 1.000000 .. 1.000000); test_c3_reduced_norms_match_oracle shows the same
+    # quantity leaving the sphere (0.87 .. 1.001) where the data term dominates
+    assert np.all(np.abs(norms - 1) < 1e-4), (norms.min(), norms.max())
+
+
+def test_c4_reduced_norm_offset_matches_oracle(gpu_ctx):
+    """The norm offset of C4's d_res is the algorithm's own: on a C4-shaped problem at
+    1/9 the size (K = 49 11^3 filters, 24x24x12 synthetic clips, n = 16 -> ni = 4,
+    Woodbury), 20 outer iterations, the engine reproduces the float64 oracle's per-filter
+    norms of d_res = crop(D{1}) (tests/golden/c4_reduced_norms.json, tools/norm_offset.py:
+    1.000000 .. 1.000162, with the projected consensus u at exactly 1)."""
+    from ccsc_code_iccv2017_amd import learners as E
+    from ccsc_code_iccv2017_amd import synth
+    g = json.load(open(os.path.join(GOLD, "c4_reduced_norms.json")))
+    sb, K, n, psf, iters = tuple(g["sb"]), g["K"], g["n"], g["psf"], g["iters"]
+    b = synth.clips_3d(n, sb, K=K, psf=psf, device="cpu")
+    r = psf // 2
+    sp = [s + 2 * r for s in sb]
+    rng = np.random.default_rng(44)
+    init = {"d": rng.standard_normal((psf,) * 3 + (K,)), "z": rng.standard_normal(sp + [K, n])}
+    d_e, *_ = E.admm_learn_conv3D_large(b, [psf] * 3 + [K], 1.0, 1.0, iters, 0.0, "none", init,
+                                       ctx=gpu_ctx)
+    norms = np.sqrt((d_e ** 2).sum(axis=(0, 1, 2)))
+    print(f"C4-shaped engine norms {norms.min():.6f} .. {norms.max():.6f}")
+    np.testing.assert_allclose(norms, np.array(g["d_res_norms"]), rtol=1e-8)
+    assert norms.max() > 1.0 + 1e-4   # the outward drift, not round-off
+
+
+def test_c3_reduced_norms_match_oracle(gpu_ctx):
+    """C3's d_res is the d-solve output: on a C3-shaped problem (K = 100, W = 31, 40x40
+    uniform-noise cubes, n = 4) whose data term dominates, the oracle's d leaves the
+    sphere (0.868 .. 1.001 after the rollback at outer iteration 8,
+    tests/golden/c3_reduced_norms.json) and the engine reproduces it."""
+    from ccsc_code_iccv2017_amd import learners as E
+    g = json.load(open(os.path.join(GOLD, "c3_reduced_norms.json")))
+    sb, W, K, n, psf, iters = tuple(g["sb"]), g["W"], g["K"], g["n"], g["psf"], g["iters"]
+    rng = np.random.default_rng(5)
+    b = rng.random(sb + (W, n))
+    sm = 0.5 * rng.random(sb + (W, n))
+    r = psf // 2
+    init = {"d": rng.standard_normal((psf, psf, K)),
+            "z": rng.standard_normal((sb[0] + 2 * r, sb[1] + 2 * r, K, n))}
+    d_e, _, _, _, log = E.admm_learn(b, [psf, psf, W, K], 1.0, 1.0, iters, 0.0, "none", init, sm,
+                                     ctx=gpu_ctx, return_log=True)
+    assert log["outer"] == g["outer"] and log["rolled_back"] == g["rolled_back"]
+    norms = np.sqrt((d_e ** 2).sum(axis=(0, 1)))
+    mn, mx, me = g["d_res_norms_min_max_mean"]
+    print(f"C3-shaped engine norms {norms.min():.6f} .. {norms.max():.6f} (mean {norms.mean():.6f})")
+    np.testing.assert_allclose([norms.min(), norms.max(), norms.mean()], [mn, mx, me], rtol=1e-8)
