@@ -57,28 +57,19 @@ namespace ccsc {
 
 constexpr int kZlWL = 7;   // waves whose w bins stay in LDS (35 columns x 110 bins, 61.6 KB)
 constexpr size_t kZlWBytes = (size_t)kZlWL * 5 * zl::Y * 16;
-// Per-lane LDS address tables (uint32 byte offsets, rows of kZlTR entries), filled once per
-// workgroup: the T addresses of the slice loop depend only on the lane's line position and
-// the register index, but cost 4 - 13 integer VALU instructions each to form (mod-110
-// wraps, the Hermitian fold, the even/odd column placement) -- read from the tables they
-// cost one add (~180 VALU instructions per wave and slice less).
-//   kLutP1 [sa][n2]  row  (11 sa + 10 n2) mod 110 of T, times RS * 16   (P1 sink)
-//   kLutP3 [s][k1]   column tcol(fold(x)) * 16 of x = (xb(s) + 11 k1) mod 110, bit 0 set
-//                    when x > 55 (conjugate: the Hermitian half, P3)
-//   kLutP7 [n1][n2]  (kZlWR wv + zoff(n1 >> 1)) * 16, wv = (n1 + n2) mod 11  (P7 rows)
-constexpr int kZlTR = 12;
-constexpr int kLutP1 = 0, kLutP3 = 10 * kZlTR, kLutP7 = kLutP3 + 11 * kZlTR;
-constexpr int kLutN = kLutP7 + 10 * kZlTR;
-constexpr size_t kZlLutOff = zl::kSmem + kZlWBytes;
-constexpr size_t kZlSmem = kZlLutOff + (size_t)kLutN * 4;
+constexpr size_t kZlSmem = zl::kSmem + kZlWBytes;
 static_assert(kZlSmem <= 160 * 1024, "z-step LDS");
 
 // clamp(a, -theta, theta): the prox and the dual update of a z-iteration are
 // u = soft(a, theta) = a - clamp(a) and u - y = 2u - a = a - 2 clamp(a) (min/max + one
 // add or FMA each, no compare/select chains)
-template <typename T>
-__device__ __forceinline__ T clamp_t(T a, T theta) {
-  return fmax(-theta, fmin(a, theta));
+// theta stays in its kernel-argument SGPRs (the VOP3 min/max read it there, negated by
+// the source modifier): as a C++ fmin/fmax operand it is canonicalised into four VGPRs
+// held across the slice loop, at the VGPR cap (inputs are finite: no NaN quieting needed)
+__device__ __forceinline__ double clamp_t(double a, double theta) {
+  double r;
+  asm("v_min_f64 %0, %1, %2\n\tv_max_f64 %0, %0, -%2" : "=&v"(r) : "v"(a), "s"(theta));
+  return r;
 }
 
 template <typename T, int R, int SIGN, typename Sink>
@@ -99,14 +90,20 @@ __device__ __forceinline__ void wave_lds_fence() {
 // last wave) run on clamped indices and so duplicate a real lane exactly: their
 // LDS and global stores write the same value to the same address, no guards.
 // The outputs stream to sink(k1, value) as the last stage forms them.
-template <typename T, int ES, typename Sink>
+// ODDROT: the inputs of the lanes n1 odd arrive divided by -i (the y-R2C's two-for-one
+// separation of the odd rows, see P7): in layout B they are register n1 (compile time),
+// so the factor -i is a free swap + negate of the DFT-10's operands.
+template <typename T, int ES, bool ODDROT = false, typename Sink>
 __device__ __forceinline__ void fwd_line(cpx<T> (&v)[11], cpx<T>* E, int s, Sink&& sink) {
   const int sa = min(s, 9);
   zdft<T, 11, -1>(v, [&](int k2, cpx<T> val) { E[(sa * 11 + k2) * ES] = val; });
   wave_lds_fence();
   cpx<T> in[10];
 #pragma unroll
-  for (int n1 = 0; n1 < 10; ++n1) in[n1] = E[(n1 * 11 + s) * ES];
+  for (int n1 = 0; n1 < 10; ++n1) {
+    const cpx<T> w = E[(n1 * 11 + s) * ES];
+    in[n1] = (ODDROT && (n1 & 1)) ? cpx<T>{w.y, -w.x} : w;
+  }
   zdft<T, 10, -1>(in, sink);
 }
 
@@ -151,41 +148,6 @@ __device__ __forceinline__ cpx<T>& lds_cpx_at(uint32_t byte_off) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   return *reinterpret_cast<cpx<T>*>(smem + byte_off);
 }
-// row r (kZlTR entries, 16-B aligned) of an address table
-__device__ __forceinline__ void lut_row(int table, int r, uint32_t (&e)[kZlTR]) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  typedef unsigned int u4 __attribute__((ext_vector_type(4)));
-  const u4* q = reinterpret_cast<const u4*>(smem + kZlLutOff + (size_t)(table + r * kZlTR) * 4);
-#pragma unroll
-  for (int i = 0; i < kZlTR / 4; ++i) {
-    const u4 v = q[i];
-    e[4 * i] = v.x;
-    e[4 * i + 1] = v.y;
-    e[4 * i + 2] = v.z;
-    e[4 * i + 3] = v.w;
-  }
-}
-__device__ void fill_luts() {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  uint32_t* lut = reinterpret_cast<uint32_t*>(smem + kZlLutOff);
-  for (int q = threadIdx.x; q < kLutN; q += blockDim.x) {
-    uint32_t v = 0;
-    if (q < kLutP3) {
-      const int sa = q / kZlTR, n2 = q % kZlTR;
-      v = (uint32_t)(((11 * sa + 10 * n2) % 110) * zl::RS * 16);
-    } else if (q < kLutP7) {
-      const int s = (q - kLutP3) / kZlTR, k1 = (q - kLutP3) % kZlTR;
-      const int x = ((s ? 110 - 10 * s : 0) + 11 * k1) % 110;
-      const bool hi = x >= zl::Xh;
-      v = (uint32_t)(tcol(hi ? zl::X - x : x) * 16) | (hi ? 1u : 0u);
-    } else {
-      const int n1 = (q - kLutP7) / kZlTR, n2 = (q - kLutP7) % kZlTR;
-      v = (uint32_t)((kZlWR * ((n1 + n2) % 11) + zoff(n1 >> 1)) * 16);
-    }
-    lut[q] = v;
-  }
-}
-
 // 16-B global access at a 32-bit byte offset from a wave-uniform base (saddr form:
 // SGPR base + one VGPR offset, no 64-bit VGPR address per access).
 template <typename V>
@@ -290,7 +252,6 @@ __global__ __launch_bounds__(zl::NT) __attribute__((amdgpu_waves_per_eu(3, 3))) 
                 "zline tol variant");
   constexpr bool kStore = TOL & kZtStore, kCmp = TOL & kZtCmp, kForm = TOL & kZtForm;
   using V2 = typename vec2_t<T>::type;
-  theta = __builtin_canonicalize(theta);   // no per-use quieting in clamp_t's min/max
   extern __shared__ __attribute__((aligned(16))) char smem[];
   cpx<T>* sT = reinterpret_cast<cpx<T>*>(smem);
   const int64_t p = blockIdx.x;
@@ -316,9 +277,6 @@ __global__ __launch_bounds__(zl::NT) __attribute__((amdgpu_waves_per_eu(3, 3))) 
       for (int k1 = 0; k1 < 10; ++k1) sW[k1 * 385 + c * 11 + sb] = zld<cpx<T>>(Wp, bo + k1 * 616 * 16);
     }
   }
-
-  fill_luts();
-  __syncthreads();
 
   for (int k = 0; k < K; ++k) {
     // lane roles, recomputed per slice from an opaque thread index (see fresh())
@@ -359,21 +317,22 @@ __global__ __launch_bounds__(zl::NT) __attribute__((amdgpu_waves_per_eu(3, 3))) 
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int k1 = 0; k1 < 10; ++k1) b[k1] = cmulc(b[k1], wv[k1]);
-      uint32_t r1[kZlTR];   // T rows of the column's elements (layout A of the y-line)
-      lut_row(kLutP1, fresh(sa), r1);
-      const uint32_t cb1 = (uint32_t)tcol(c) * 16u;
-      inv_line<T, zl::RS>(b, Ey, sb, [&](int n2, cpx<T> val) { lds_cpx_at<T>(r1[n2] + cb1) = val; });
+      inv_line<T, zl::RS>(b, Ey, sb, [&](int n2, cpx<T> val) {
+        sT[mod110(11 * sa + 10 * n2) * zl::RS + tcol(c)] = val;
+      });
       zl_sync();   // P2
       if (xwave) {
         // ---- P3: x-C2R of row pair j: Z(x) = R_2j(x) + i R_2j+1(x), Hermitian ext. ----
         const int s3 = fresh(sb);
+        const int xb = s3 ? 110 - 10 * s3 : 0;   // elem_b(k2, 0)
         cpx<T> zb[10], zr[10];
-        uint32_t e3[kZlTR];   // column of x = elem_b(s3, k1) (+ 1: conjugate, x > 55)
-        lut_row(kLutP3, s3, e3);
+        uint32_t e3[10];   // byte offset of the T column of x = elem_b(s3, k1), + 1 if x > 55
         const uint32_t r0 = (uint32_t)(2 * j * zl::RS) * 16u;
         // the 20 reads first, then the rebuild (as P7: no pairwise lgkmcnt waits)
 #pragma unroll
         for (int k1 = 0; k1 < 10; ++k1) {
+          const int x = mod110(xb + 11 * k1);
+          e3[k1] = (uint32_t)(tcol(x >= zl::Xh ? zl::X - x : x) * 16) | (x >= zl::Xh ? 1u : 0u);
           const uint32_t o = r0 + (e3[k1] & ~15u);
           zb[k1] = lds_cpx_at<T>(o);
           zr[k1] = lds_cpx_at<T>(o + zl::RS * 16);
@@ -482,27 +441,25 @@ __global__ __launch_bounds__(zl::NT) __attribute__((amdgpu_waves_per_eu(3, 3))) 
     {
       const int n1 = fresh(sa);
       const uint32_t a1 = (uint32_t)zslot(c) * 16u, a2 = (uint32_t)zslot((c == 0) ? 0 : zl::X - c) * 16u;
-      // even rows: z1 + conj z2; odd rows: (z1 - conj z2) / i (row parity = n1's) -- twice
-      // the row spectra: the 1/2 is applied once to the patch's accumulated bins
-      const bool odd = n1 & 1;
-      // row y = (11 n1 + 10 n2) mod 110: pair y >> 1 is line n1 >> 1 of wave (n1 + n2) mod 11
-      uint32_t e7[kZlTR];
-      lut_row(kLutP7, n1, e7);
+      // even rows z1 + conj z2, odd rows z1 - conj z2 -- twice the row spectra (the 1/2 is
+      // applied once to the patch's accumulated bins), the odd rows' times i (the -i is
+      // applied in P9's DFT-10, where the odd rows are compile-time registers -- fwd_line
+      // ODDROT); row parity = n1's
+      const T sg = (n1 & 1) ? (T)-1 : (T)1;
       // all 22 reads first, then the arithmetic: the scheduler otherwise interleaves them
       // pairwise with a full lgkmcnt wait each (eleven LDS round trips per wave)
       cpx<T> z1[11], z2[11];
 #pragma unroll
       for (int n2 = 0; n2 < 11; ++n2) {
-        z1[n2] = lds_cpx_at<T>(e7[n2] + a1);
-        z2[n2] = lds_cpx_at<T>(e7[n2] + a2);
+        // row y = (11 n1 + 10 n2) mod 110: pair y >> 1 is line n1 >> 1 of wave (n1 + n2) mod 11
+        const uint32_t e7 = (uint32_t)((kZlWR * (n1 + n2 >= 11 ? n1 + n2 - 11 : n1 + n2) + zoff(n1 >> 1)) * 16);
+        z1[n2] = lds_cpx_at<T>(e7 + a1);
+        z2[n2] = lds_cpx_at<T>(e7 + a2);
       }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int n2 = 0; n2 < 11; ++n2) {
-        const T ex = z1[n2].x + z2[n2].x, ey = z1[n2].y - z2[n2].y;
-        const T ox = z1[n2].y + z2[n2].y, oy = z2[n2].x - z1[n2].x;
-        col[n2] = {odd ? ox : ex, odd ? oy : ey};
-      }
+      for (int n2 = 0; n2 < 11; ++n2)
+        col[n2] = {fma(sg, z2[n2].x, z1[n2].x), fma(-sg, z2[n2].y, z1[n2].y)};
     }
     zl_sync();   // P8
     // ---- P9: y-R2C of column c -> bins, accumulate sum_k dhat_k C_k ----
@@ -510,7 +467,7 @@ __global__ __launch_bounds__(zl::NT) __attribute__((amdgpu_waves_per_eu(3, 3))) 
       const int s9 = fresh(sb);
       const cpx<T>* dk = dhat + (int64_t)k * zl::F;
       const uint32_t bo = (uint32_t)(c * 11 + s9) * 16u;
-      fwd_line<T, zl::RS>(col, Ey, s9, [&](int k1, cpx<T> cb) {
+      fwd_line<T, zl::RS, true>(col, Ey, s9, [&](int k1, cpx<T> cb) {
         acc[k1] = cadd(acc[k1], cmul(fld<cpx<T>>(dk, bo, k1 * 616 * 16), cb));
       });
     }
@@ -598,7 +555,6 @@ __global__ __launch_bounds__(zl::NT) void k_zhat_line(const T* __restrict__ A,
   const cpx<T>* Wp = W + p * zl::F;
   const bool xwave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6) < 11;
   const T sc = (T)zl::P;
-  theta = __builtin_canonicalize(theta);
   for (int kk = 0; kk < KB; ++kk) {
     const int k = k0 + kk;
     if (k >= K) break;   // uniform
@@ -631,16 +587,15 @@ __global__ __launch_bounds__(zl::NT) void k_zhat_line(const T* __restrict__ A,
     {
       const int n1 = fresh(sa);
       const int zc1 = zslot(c), zc2 = zslot((c == 0) ? 0 : zl::X - c);
-      const bool odd = n1 & 1;   // twice the row spectra, halved at the store
+      // twice the row spectra (halved at the store); odd rows times i (undone in P9, ODDROT)
+      const T sg = (n1 & 1) ? (T)-1 : (T)1;
 #pragma unroll
       for (int n2 = 0; n2 < 11; ++n2) {
         // row y = (11 n1 + 10 n2) mod 110: pair y >> 1 is line n1 >> 1 of wave (n1 + n2) mod 11
         const int wv = n1 + n2 >= 11 ? n1 + n2 - 11 : n1 + n2;
         const cpx<T>* r0 = sT + kZlWR * wv + zoff(n1 >> 1);
         const cpx<T> z1 = r0[zc1], z2 = r0[zc2];
-        const T ex = z1.x + z2.x, ey = z1.y - z2.y;
-        const T ox = z1.y + z2.y, oy = z2.x - z1.x;
-        col[n2] = {odd ? ox : ex, odd ? oy : ey};
+        col[n2] = {fma(sg, z2.x, z1.x), fma(-sg, z2.y, z1.y)};
       }
     }
     lds_sync();
@@ -650,7 +605,7 @@ __global__ __launch_bounds__(zl::NT) void k_zhat_line(const T* __restrict__ A,
       const cpx<T>* dk = dcorr + (int64_t)k * zl::F;
       const uint32_t bo = (uint32_t)(c * 11 + s9) * 16u;
       cpx<T>* out = dst + (p * K + k) * (int64_t)zl::F + c;
-      fwd_line<T, zl::RS>(col, Ey, s9, [&](int k1, cpx<T> cb) {
+      fwd_line<T, zl::RS, true>(col, Ey, s9, [&](int k1, cpx<T> cb) {
         const cpx<T> q = cmulc(fld<cpx<T>>(dk, bo, k1 * 616 * 16), wld<cpx<T>>(Wp, bo, k1 * 616 * 16));
         out[zl::elem_b(s9, k1) * zl::Xh] = {fma((T)0.5, cb.x, sc * q.x), fma((T)0.5, cb.y, sc * q.y)};
       });

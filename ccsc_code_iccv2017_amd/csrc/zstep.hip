@@ -85,11 +85,8 @@ hipError_t launch_zstep_diag(T* z, T* as, const cpx<T>* E, const T* sden, int64_
     hipLaunchKernelGGL(kern, dim3((unsigned)nslices), dim3(kNT), slice_smem_bytes(G, sizeof(T)),
                        st, z, as, E, sden, tw, G, theta, rho, znorm, tol ? 1 : 0, write_z ? 1 : 0);
   };
-#ifndef ZS_TMP_ALL
   if (slice_fits(kRm74, G)) go(k_zstep_diag<T, kRm74>);   // the 74 grid (C5): 2 slices per CU
-  else
-#endif
-  go(k_zstep_diag<T, kRmAll>);
+  else go(k_zstep_diag<T, kRmAll>);
   return hipGetLastError();
 }
 
