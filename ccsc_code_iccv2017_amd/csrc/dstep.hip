@@ -983,6 +983,139 @@ __global__ __launch_bounds__(64 * kWbWG) void k_dsolve_wb(const cpx<T>* __restri
   }
 }
 
+// Many right-hand sides per f (4D: the NV = U V views share A_f, L4 precompute): one wave
+// per (block, f) with lanes over the views instead of k.  A_f and L_M are wave-uniform:
+// copied once into the wave's LDS slice (the slot is contiguous) and read as broadcasts,
+// so each lane runs t = A r, M s = t and x = (r - A^H s) / rho for its own view with no
+// cross-lane sums -- the lanes-over-k form spends 2 ni NV wave reductions per f on t.
+// r stays in registers (KR >= K rows).
+constexpr int kWbvMaxNV = 64;
+constexpr int kWbvCH = 8;   // rows of r per load chunk
+template <typename T, int KR>
+__global__ __launch_bounds__(64 * kWbWG) __attribute__((amdgpu_waves_per_eu(KR > 16 ? 2 : 4))) void k_dsolve_wbv(const cpx<T>* __restrict__ L,
+                                                           const cpx<T>* __restrict__ h,
+                                                           const cpx<T>* __restrict__ Ch,
+                                                           cpx<T>* __restrict__ Dh, int F, int K,
+                                                           T rho, int fgroups, int ntot, int NV,
+                                                           int ni, int Kp) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int g = xcd_group(ntot);
+  const int blk = g / fgroups;
+  const int f = (g - blk * fgroups) * kWbWG + wave;
+  if (g < 0 || f >= F) return;   // wave-uniform; the waves never meet at a barrier
+  const int sz = ni * K + ni * ni;   // + KR zeros: row reads past K stay finite
+  cpx<T>* sA = reinterpret_cast<cpx<T>*>(smem) + wave * (sz + KR);
+  const cpx<T>* slot = L + ((int64_t)blk * F + f) * Kp;
+  for (int i = lane; i < sz + KR; i += 64) sA[i] = i < sz ? slot[i] : cpx<T>{(T)0, (T)0};
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  const cpx<T> zero = {(T)0, (T)0};
+  // branch-free body: rows k >= K and views >= NV load a clamped valid address and are
+  // zeroed (r) or not stored; rows p >= ni of A contribute through t[p] = 0
+  const int lv = min(lane, NV - 1);
+  // wave-uniform 64-bit bases + 32-bit lane offsets (global_load saddr form: no 64-bit
+  // per-lane address per row)
+  const int64_t cs = (int64_t)NV * F;   // k stride of Ch / Dh ([blk][k][uv][F])
+  const cpx<T>* hf = h + ((int64_t)blk * F + f) * NV * K;   // [blk][f][uv][k]
+  const cpx<T>* Cb = Ch + (int64_t)blk * K * cs + f;
+  const uint32_t lh = (uint32_t)(lv * K) * sizeof(cpx<T>), lc = (uint32_t)(lv * F) * sizeof(cpx<T>);
+  auto at = [](const cpx<T>* base, uint32_t boff) -> const cpx<T>& {
+    return *reinterpret_cast<const cpx<T>*>(reinterpret_cast<const char*>(base) + boff);
+  };
+  // r = h + rho c in chunks of kWbvCH rows (sched_barrier: the compiler would otherwise
+  // hoist every load of r to the top, 8 KR registers in flight); the latency of a chunk's
+  // loads is covered by the other waves of the SIMD
+  constexpr int NCH = KR / kWbvCH;
+  cpx<T> r[KR];
+  cpx<T> t[kWbMaxNi];
+#pragma unroll
+  for (int p = 0; p < kWbMaxNi; ++p) t[p] = zero;
+  // row p of A in LDS (clamped to ni - 1; its t is discarded); columns k >= K read the
+  // next row or the zero pad, times r[k] = 0
+  int ar[kWbMaxNi];
+#pragma unroll
+  for (int p = 0; p < kWbMaxNi; ++p) ar[p] = min(p, ni - 1) * K;
+#pragma unroll
+  for (int ch = 0; ch < NCH; ++ch) {
+    cpx<T> hb[kWbvCH], cb[kWbvCH];
+#pragma unroll
+    for (int i = 0; i < kWbvCH; ++i) {
+      const int k = min(ch * kWbvCH + i, K - 1);
+      cb[i] = at(Cb + k * cs, lc);
+      hb[i] = at(hf + k, lh);
+    }
+#pragma unroll
+    for (int i = 0; i < kWbvCH; ++i) {
+      const bool ok = ch * kWbvCH + i < K;
+      r[ch * kWbvCH + i] = {ok ? fma(rho, cb[i].x, hb[i].x) : (T)0,
+                            ok ? fma(rho, cb[i].y, hb[i].y) : (T)0};
+    }
+#pragma unroll
+    for (int p = 0; p < kWbMaxNi; ++p) {
+#pragma unroll
+      for (int i = 0; i < kWbvCH; ++i) {
+        const int k = ch * kWbvCH + i;
+        const cpx<T> a = sA[ar[p] + k];
+        t[p].x = fma(a.x, r[k].x, fma(-a.y, r[k].y, t[p].x));
+        t[p].y = fma(a.x, r[k].y, fma(a.y, r[k].x, t[p].y));
+      }
+      // pin the chunk's products here (LLVM otherwise sinks them to the solve, keeping
+      // every loaded operand live)
+      asm volatile("" : "+v"(t[p].x), "+v"(t[p].y));
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  // M s = t: forward L_M y = t, backward L_M^H s = y (ni wave-uniform)
+  const cpx<T>* lm = sA + ni * K;
+  T dinv[kWbMaxNi];
+#pragma unroll
+  for (int j = 0; j < kWbMaxNi; ++j) dinv[j] = (T)1 / lm[min(j, ni - 1) * (ni + 1)].x;
+#pragma unroll
+  for (int j = 0; j < kWbMaxNi; ++j) {
+    if (j < ni) {
+      t[j] = cscale(t[j], dinv[j]);
+#pragma unroll
+      for (int q = j + 1; q < kWbMaxNi; ++q)
+        if (q < ni) t[q] = csub(t[q], cmul(lm[q * ni + j], t[j]));
+    }
+  }
+#pragma unroll
+  for (int j = kWbMaxNi - 1; j >= 0; --j) {
+    if (j < ni) {
+      t[j] = cscale(t[j], dinv[j]);
+#pragma unroll
+      for (int q = 0; q < j; ++q) t[q] = csub(t[q], cmulc(lm[j * ni + q], t[j]));   // conj(L_M[j][q])
+    }
+  }
+#pragma unroll
+  for (int p = 0; p < kWbMaxNi; ++p)
+    if (p >= ni) t[p] = zero;
+  // x = (r - A^H s) / rho; A re-read from LDS through an opaque base (kept from the t loop,
+  // 8 KR complex would not fit the registers)
+  int xo = wave * (sz + KR);
+  asm volatile("" : "+s"(xo));
+  const cpx<T>* sA2 = reinterpret_cast<const cpx<T>*>(smem) + xo;
+  const T irho = (T)1 / rho;
+  cpx<T>* Db = Dh + (int64_t)blk * K * cs + f;
+  if (lane < NV) {
+#pragma unroll
+    for (int k = 0; k < KR; ++k) {
+      if (k < K) {
+        cpx<T> x = r[k];
+#pragma unroll
+        for (int p = 0; p < kWbMaxNi; ++p) {   // x -= conj(A[p][k]) s_p
+          const cpx<T> a = sA2[ar[p] + k];
+          x.x = fma(-a.x, t[p].x, fma(-a.y, t[p].y, x.x));
+          x.y = fma(-a.x, t[p].y, fma(a.y, t[p].x, x.y));
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        *reinterpret_cast<cpx<T>*>(reinterpret_cast<char*>(Db + k * cs) + lc) = cscale(x, irho);
+      }
+    }
+  }
+}
+
 template <typename T>
 hipError_t launch_gram_wb(const cpx<T>* Zh, const cpx<T>* Bh, cpx<T>* L, cpx<T>* h, int F, int K,
                           int ni, T rho, int NV, hipStream_t st) {
@@ -1015,6 +1148,19 @@ hipError_t launch_dsolve_wb(const cpx<T>* L, const cpx<T>* h, const cpx<T>* Ch, 
   const int fgroups = (F + kWbWG - 1) / kWbWG;
   const int n = nblocks * fgroups;
   const dim3 grid((unsigned)(((n + 7) / 8) * 8), (unsigned)nblocks);   // whole XCD rounds
+  if (NV > 1 && NV <= kWbvMaxNV && K <= 64) {   // lanes over the views
+    const size_t smem = (size_t)kWbWG * (ni * K + ni * ni + 64) * sizeof(cpx<T>);
+    auto go = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3(grid.x), dim3(64 * kWbWG), smem, st, L, h, Ch, Dh, F, K, rho,
+                         fgroups, n, NV, ni, K * (K + 1) / 2);
+    };
+    if (K <= 16) go(k_dsolve_wbv<T, 16>);
+    else if (K <= 32) go(k_dsolve_wbv<T, 32>);
+    else if (K <= 48) go(k_dsolve_wbv<T, 48>);
+    else if (K <= 56) go(k_dsolve_wbv<T, 56>);
+    else go(k_dsolve_wbv<T, 64>);
+    return hipGetLastError();
+  }
   if (K <= 64) {
     if (NV == 1) dsolve_wb_go<T, 1, 1>(grid, st, L, h, Ch, Dh, F, K, rho, fgroups, NV, ni);
     else dsolve_wb_go<T, 1, 4>(grid, st, L, h, Ch, Dh, F, K, rho, fgroups, NV, ni);

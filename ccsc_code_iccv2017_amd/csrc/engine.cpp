@@ -507,6 +507,7 @@ struct Session2D {
   DevBuf twt2;
   DevBuf BhatT, dhatT, sdenT;   // B^, the filter spectrum, sden in k_tsolve3's tile order
   int tsolve_ppw = 16;          // patches per k_tsolve3 workgroup
+  bool c_ready = false;         // 3D: the z-step spectrum C already holds the next forward
 
   // host-side log
   int outer_done = 0;
@@ -900,7 +901,9 @@ struct Session2D {
   // write_z: the 3D / 4D z-steps store z only for the iterations whose z is read (the last
   // of the phase -- the D-precompute's -- the objective's, the tol test's); `yz` holds
   // their state a = z + y (kernels3d.hip, zstep.hip)
-  ZTests zstep_iter(bool tol_on, bool write_z = true) {
+  // more: another z-iteration follows directly (3D: its forward plane transform is fused
+  // into this one's inverse, c_ready)
+  ZTests zstep_iter(bool tol_on, bool write_z = true, bool more = false) {
     const auto* twc = tw.as<cpx<double>>();
     if (is4) {
       HIPCHK(launch_zstep_diag<double>(z.as<double>(), yz.as<double>(), E.as<cpx<double>>(),
@@ -910,8 +913,9 @@ struct Session2D {
       cpx<double>* C = E.as<cpx<double>>();
       const auto* twtc = twt.as<cpx<double>>();
       // the state a = z + y lives in `yz` (modes 3, kernels3d.hip)
-      HIPCHK(launch_plane_fwd<double>(3, z.as<double>(), yz.as<double>(), nullptr, 0, 0, 0, 0,
-                                      theta, 1, r, C, np * K, Tn, twc, G, st, tsolve_tc));
+      if (!c_ready)
+        HIPCHK(launch_plane_fwd<double>(3, z.as<double>(), yz.as<double>(), nullptr, 0, 0, 0, 0,
+                                        theta, 1, r, C, np * K, Tn, twc, G, st, tsolve_tc));
       if (tsolve_tc) {
         HIPCHK(launch_tsolve3<double>(C, BhatT.as<cpx<double>>(), dhatT.as<cpx<double>>(),
                                       sdenT.as<double>(), np, K, G.Y, G.Xh, tsolve_tc,
@@ -926,7 +930,8 @@ struct Session2D {
       HIPCHK(launch_plane_inv<double>(3, C, z.as<double>(), nullptr, nullptr,
                                       tol_on ? znorm.as<double>() : nullptr, 0, 1.0, r, np * K,
                                       Tn, twc, G, st, tsolve_tc, yz.as<double>(), theta,
-                                      write_z || tol_on));
+                                      write_z || tol_on, more ? C : nullptr));
+      c_ready = more;
     } else if (zl_on) {
       // register-line z-step (zline.hip): mode 0 reads (z, y) and leaves a in state order.
       // tol > 0: a launch whose starting w was solved with the current filters measures
@@ -1276,13 +1281,16 @@ struct Session2D {
     // without the lag (zl_materialize_tol)
     const bool zl_tol = zl_on && tol_on;
     bool zbreak = false;
+    c_ready = false;
     for (int iz = 0; iz < p.max_it_z; ++iz) {
       ZTests zt_done;
       const bool wz = want_oz || iz + 1 == p.max_it_z;
+      // the objective (want_oz) reuses the spectrum buffer between iterations
+      const bool more = iz + 1 < p.max_it_z && !want_oz;
       if (zsplit_ok(tol_on))
-        zt_done = zstep_iter(tol_on, wz);   // timed as one phase record by zsplit_join
+        zt_done = zstep_iter(tol_on, wz, more);   // timed as one phase record by zsplit_join
       else
-        timed(0, [&] { zt_done = zstep_iter(tol_on, wz); });
+        timed(0, [&] { zt_done = zstep_iter(tol_on, wz, more); });
       ++nz;
       if (zt_done.lagged && z_test(iz - 1, zpart(), np) < p.tol) {   // dP:165-167 for iz - 1
         zl_rollback();

@@ -176,13 +176,14 @@ template <typename T>
 hipError_t launch_plane_inv(int mode, const cpx<T>* src, T* dst, const T* yv, T* supp, T* norms,
                             int64_t nfirst, T scale, int r, int64_t nslices, int Tn,
                             const cpx<T>* tw, const Grid2D& G, hipStream_t stream, int tc = 0,
-                            T* state = nullptr, T theta = 0, bool wz = true);
+                            T* state = nullptr, T theta = 0, bool wz = true,
+                            cpx<T>* nxt = nullptr);
 // fused t-FFT + z-solve + inverse t-FFT over (patch, y, TC x' columns) tiles; Gt2 plans
 // the t lines of K * TC columns (make_gridt with Xh = K * TC); C, Bhat, dhat, sden in the
 // t-minor tile order of tile width TC; ppw patches per workgroup (the filter-spectrum
 // columns of a block stay in L2 across them)
 bool tsolve3_ok(int Tn, int K, int TC);
-size_t tsolve3_smem_bytes(const Grid2D& Gt2, int K, int TC, size_t tsize);
+size_t tsolve3_smem_bytes(const Grid2D& Gt2, int K, int TC, size_t tsize, bool dl = false);
 template <typename T>
 hipError_t launch_tsolve3(cpx<T>* C, const cpx<T>* Bhat, const cpx<T>* dhat, const T* sden,
                           int64_t npatch, int K, int Yn, int Xh, int TC, T invP3,

@@ -119,15 +119,19 @@ void k_tfft(const cpx<T>* src, cpx<T>* dst, int Yn, int F2,
 // mode 0: dst = plane * scale
 // mode 2: D-step: D = plane * scale; support gather of D + y (L3:239-240), d-norms
 // mode 3: z-step on the state a (k_plane_fwd mode 3): a' = z' + clamp(a) into `state`,
-//         z' into dst only when wz (the iterations whose z is read), tol norms vs old z
+//         z' into dst only when wz (the iterations whose z is read), tol norms vs old z;
+//         with nxt, also the next z-iteration's k_plane_fwd (c' = a' - 2 clamp(a'), plane
+//         R2C) into nxt -- the plane's own bins of src, overwritten in place -- so the
+//         state is not read back by a separate forward launch
 template <typename T, int RM>
 __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(slice_waves<RM>())))
-void k_plane_inv(int mode, const cpx<T>* __restrict__ src,
+void k_plane_inv(int mode, const cpx<T>* src,
                                                    T* __restrict__ dst, const T* __restrict__ yv,
                                                    T* __restrict__ supp, T* __restrict__ norms,
                                                    int64_t nfirst, T scale, int r, int Tn,
                                                    const cpx<T>* __restrict__ twg, Grid2D G,
-                                                   int tc, T* __restrict__ state, T theta, int wz) {
+                                                   int tc, T* __restrict__ state, T theta, int wz,
+                                                   cpx<T>* nxt) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   Smem<T> S = carve<T>(smem, G);
   load_twiddles(S.tw, twg, G.ntw);
@@ -157,8 +161,10 @@ void k_plane_inv(int mode, const cpx<T>* __restrict__ src,
     }
     if (mode == 3) {
       const T q = state[off + e];
-      state[off + e] = v + fmax(-theta, fmin(q, theta));
+      const T an = v + fmax(-theta, fmin(q, theta));
+      state[off + e] = an;
       if (wz) dst[off + e] = v;
+      if (nxt) S.slice[y * G.RS + x] = fma((T)-2, fmax(-theta, fmin(an, theta)), an);
     } else {
       dst[off + e] = v;
     }
@@ -181,6 +187,19 @@ void k_plane_inv(int mode, const cpx<T>* __restrict__ src,
     if (threadIdx.x == 0) {
       norms[2 * (slice * Tn + t)] = acc_d;
       norms[2 * (slice * Tn + t) + 1] = acc_n;
+    }
+  }
+  if (mode == 3 && nxt) {   // the next iteration's forward plane transform (k_plane_fwd mode 3)
+    zero_pad_row(S.slice, G);
+    slice_r2c<T, kMaxB, RM>(S.slice, G, S.tw);
+    if (tc > 0) {
+      const int ntile = (G.Xh + tc - 1) / tc;
+      cpx<T>* out = nxt + slice * ((int64_t)G.Y * ntile * Tn * tc);
+      for (int f = threadIdx.x; f < G.F; f += kNT)
+        out[ttile_idx(t, f, Tn, G.Xh, tc, ntile)] = lds_cpx(S.slice + bin_off(f, G), 1);
+    } else {
+      cpx<T>* out = nxt + (slice * Tn + t) * G.F;
+      for (int f = threadIdx.x; f < G.F; f += kNT) out[f] = lds_cpx(S.slice + bin_off(f, G), 1);
     }
   }
 }
@@ -218,7 +237,11 @@ __global__ void k_zsolve3(cpx<T>* __restrict__ C, const cpx<T>* __restrict__ Bha
 // block into registers (LD complex per thread) while the current one is transformed
 // (82 KB of LDS at TC = 2: one workgroup per CU, nothing else hides the HBM reads).
 // Gt2: the t plan for K*TC lines.
-template <typename T, int RM, int LD, int KMAX>
+// DL: the block's K filter-spectrum columns (and sden) are staged in LDS once per
+// workgroup -- the solve of every patch reads them there instead of from L2 (two exposed
+// global round trips per patch otherwise) -- and each patch's B^ values are loaded before
+// its forward t-FFT, consumed after it.
+template <typename T, int RM, int LD, int KMAX, bool DL>
 __global__ __launch_bounds__(kNT) void k_tsolve3(cpx<T>* __restrict__ C,
                                                  const cpx<T>* __restrict__ Bhat,
                                                  const cpx<T>* __restrict__ dhat,
@@ -260,6 +283,15 @@ __global__ __launch_bounds__(kNT) void k_tsolve3(cpx<T>* __restrict__ C,
   const int G = max(1, kNT / nb);
   const int kg = (K + G - 1) / G;
   cpx<T>* part = reinterpret_cast<cpx<T>*>(lds + 2 * (size_t)Tn * NL);   // [G][nb]
+  cpx<T>* sD = part + (size_t)G * nb;                                    // DL: [K][nb]
+  T* sS = reinterpret_cast<T*>(sD + (size_t)K * nb);                     // DL: [nb]
+  if constexpr (DL) {   // visible after the patch loop's first barrier
+    for (int i = threadIdx.x; i < K * nb; i += kNT) {
+      const int k = i / nb, bb = i - k * nb;
+      sD[i] = dhat[(int64_t)k * F3t + blk + bb];
+    }
+    for (int i = threadIdx.x; i < nb; i += kNT) sS[i] = sden[blk + i];
+  }
   {
     const cpx<T>* Cp = C + p0 * K * F3t + blk;
 #pragma unroll
@@ -289,6 +321,11 @@ __global__ __launch_bounds__(kNT) void k_tsolve3(cpx<T>* __restrict__ C,
         pre[j] = src >= 0 ? Cn[src] : cpx<T>{(T)0, (T)0};
       }
     }
+    cpx<T> bh = {(T)0, (T)0};
+    if constexpr (DL) {   // this patch's B^ in flight under the forward t-FFT
+      const int b = tid % nb, grp = tid / nb;
+      if (grp < G && b - (b / TC) * TC < nc) bh = Bhat[p * F3t + blk + b];
+    }
     fft_dir<T, kMaxB, -1, kMaxPass, kNT, 1, 1, RM>(lds, kModePlain, g, g, Gt, Gt.py, s_tw);
     // per bin (t, c): w = (B - sum_k d_k C_k) sden, C_k <- C_k / P3 + conj(d_k) w; the
     // d_k of a thread's k range stay in registers between the two sweeps, partial sums
@@ -305,7 +342,9 @@ __global__ __launch_bounds__(kNT) void k_tsolve3(cpx<T>* __restrict__ C,
 #pragma unroll
     for (int j = 0; j < KMAX; ++j) {
       const int k = grp * kg + j;
-      dv[j] = (on && j < kg && k < K) ? dhat[(int64_t)k * F3t + f3] : cpx<T>{(T)0, (T)0};
+      const bool ok = on && j < kg && k < K;
+      if constexpr (DL) dv[j] = ok ? sD[k * nb + b] : cpx<T>{(T)0, (T)0};
+      else dv[j] = ok ? dhat[(int64_t)k * F3t + f3] : cpx<T>{(T)0, (T)0};
     }
 #pragma unroll
     for (int j = 0; j < KMAX; ++j) {
@@ -317,7 +356,12 @@ __global__ __launch_bounds__(kNT) void k_tsolve3(cpx<T>* __restrict__ C,
     if (on) {
       cpx<T> tot = {(T)0, (T)0};
       for (int q = 0; q < G; ++q) tot = cadd(tot, part[q * nb + b]);
-      const cpx<T> w = cscale(csub(Bhat[p * F3t + f3], tot), sden[f3]);
+      cpx<T> w;
+      if constexpr (DL) {
+        w = cscale(csub(bh, tot), sS[b]);
+      } else {
+        w = cscale(csub(Bhat[p * F3t + f3], tot), sden[f3]);
+      }
 #pragma unroll
       for (int j = 0; j < KMAX; ++j) {
         const int k = grp * kg + j;
@@ -479,11 +523,16 @@ bool tsolve3_ok(int Tn, int K, int TC) {
   return tsolve3_kg(Tn, K, TC) <= 16 && tsolve3_ld(Tn, K, TC) <= 8;
 }
 
-size_t tsolve3_smem_bytes(const Grid2D& Gt2, int K, int TC, size_t tsize) {
+size_t tsolve3_smem_bytes(const Grid2D& Gt2, int K, int TC, size_t tsize, bool dl) {
   const int nb = Gt2.Y * TC;
   const int G = std::max(1, kNT / nb);
   return (size_t)Gt2.ntw * 2 * tsize + (size_t)Gt2.Y * K * TC * 2 * tsize +
-         (size_t)G * nb * 2 * tsize;   // + the solve's partial sums
+         (size_t)G * nb * 2 * tsize +                        // + the solve's partial sums
+         (dl ? (size_t)K * nb * 2 * tsize + (size_t)nb * tsize : 0);   // + dhat, sden (DL)
+}
+// the fused t-solve's LDS with the filter block staged (DL) when it fits one CU
+static bool tsolve3_dl(const Grid2D& Gt2, int K, int TC, size_t tsize) {
+  return tsolve3_smem_bytes(Gt2, K, TC, tsize, true) <= 160 * 1024;
 }
 
 template <typename T>
@@ -498,17 +547,21 @@ hipError_t launch_tsolve3(cpx<T>* C, const cpx<T>* Bhat, const cpx<T>* dhat, con
   ppw = std::max(1, std::min<int>(ppw, (int)npatch));
   const int64_t pgroups = (npatch + ppw - 1) / ppw;
   const dim3 grid((unsigned)(pgroups * Yn * xtiles));
-  const size_t smem = tsolve3_smem_bytes(Gt2, K, TC, sizeof(T));
+  const bool dl = tsolve3_dl(Gt2, K, TC, sizeof(T));
+  const size_t smem = tsolve3_smem_bytes(Gt2, K, TC, sizeof(T), dl);
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, grid, dim3(kNT), smem, stream, C, Bhat, dhat, sden, K, Yn, Xh, TC,
                        xtiles, invP3, tw, Gt2, npatch, ppw);
   };
   const bool r42 = rm_fits(kRm42, Gt2.py, Gt2.Xh);
   const bool small = tsolve3_ld(Gt2.Y, K, TC) <= 5 && tsolve3_kg(Gt2.Y, K, TC) <= 8;
-  if (r42 && small) go(k_tsolve3<T, kRm42, 5, 8>);
-  else if (r42) go(k_tsolve3<T, kRm42, 8, 16>);
-  else if (small) go(k_tsolve3<T, kRmAll, 5, 8>);
-  else go(k_tsolve3<T, kRmAll, 8, 16>);
+  if (r42 && small && dl) go(k_tsolve3<T, kRm42, 5, 8, true>);   // C4
+  else if (r42 && small) go(k_tsolve3<T, kRm42, 5, 8, false>);
+  else if (r42) go(k_tsolve3<T, kRm42, 8, 16, false>);
+  else if (small && dl) go(k_tsolve3<T, kRmAll, 5, 8, true>);
+  else if (small) go(k_tsolve3<T, kRmAll, 5, 8, false>);
+  else if (dl) go(k_tsolve3<T, kRmAll, 8, 16, true>);
+  else go(k_tsolve3<T, kRmAll, 8, 16, false>);
   return hipGetLastError();
 }
 
@@ -516,13 +569,14 @@ template <typename T>
 hipError_t launch_plane_inv(int mode, const cpx<T>* src, T* dst, const T* yv, T* supp, T* norms,
                             int64_t nfirst, T scale, int r, int64_t nslices, int Tn,
                             const cpx<T>* tw, const Grid2D& G, hipStream_t stream, int tc,
-                            T* state, T theta, bool wz) {
+                            T* state, T theta, bool wz, cpx<T>* nxt) {
   if (nslices <= 0) return hipSuccess;
   if (mode == 3 && (!state || (norms && !wz))) return hipErrorInvalidValue;
+  if (nxt && (mode != 3 || nxt != src)) return hipErrorInvalidValue;
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3((unsigned)(nslices * Tn)), dim3(kNT),
                        slice_smem_bytes(G, sizeof(T)), stream, mode, src, dst, yv, supp, norms,
-                       nfirst, scale, r, Tn, tw, G, tc, state, theta, wz ? 1 : 0);
+                       nfirst, scale, r, Tn, tw, G, tc, state, theta, wz ? 1 : 0, nxt);
   };
   if (slice_fits(kRm74, G)) go(k_plane_inv<T, kRm74>);
   else go(k_plane_inv<T, kRmAll>);
@@ -567,7 +621,7 @@ template hipError_t launch_tfft<double>(const cpx<double>*, cpx<double>*, int64_
 template hipError_t launch_plane_inv<double>(int, const cpx<double>*, double*, const double*,
                                              double*, double*, int64_t, double, int, int64_t, int,
                                              const cpx<double>*, const Grid2D&, hipStream_t, int,
-                                             double*, double, bool);
+                                             double*, double, bool, cpx<double>*);
 template hipError_t launch_tsolve3<double>(cpx<double>*, const cpx<double>*,
                                            const cpx<double>*, const double*, int64_t, int, int,
                                            int, int, double, const cpx<double>*, const Grid2D&,
