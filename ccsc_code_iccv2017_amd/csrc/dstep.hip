@@ -987,47 +987,66 @@ __global__ __launch_bounds__(64 * kWbWG) void k_dsolve_wb(const cpx<T>* __restri
 // per (block, f) with lanes over the views instead of k.  A_f and L_M are wave-uniform:
 // copied once into the wave's LDS slice (the slot is contiguous) and read as broadcasts,
 // so each lane runs t = A r, M s = t and x = (r - A^H s) / rho for its own view with no
-// cross-lane sums -- the lanes-over-k form spends 2 ni NV wave reductions per f on t.
-// r stays in registers (KR >= K rows).
+// wave reductions -- the lanes-over-k form spends 2 ni NV of them per f on t.  With
+// NV <= 32 the two half-waves take the two halves of the k range (H = 2: lane = 32 hh + v,
+// rows hh KH .. hh KH + KH - 1, KH = ceil(K / 2)): half the rows of r per lane, and the
+// half sums of t meet through v_permlane32_swap.  r stays in registers (KR >= KH rows).
 constexpr int kWbvMaxNV = 64;
 constexpr int kWbvCH = 8;   // rows of r per load chunk
-template <typename T, int KR>
-__global__ __launch_bounds__(64 * kWbWG) __attribute__((amdgpu_waves_per_eu(KR > 16 ? 2 : 4))) void k_dsolve_wbv(const cpx<T>* __restrict__ L,
+constexpr int kWbvPad = 64;   // zero complex past a wave's slot in LDS (row reads past K)
+__device__ __forceinline__ double half_swap_sum(double v) {
+  // v(lanes l mod 32) + v(lanes 32 + l mod 32) in every lane, the same order in both halves
+  const auto lo = __builtin_amdgcn_permlane32_swap(__double2loint(v), __double2loint(v), false, false);
+  const auto hi = __builtin_amdgcn_permlane32_swap(__double2hiint(v), __double2hiint(v), false, false);
+  return __hiloint2double(hi[0], lo[0]) + __hiloint2double(hi[1], lo[1]);
+}
+template <typename T, int KR, int H>
+__global__ __launch_bounds__(64 * kWbWG) __attribute__((amdgpu_waves_per_eu(KR <= 8 ? 4 : 2))) void k_dsolve_wbv(const cpx<T>* __restrict__ L,
                                                            const cpx<T>* __restrict__ h,
                                                            const cpx<T>* __restrict__ Ch,
                                                            cpx<T>* __restrict__ Dh, int F, int K,
                                                            T rho, int fgroups, int ntot, int NV,
                                                            int ni, int Kp) {
+  static_assert(H == 1 || H == 2, "row segments");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int g = xcd_group(ntot);
   const int blk = g / fgroups;
   const int f = (g - blk * fgroups) * kWbWG + wave;
   if (g < 0 || f >= F) return;   // wave-uniform; the waves never meet at a barrier
-  const int sz = ni * K + ni * ni;   // + KR zeros: row reads past K stay finite
-  cpx<T>* sA = reinterpret_cast<cpx<T>*>(smem) + wave * (sz + KR);
+  const int sz = ni * K + ni * ni;   // + kWbvPad zeros: row reads past K stay finite
+  cpx<T>* sA = reinterpret_cast<cpx<T>*>(smem) + wave * (sz + kWbvPad);
   const cpx<T>* slot = L + ((int64_t)blk * F + f) * Kp;
-  for (int i = lane; i < sz + KR; i += 64) sA[i] = i < sz ? slot[i] : cpx<T>{(T)0, (T)0};
+  for (int i = lane; i < sz + kWbvPad; i += 64) sA[i] = i < sz ? slot[i] : cpx<T>{(T)0, (T)0};
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   const cpx<T> zero = {(T)0, (T)0};
+  constexpr int VL = 64 / H;   // view lanes per row segment
+  const int v = lane & (VL - 1), hh = H == 1 ? 0 : lane / VL;
+  const int KH = (K + H - 1) / H;
+  const int k0 = hh * KH;   // the lane's first row
   // branch-free body: rows k >= K and views >= NV load a clamped valid address and are
   // zeroed (r) or not stored; rows p >= ni of A contribute through t[p] = 0
-  const int lv = min(lane, NV - 1);
+  const int lv = min(v, NV - 1);
   // wave-uniform 64-bit bases + 32-bit lane offsets (global_load saddr form: no 64-bit
-  // per-lane address per row)
+  // per-lane address per row; the host keeps a block's K NV F spectra under 4 GB)
   const int64_t cs = (int64_t)NV * F;   // k stride of Ch / Dh ([blk][k][uv][F])
   const cpx<T>* hf = h + ((int64_t)blk * F + f) * NV * K;   // [blk][f][uv][k]
   const cpx<T>* Cb = Ch + (int64_t)blk * K * cs + f;
-  const uint32_t lh = (uint32_t)(lv * K) * sizeof(cpx<T>), lc = (uint32_t)(lv * F) * sizeof(cpx<T>);
   auto at = [](const cpx<T>* base, uint32_t boff) -> const cpx<T>& {
     return *reinterpret_cast<const cpx<T>*>(reinterpret_cast<const char*>(base) + boff);
   };
+  // lane offsets of row i of the lane's segment: hf + i, Cb + i cs (segment start folded in)
+  auto offh = [&](int i) {
+    return (uint32_t)(lv * K + min(k0 + i, K - 1) - i) * (uint32_t)sizeof(cpx<T>);
+  };
+  auto offc = [&](int i) {
+    return (uint32_t)(lv * F + (min(k0 + i, K - 1) - i) * cs) * (uint32_t)sizeof(cpx<T>);
+  };
   // r = h + rho c in chunks of kWbvCH rows (sched_barrier: the compiler would otherwise
-  // hoist every load of r to the top, 8 KR registers in flight); the latency of a chunk's
-  // loads is covered by the other waves of the SIMD
-  constexpr int NCH = KR / kWbvCH;
-  cpx<T> r[KR];
+  // hoist every load of r to the top, 8 KR registers in flight)
+  constexpr int NCH = (KR + kWbvCH - 1) / kWbvCH;
+  cpx<T> r[NCH * kWbvCH];
   cpx<T> t[kWbMaxNi];
 #pragma unroll
   for (int p = 0; p < kWbMaxNi; ++p) t[p] = zero;
@@ -1035,36 +1054,47 @@ __global__ __launch_bounds__(64 * kWbWG) __attribute__((amdgpu_waves_per_eu(KR >
   // next row or the zero pad, times r[k] = 0
   int ar[kWbMaxNi];
 #pragma unroll
-  for (int p = 0; p < kWbMaxNi; ++p) ar[p] = min(p, ni - 1) * K;
+  for (int p = 0; p < kWbMaxNi; ++p) ar[p] = min(p, ni - 1) * K + k0;
+  // chunk ch + 1's loads are issued before chunk ch's products (double buffer)
+  cpx<T> hb[kWbvCH], cb[kWbvCH];
+  auto load = [&](int ch) {
+#pragma unroll
+    for (int i = 0; i < kWbvCH; ++i) {
+      const int ii = ch * kWbvCH + i;
+      cb[i] = at(Cb + ii * cs, offc(ii));
+      hb[i] = at(hf + ii, offh(ii));
+    }
+  };
+  load(0);
 #pragma unroll
   for (int ch = 0; ch < NCH; ++ch) {
-    cpx<T> hb[kWbvCH], cb[kWbvCH];
 #pragma unroll
     for (int i = 0; i < kWbvCH; ++i) {
-      const int k = min(ch * kWbvCH + i, K - 1);
-      cb[i] = at(Cb + k * cs, lc);
-      hb[i] = at(hf + k, lh);
+      const int ii = ch * kWbvCH + i;
+      const bool ok = ii < KH && k0 + ii < K;
+      r[ii] = {ok ? fma(rho, cb[i].x, hb[i].x) : (T)0, ok ? fma(rho, cb[i].y, hb[i].y) : (T)0};
+      asm volatile("" : "+v"(r[ii].x), "+v"(r[ii].y));
     }
-#pragma unroll
-    for (int i = 0; i < kWbvCH; ++i) {
-      const bool ok = ch * kWbvCH + i < K;
-      r[ch * kWbvCH + i] = {ok ? fma(rho, cb[i].x, hb[i].x) : (T)0,
-                            ok ? fma(rho, cb[i].y, hb[i].y) : (T)0};
-    }
+    if (ch + 1 < NCH) load(ch + 1);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int p = 0; p < kWbMaxNi; ++p) {
 #pragma unroll
       for (int i = 0; i < kWbvCH; ++i) {
-        const int k = ch * kWbvCH + i;
-        const cpx<T> a = sA[ar[p] + k];
-        t[p].x = fma(a.x, r[k].x, fma(-a.y, r[k].y, t[p].x));
-        t[p].y = fma(a.x, r[k].y, fma(a.y, r[k].x, t[p].y));
+        const int ii = ch * kWbvCH + i;
+        const cpx<T> a = sA[ar[p] + ii];
+        t[p].x = fma(a.x, r[ii].x, fma(-a.y, r[ii].y, t[p].x));
+        t[p].y = fma(a.x, r[ii].y, fma(a.y, r[ii].x, t[p].y));
       }
       // pin the chunk's products here (LLVM otherwise sinks them to the solve, keeping
       // every loaded operand live)
       asm volatile("" : "+v"(t[p].x), "+v"(t[p].y));
       __builtin_amdgcn_sched_barrier(0);
     }
+  }
+  if constexpr (H == 2) {
+#pragma unroll
+    for (int p = 0; p < kWbMaxNi; ++p) t[p] = {half_swap_sum(t[p].x), half_swap_sum(t[p].y)};
   }
   // M s = t: forward L_M y = t, backward L_M^H s = y (ni wave-uniform)
   const cpx<T>* lm = sA + ni * K;
@@ -1093,24 +1123,24 @@ __global__ __launch_bounds__(64 * kWbWG) __attribute__((amdgpu_waves_per_eu(KR >
     if (p >= ni) t[p] = zero;
   // x = (r - A^H s) / rho; A re-read from LDS through an opaque base (kept from the t loop,
   // 8 KR complex would not fit the registers)
-  int xo = wave * (sz + KR);
+  int xo = wave * (sz + kWbvPad);
   asm volatile("" : "+s"(xo));
   const cpx<T>* sA2 = reinterpret_cast<const cpx<T>*>(smem) + xo;
   const T irho = (T)1 / rho;
   cpx<T>* Db = Dh + (int64_t)blk * K * cs + f;
-  if (lane < NV) {
+  if (v < NV) {
 #pragma unroll
-    for (int k = 0; k < KR; ++k) {
-      if (k < K) {
-        cpx<T> x = r[k];
+    for (int ii = 0; ii < KR; ++ii) {
+      if (ii < KH && k0 + ii < K) {
+        cpx<T> x = r[ii];
 #pragma unroll
         for (int p = 0; p < kWbMaxNi; ++p) {   // x -= conj(A[p][k]) s_p
-          const cpx<T> a = sA2[ar[p] + k];
+          const cpx<T> a = sA2[ar[p] + ii];
           x.x = fma(-a.x, t[p].x, fma(-a.y, t[p].y, x.x));
           x.y = fma(-a.x, t[p].y, fma(a.y, t[p].x, x.y));
         }
         __builtin_amdgcn_sched_barrier(0);
-        *reinterpret_cast<cpx<T>*>(reinterpret_cast<char*>(Db + k * cs) + lc) = cscale(x, irho);
+        *reinterpret_cast<cpx<T>*>(reinterpret_cast<char*>(Db + ii * cs) + offc(ii)) = cscale(x, irho);
       }
     }
   }
@@ -1148,17 +1178,27 @@ hipError_t launch_dsolve_wb(const cpx<T>* L, const cpx<T>* h, const cpx<T>* Ch, 
   const int fgroups = (F + kWbWG - 1) / kWbWG;
   const int n = nblocks * fgroups;
   const dim3 grid((unsigned)(((n + 7) / 8) * 8), (unsigned)nblocks);   // whole XCD rounds
-  if (NV > 1 && NV <= kWbvMaxNV && K <= 64) {   // lanes over the views
-    const size_t smem = (size_t)kWbWG * (ni * K + ni * ni + 64) * sizeof(cpx<T>);
+  if (NV > 1 && NV <= kWbvMaxNV && K <= 64 &&
+      (int64_t)K * NV * F * (int64_t)sizeof(cpx<T>) < ((int64_t)1 << 32)) {   // lanes over the views
+    const size_t smem = (size_t)kWbWG * (ni * K + ni * ni + kWbvPad) * sizeof(cpx<T>);
     auto go = [&](auto kern) {
       hipLaunchKernelGGL(kern, dim3(grid.x), dim3(64 * kWbWG), smem, st, L, h, Ch, Dh, F, K, rho,
                          fgroups, n, NV, ni, K * (K + 1) / 2);
     };
-    if (K <= 16) go(k_dsolve_wbv<T, 16>);
-    else if (K <= 32) go(k_dsolve_wbv<T, 32>);
-    else if (K <= 48) go(k_dsolve_wbv<T, 48>);
-    else if (K <= 56) go(k_dsolve_wbv<T, 56>);
-    else go(k_dsolve_wbv<T, 64>);
+    if (NV <= 32) {   // two row segments of KH = ceil(K / 2) <= 32
+      const int kh = (K + 1) / 2;
+      if (kh <= 8) go(k_dsolve_wbv<T, 8, 2>);
+      else if (kh <= 16) go(k_dsolve_wbv<T, 16, 2>);
+      else if (kh <= 24) go(k_dsolve_wbv<T, 24, 2>);
+      else if (kh <= 28) go(k_dsolve_wbv<T, 28, 2>);
+      else go(k_dsolve_wbv<T, 32, 2>);
+    } else {
+      if (K <= 16) go(k_dsolve_wbv<T, 16, 1>);
+      else if (K <= 32) go(k_dsolve_wbv<T, 32, 1>);
+      else if (K <= 48) go(k_dsolve_wbv<T, 48, 1>);
+      else if (K <= 56) go(k_dsolve_wbv<T, 56, 1>);
+      else go(k_dsolve_wbv<T, 64, 1>);
+    }
     return hipGetLastError();
   }
   if (K <= 64) {

@@ -85,25 +85,28 @@ void k_dual_r2c(const T* __restrict__ D, T* __restrict__ yD,
                                                   int K, int r) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   Smem<T> S = carve<T>(smem, G);
-  load_twiddles(S.tw, twg, G.ntw);
+  using Q = SG<RM>;
+  const int GX = Q::X(G), GY = Q::Y(G), RS = Q::RS(G), GF = Q::F(G);
+  if constexpr (!Q::fixed) load_twiddles(S.tw, twg, G.ntw);
   const int slice = blockIdx.x;
   const int g = slice % K;   // K here = KG filter slices per block
   const int s = 2 * r + 1;
-  const int P = G.X * G.Y;
+  const int P = GX * GY;
   const int64_t off = (int64_t)slice * P;
   const T* u = Usup + (int64_t)g * s * s;
   for (int e = threadIdx.x; e < P; e += kNT) {
-    const int y = e / G.X, x = e - y * G.X;
-    const int sxx = (x + r) % G.X, syy = (y + r) % G.Y;
+    const int y = e / GX, x = e - y * GX;
+    const int xr = x + r, yr = y + r;
+    const int sxx = xr >= GX ? xr - GX : xr, syy = yr >= GY ? yr - GY : yr;   // (x + r) mod X
     const T uv = (sxx < s && syy < s) ? u[syy * s + sxx] : (T)0;
     const T yv = yD[off + e] + D[off + e] - uv;
     yD[off + e] = yv;
-    S.slice[y * G.RS + x] = uv - yv;
+    S.slice[y * RS + x] = uv - yv;
   }
   zero_pad_row(S.slice, G);
-  slice_r2c<T, kMaxB, RM>(S.slice, G, S.tw);
-  cpx<T>* out = Ch + (int64_t)slice * G.F;
-  for (int f = threadIdx.x; f < G.F; f += kNT) { const int o = bin_off(f, G); out[f] = {S.slice[o], S.slice[o + 1]}; }
+  slice_r2c_rm<T, RM>(S.slice, G, S.tw);
+  cpx<T>* out = Ch + (int64_t)slice * GF;
+  for (int f = threadIdx.x; f < GF; f += kNT) { const int o = Q::bin(f, G); out[f] = {S.slice[o], S.slice[o + 1]}; }
 }
 
 // ---------------------------------------------------------------------------
@@ -122,23 +125,25 @@ void k_c2r_dout(const cpx<T>* __restrict__ Dh,
                                                   Grid2D G, int r, T invP) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   Smem<T> S = carve<T>(smem, G);
-  load_twiddles(S.tw, twg, G.ntw);
+  using Q = SG<RM>;
+  const int GX = Q::X(G), GY = Q::Y(G), RS = Q::RS(G), GF = Q::F(G);
+  if constexpr (!Q::fixed) load_twiddles(S.tw, twg, G.ntw);
   const int slice = blockIdx.x;
-  const cpx<T>* in = Dh + (int64_t)slice * G.F;
-  for (int f = threadIdx.x; f < G.F; f += kNT) {
+  const cpx<T>* in = Dh + (int64_t)slice * GF;
+  for (int f = threadIdx.x; f < GF; f += kNT) {
     const cpx<T> v = in[f];
-    const int o = bin_off(f, G);
+    const int o = Q::bin(f, G);
     S.slice[o] = v.x;
     S.slice[o + 1] = v.y;
   }
-  slice_c2r<T, kMaxB, RM>(S.slice, G, S.tw);
-  const int P = G.X * G.Y;
+  slice_c2r_rm<T, RM>(S.slice, G, S.tw);
+  const int P = GX * GY;
   const int64_t off = (int64_t)slice * P;
   const bool first = slice < nfirst;
   T acc_d = 0, acc_n = 0;
   for (int e = threadIdx.x; e < P; e += kNT) {
-    const int y = e / G.X, x = e - y * G.X;
-    const T v = S.slice[y * G.RS + x] * invP;
+    const int y = e / GX, x = e - y * GX;
+    const T v = S.slice[y * RS + x] * invP;
     if (first) {
       const T o = D[off + e];
       acc_d += (v - o) * (v - o);
@@ -150,8 +155,8 @@ void k_c2r_dout(const cpx<T>* __restrict__ Dh,
   T* sp = supp + (int64_t)slice * s * s;
   for (int q = threadIdx.x; q < s * s; q += kNT) {
     const int sy = q / s, sx = q - sy * s;
-    const int x = (sx - r + G.X) % G.X, y = (sy - r + G.Y) % G.Y;
-    sp[q] = S.slice[y * G.RS + x] * invP + yD[off + y * G.X + x];
+    const int x = (sx - r + GX) % GX, y = (sy - r + GY) % GY;
+    sp[q] = S.slice[y * RS + x] * invP + yD[off + y * GX + x];
   }
   if (first) {
     acc_d = block_sum(acc_d, S.red);
@@ -288,7 +293,8 @@ hipError_t launch_dual_r2c(const T* D, T* yD, const T* Usup, cpx<T>* Ch, int64_t
     hipLaunchKernelGGL(kern, dim3((unsigned)nslices), dim3(kNT), sm, st, D, yD, Usup, Ch, tw, G,
                        K, r);
   };
-  if (slice_fits(kRm74, G)) go(k_dual_r2c<T, kRm74>);   // the 74 grid (C5): 2 slices per CU
+  if (grid_is74(G)) go(k_dual_r2c<T, kRm74F>);   // the 74 grid (C5): 2 slices per CU
+  else if (slice_fits(kRm74, G)) go(k_dual_r2c<T, kRm74>);
   else go(k_dual_r2c<T, kRmAll>);
   return hipGetLastError();
 }
@@ -303,7 +309,8 @@ hipError_t launch_c2r_dout(const cpx<T>* Dh, T* D, const T* yD, T* supp, T* dnor
     hipLaunchKernelGGL(kern, dim3((unsigned)nslices), dim3(kNT), sm, st, Dh, D, yD, supp, dnorm,
                        nfirst, tw, G, r, (T)1 / (T)(G.X * G.Y));
   };
-  if (slice_fits(kRm74, G)) go(k_c2r_dout<T, kRm74>);
+  if (grid_is74(G)) go(k_c2r_dout<T, kRm74F>);
+  else if (slice_fits(kRm74, G)) go(k_c2r_dout<T, kRm74>);
   else go(k_c2r_dout<T, kRmAll>);
   return hipGetLastError();
 }

@@ -39,20 +39,22 @@ void k_plane_fwd(int mode, const T* __restrict__ a,
                                                    Grid2D G, int tc) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   Smem<T> S = carve<T>(smem, G);
-  load_twiddles(S.tw, twg, G.ntw);
+  using Q = SG<RM>;
+  const int GX = Q::X(G), GY = Q::Y(G), RS = Q::RS(G), GF = Q::F(G), GXh = Q::Xh(G);
+  if constexpr (!Q::fixed) load_twiddles(S.tw, twg, G.ntw);
   const int64_t slice = blockIdx.x / Tn;
   const int t = blockIdx.x - (int)(slice * Tn);
-  const int P = G.X * G.Y;
+  const int P = GX * GY;
   const int s = 2 * r + 1;
   if (mode == 0) {
-    for (int e = threadIdx.x; e < G.Yp * G.RS; e += kNT) S.slice[e] = (T)0;
+    for (int e = threadIdx.x; e < Q::Yp(G) * RS; e += kNT) S.slice[e] = (T)0;
     lds_sync();
     const int tt = t - o;
     if (tt >= 0 && tt < st) {
       const T* in = a + ((int64_t)slice * st + tt) * sx * sy;
       for (int e = threadIdx.x; e < sx * sy; e += kNT) {
         const int y = e / sx, x = e - y * sx;
-        S.slice[(y + o) * G.RS + x + o] = in[e];
+        S.slice[(y + o) * RS + x + o] = in[e];
       }
     }
   } else {
@@ -60,32 +62,32 @@ void k_plane_fwd(int mode, const T* __restrict__ a,
     const int st3 = (t + r) % Tn;
     const T* u = usup + (int64_t)(slice % KG) * s * s * s;
     for (int e = threadIdx.x; e < P; e += kNT) {
-      const int y = e / G.X, x = e - y * G.X;
+      const int y = e / GX, x = e - y * GX;
       T c;
       if (mode == 3) {   // the z-step (L3:168-172) on the state a = z + y
         const T q = b[off + e];
         c = fma((T)-2, fmax(-theta, fmin(q, theta)), q);
       } else {
-        const int sxx = (x + r) % G.X, syy = (y + r) % G.Y;
+        const int sxx = (x + r) % GX, syy = (y + r) % GY;
         const T uv = (sxx < s && syy < s && st3 < s) ? u[(st3 * s + syy) * s + sxx] : (T)0;
         const T yn = b[off + e] + a[off + e] - uv;
         b[off + e] = yn;
         c = uv - yn;
       }
-      S.slice[y * G.RS + x] = c;
+      S.slice[y * RS + x] = c;
     }
     zero_pad_row(S.slice, G);
   }
-  slice_r2c<T, kMaxB, RM>(S.slice, G, S.tw);
+  slice_r2c_rm<T, RM>(S.slice, G, S.tw);
   if (tc > 0) {   // t-minor tiles (k_tsolve3's order)
-    const int ntile = (G.Xh + tc - 1) / tc;
-    cpx<T>* out = dst + slice * ((int64_t)G.Y * ntile * Tn * tc);
-    for (int f = threadIdx.x; f < G.F; f += kNT)
-      out[ttile_idx(t, f, Tn, G.Xh, tc, ntile)] = lds_cpx(S.slice + bin_off(f, G), 1);
+    const int ntile = (GXh + tc - 1) / tc;
+    cpx<T>* out = dst + slice * ((int64_t)GY * ntile * Tn * tc);
+    for (int f = threadIdx.x; f < GF; f += kNT)
+      out[ttile_idx(t, f, Tn, GXh, tc, ntile)] = lds_cpx(S.slice + Q::bin(f, G), 1);
     return;
   }
-  cpx<T>* out = dst + (slice * Tn + t) * G.F;
-  for (int f = threadIdx.x; f < G.F; f += kNT) out[f] = lds_cpx(S.slice + bin_off(f, G), 1);
+  cpx<T>* out = dst + (slice * Tn + t) * GF;
+  for (int f = threadIdx.x; f < GF; f += kNT) out[f] = lds_cpx(S.slice + Q::bin(f, G), 1);
 }
 
 // ---- t-direction complex FFT (src may equal dst); one workgroup per (slice, y)
@@ -134,26 +136,28 @@ void k_plane_inv(int mode, const cpx<T>* src,
                                                    cpx<T>* nxt) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   Smem<T> S = carve<T>(smem, G);
-  load_twiddles(S.tw, twg, G.ntw);
+  using Q = SG<RM>;
+  const int GX = Q::X(G), GY = Q::Y(G), RS = Q::RS(G), GF = Q::F(G), GXh = Q::Xh(G);
+  if constexpr (!Q::fixed) load_twiddles(S.tw, twg, G.ntw);
   const int64_t slice = blockIdx.x / Tn;
   const int t = blockIdx.x - (int)(slice * Tn);
   if (tc > 0) {   // t-minor tiles (k_tsolve3's order)
-    const int ntile = (G.Xh + tc - 1) / tc;
-    const cpx<T>* in = src + slice * ((int64_t)G.Y * ntile * Tn * tc);
-    for (int f = threadIdx.x; f < G.F; f += kNT)
-      lds_cpx_store(S.slice + bin_off(f, G), 1, in[ttile_idx(t, f, Tn, G.Xh, tc, ntile)]);
+    const int ntile = (GXh + tc - 1) / tc;
+    const cpx<T>* in = src + slice * ((int64_t)GY * ntile * Tn * tc);
+    for (int f = threadIdx.x; f < GF; f += kNT)
+      lds_cpx_store(S.slice + Q::bin(f, G), 1, in[ttile_idx(t, f, Tn, GXh, tc, ntile)]);
   } else {
-    const cpx<T>* in = src + (slice * Tn + t) * G.F;
-    for (int f = threadIdx.x; f < G.F; f += kNT) lds_cpx_store(S.slice + bin_off(f, G), 1, in[f]);
+    const cpx<T>* in = src + (slice * Tn + t) * GF;
+    for (int f = threadIdx.x; f < GF; f += kNT) lds_cpx_store(S.slice + Q::bin(f, G), 1, in[f]);
   }
-  slice_c2r<T, kMaxB, RM>(S.slice, G, S.tw);
-  const int P = G.X * G.Y;
+  slice_c2r_rm<T, RM>(S.slice, G, S.tw);
+  const int P = GX * GY;
   const int64_t off = (slice * Tn + t) * P;
   const bool nrm = (mode == 3 && norms) || (mode == 2 && slice < nfirst);
   T acc_d = 0, acc_n = 0;
   for (int e = threadIdx.x; e < P; e += kNT) {
-    const int y = e / G.X, x = e - y * G.X;
-    const T v = S.slice[y * G.RS + x] * scale;
+    const int y = e / GX, x = e - y * GX;
+    const T v = S.slice[y * RS + x] * scale;
     if (nrm) {
       const T o = dst[off + e];
       acc_d += (v - o) * (v - o);
@@ -164,7 +168,7 @@ void k_plane_inv(int mode, const cpx<T>* src,
       const T an = v + fmax(-theta, fmin(q, theta));
       state[off + e] = an;
       if (wz) dst[off + e] = v;
-      if (nxt) S.slice[y * G.RS + x] = fma((T)-2, fmax(-theta, fmin(an, theta)), an);
+      if (nxt) S.slice[y * RS + x] = fma((T)-2, fmax(-theta, fmin(an, theta)), an);
     } else {
       dst[off + e] = v;
     }
@@ -176,8 +180,8 @@ void k_plane_inv(int mode, const cpx<T>* src,
       T* sp = supp + (slice * s + st3) * s * s;
       for (int q = threadIdx.x; q < s * s; q += kNT) {
         const int sy = q / s, sx = q - sy * s;
-        const int x = (sx - r + G.X) % G.X, y = (sy - r + G.Y) % G.Y;
-        sp[q] = S.slice[y * G.RS + x] * scale + yv[off + y * G.X + x];
+        const int x = (sx - r + GX) % GX, y = (sy - r + GY) % GY;
+        sp[q] = S.slice[y * RS + x] * scale + yv[off + y * GX + x];
       }
     }
   }
@@ -191,15 +195,15 @@ void k_plane_inv(int mode, const cpx<T>* src,
   }
   if (mode == 3 && nxt) {   // the next iteration's forward plane transform (k_plane_fwd mode 3)
     zero_pad_row(S.slice, G);
-    slice_r2c<T, kMaxB, RM>(S.slice, G, S.tw);
+    slice_r2c_rm<T, RM>(S.slice, G, S.tw);
     if (tc > 0) {
-      const int ntile = (G.Xh + tc - 1) / tc;
-      cpx<T>* out = nxt + slice * ((int64_t)G.Y * ntile * Tn * tc);
-      for (int f = threadIdx.x; f < G.F; f += kNT)
-        out[ttile_idx(t, f, Tn, G.Xh, tc, ntile)] = lds_cpx(S.slice + bin_off(f, G), 1);
+      const int ntile = (GXh + tc - 1) / tc;
+      cpx<T>* out = nxt + slice * ((int64_t)GY * ntile * Tn * tc);
+      for (int f = threadIdx.x; f < GF; f += kNT)
+        out[ttile_idx(t, f, Tn, GXh, tc, ntile)] = lds_cpx(S.slice + Q::bin(f, G), 1);
     } else {
-      cpx<T>* out = nxt + (slice * Tn + t) * G.F;
-      for (int f = threadIdx.x; f < G.F; f += kNT) out[f] = lds_cpx(S.slice + bin_off(f, G), 1);
+      cpx<T>* out = nxt + (slice * Tn + t) * GF;
+      for (int f = threadIdx.x; f < GF; f += kNT) out[f] = lds_cpx(S.slice + Q::bin(f, G), 1);
     }
   }
 }
@@ -463,7 +467,8 @@ hipError_t launch_plane_fwd(int mode, const T* a, T* b, const T* usup, int sx, i
                        slice_smem_bytes(G, sizeof(T)), stream, mode, a, b, usup, sx, sy, st, o,
                        theta, KG, r, dst, Tn, tw, G, tc);
   };
-  if (slice_fits(kRm74, G)) go(k_plane_fwd<T, kRm74>);
+  if (grid_is74(G)) go(k_plane_fwd<T, kRm74F>);
+  else if (slice_fits(kRm74, G)) go(k_plane_fwd<T, kRm74>);
   else go(k_plane_fwd<T, kRmAll>);
   return hipGetLastError();
 }
@@ -578,7 +583,8 @@ hipError_t launch_plane_inv(int mode, const cpx<T>* src, T* dst, const T* yv, T*
                        slice_smem_bytes(G, sizeof(T)), stream, mode, src, dst, yv, supp, norms,
                        nfirst, scale, r, Tn, tw, G, tc, state, theta, wz ? 1 : 0, nxt);
   };
-  if (slice_fits(kRm74, G)) go(k_plane_inv<T, kRm74>);
+  if (grid_is74(G)) go(k_plane_inv<T, kRm74F>);
+  else if (slice_fits(kRm74, G)) go(k_plane_inv<T, kRm74>);
   else go(k_plane_inv<T, kRmAll>);
   return hipGetLastError();
 }

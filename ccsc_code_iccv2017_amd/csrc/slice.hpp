@@ -2,6 +2,7 @@
 #pragma once
 
 #include "kernels.hpp"
+#include "fft_fixed.hpp"
 
 namespace ccsc {
 
@@ -9,6 +10,9 @@ namespace ccsc {
 // instantiations fit 64 VGPRs, so two 1024-thread workgroups (two slices) share a CU
 // and one's barriers and HBM waits overlap the other's passes; the all-radix build
 // needs ~95-127 VGPRs (one workgroup per CU).
+// (the fixed-geometry 74 build, kRm74F, needs ~70 and spills a little at 64: still
+// faster than one workgroup per CU, C4 0.247 vs 0.307 s per outer iteration, round 4)
+constexpr int kRm74Fbit = 1 << 14;
 template <int RM>
 constexpr int slice_waves() { return RM == kRmAll ? 4 : 8; }
 
@@ -53,6 +57,76 @@ __device__ __forceinline__ void zero_pad_row(T* lds, const Grid2D& G) {
 __device__ __forceinline__ int bin_off(int f, const Grid2D& G) {
   const int y = f / G.Xh;
   return y * G.RS + 2 * (f - y * G.Xh);
+}
+
+// ---- the 74 x 74 grid of the C4 / C5 configs (64 + 2 * 5), compile-time ----------
+// Planned as a radix-2 pass then the 37-point prime-factor pass per direction (no
+// twiddles).  kRm74F instantiations run on exactly this grid: geometry and the radix-2
+// passes are compile-time (fft_fixed.hpp fpass; the runtime pass's arithmetic, bit for
+// bit), so the element / bin index divisions of the slice kernels fold to multiplies
+// and the pass geometry to immediates.
+using Grid74 = FixedGrid<2, kPfaM, 2, kPfaM>;
+constexpr int kRm74F = kRm74 | kRm74Fbit;
+
+__host__ inline bool grid_is74(const Grid2D& G) {
+  auto plan_ok = [](const Plan1D& p) {
+    return p.n == Grid74::X && p.npass == 2 && p.rad[0] == 2 && p.rad[1] == kPfaM && p.pfa;
+  };
+  return G.X == Grid74::X && G.Y == Grid74::Y && G.RS == Grid74::RS && G.Yp == Grid74::Yp &&
+         plan_ok(G.px) && plan_ok(G.py);
+}
+
+// slice geometry of an instantiation: compile-time for kRm74F, else the runtime grid
+template <int RM>
+struct SG {
+  static constexpr bool fixed = RM == kRm74F;
+  __device__ static int X(const Grid2D& G) { if constexpr (fixed) return Grid74::X; else return G.X; }
+  __device__ static int Y(const Grid2D& G) { if constexpr (fixed) return Grid74::Y; else return G.Y; }
+  __device__ static int Xh(const Grid2D& G) { if constexpr (fixed) return Grid74::Xh; else return G.Xh; }
+  __device__ static int RS(const Grid2D& G) { if constexpr (fixed) return Grid74::RS; else return G.RS; }
+  __device__ static int Yp(const Grid2D& G) { if constexpr (fixed) return Grid74::Yp; else return G.Yp; }
+  __device__ static int F(const Grid2D& G) { if constexpr (fixed) return Grid74::F; else return G.F; }
+  __device__ static int bin(int f, const Grid2D& G) {
+    const int y = f / Xh(G);
+    return y * RS(G) + 2 * (f - y * Xh(G));
+  }
+};
+
+template <typename T, int SIGN>
+__device__ __forceinline__ void pfa74(T* lds, bool xdir) {
+  using FG = Grid74;
+  constexpr LineGeom gx = {FG::Yp / 2, 2 * FG::RS, 1, FG::RS};
+  constexpr LineGeom gy = {FG::Xh, 2, FG::RS, 1};
+  if (xdir) fft_pass_pfa<T, kPfaM, SIGN, kPfaQP, kNT>(lds, gx);
+  else fft_pass_pfa<T, kPfaM, SIGN, kPfaQP, kNT>(lds, gy);
+}
+
+// slice_r2c / slice_c2r of instantiation RM (fft.hpp), the fixed passes on kRm74F
+template <typename T, int RM>
+__device__ __forceinline__ void slice_r2c_rm(T* lds, const Grid2D& G, const cpx<T>* tw) {
+  if constexpr (RM == kRm74F) {
+    lds_sync();
+    const int tid = threadIdx.x;
+    fpass<T, Grid74, kNT, true, 2, 1, -1, kModePlain>(lds, tw, tid);
+    pfa74<T, -1>(lds, true);
+    fpass<T, Grid74, kNT, false, 2, 1, -1, kModeSplitToHalf>(lds, tw, tid);
+    pfa74<T, -1>(lds, false);
+  } else {
+    slice_r2c<T, kMaxB, RM>(lds, G, tw);
+  }
+}
+template <typename T, int RM>
+__device__ __forceinline__ void slice_c2r_rm(T* lds, const Grid2D& G, const cpx<T>* tw) {
+  if constexpr (RM == kRm74F) {
+    lds_sync();
+    const int tid = threadIdx.x;
+    fpass<T, Grid74, kNT, false, 2, 1, +1, kModePlain>(lds, tw, tid);
+    pfa74<T, +1>(lds, false);
+    fpass<T, Grid74, kNT, true, 2, 1, +1, kModeHermPair>(lds, tw, tid);
+    pfa74<T, +1>(lds, true);
+  } else {
+    slice_c2r<T, kMaxB, RM>(lds, G, tw);
+  }
 }
 
 // Register budget of the per-bin accumulators (bins per thread) of the fused

@@ -29,33 +29,35 @@ void k_zstep_diag(T* __restrict__ z, T* __restrict__ as,
                                                     int TOL, int WZ) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   Smem<T> S = carve<T>(smem, G);
-  load_twiddles(S.tw, twg, G.ntw);
+  using Q = SG<RM>;
+  const int GX = Q::X(G), RS = Q::RS(G);
+  if constexpr (!Q::fixed) load_twiddles(S.tw, twg, G.ntw);
   const int64_t slice = blockIdx.x;
-  const int P = G.X * G.Y;
-  const int F = G.F;
+  const int P = GX * Q::Y(G);
+  const int F = Q::F(G);
   const int64_t off = slice * P;
   theta = __builtin_canonicalize(theta);
   lds_sync();
   for (int e = threadIdx.x; e < P; e += kNT) {
-    const int y = e / G.X, x = e - y * G.X;
+    const int y = e / GX, x = e - y * GX;
     const T a = as[off + e];
-    S.slice[y * G.RS + x] = fma((T)-2, fmax(-theta, fmin(a, theta)), a);
+    S.slice[y * RS + x] = fma((T)-2, fmax(-theta, fmin(a, theta)), a);
   }
   zero_pad_row(S.slice, G);
-  slice_r2c<T, kMaxB, RM>(S.slice, G, S.tw);
+  slice_r2c_rm<T, RM>(S.slice, G, S.tw);
   const cpx<T>* Es = E + slice * F;
   for (int f = threadIdx.x; f < F; f += kNT) {
-    T* q = S.slice + bin_off(f, G);
+    T* q = S.slice + Q::bin(f, G);
     const cpx<T> c = lds_cpx(q, 1);
     const cpx<T> e = Es[f];
     const T sc = sden[f];
     lds_cpx_store(q, 1, cpx<T>{(e.x + rho * c.x) * sc, (e.y + rho * c.y) * sc});
   }
-  slice_c2r<T, kMaxB, RM>(S.slice, G, S.tw);
+  slice_c2r_rm<T, RM>(S.slice, G, S.tw);
   T nd = 0, nz = 0;
   for (int e = threadIdx.x; e < P; e += kNT) {
-    const int y = e / G.X, x = e - y * G.X;
-    const T zn = S.slice[y * G.RS + x];
+    const int y = e / GX, x = e - y * GX;
+    const T zn = S.slice[y * RS + x];
     if (TOL) {
       const T zo = z[off + e];
       nd += (zn - zo) * (zn - zo);
@@ -85,7 +87,8 @@ hipError_t launch_zstep_diag(T* z, T* as, const cpx<T>* E, const T* sden, int64_
     hipLaunchKernelGGL(kern, dim3((unsigned)nslices), dim3(kNT), slice_smem_bytes(G, sizeof(T)),
                        st, z, as, E, sden, tw, G, theta, rho, znorm, tol ? 1 : 0, write_z ? 1 : 0);
   };
-  if (slice_fits(kRm74, G)) go(k_zstep_diag<T, kRm74>);   // the 74 grid (C5): 2 slices per CU
+  if (grid_is74(G)) go(k_zstep_diag<T, kRm74F>);   // the 74 grid (C5): 2 slices per CU
+  else if (slice_fits(kRm74, G)) go(k_zstep_diag<T, kRm74>);
   else go(k_zstep_diag<T, kRmAll>);
   return hipGetLastError();
 }
