@@ -555,10 +555,23 @@ __constant__ const unsigned char kDtMap[4][kDtTW] = {
     {3 * 8 + 2, 3 * 8 + 3, 0 * 8 + 0, 2 * 8 + 0, 6 * 8 + 0, 5 * 8 + 1, 6 * 8 + 2},
     {4 * 8 + 3, 4 * 8 + 4, 3 * 8 + 0, 5 * 8 + 0, 3 * 8 + 1, 6 * 8 + 1, 5 * 8 + 2}};
 
-// sum over the four 16-lane rows (lanes row, row + 16, row + 32, row + 48)
+// sum over the four 16-lane rows (lanes row, row + 16, row + 32, row + 48) through the
+// gfx950 row-swap moves (VALU; the xor shuffles they replace were LDS bpermute round trips
+// on the sweeps' serial chain): permlane16_swap pairs rows 0/1 and 2/3, permlane32_swap
+// the two halves; each add sees the same two operands as v + shfl_xor(v, 16 | 32)
+__device__ __forceinline__ double pl_pair_sum(double v, bool r32) {
+  const int lo = __double2loint(v), hi = __double2hiint(v);
+  if (r32) {
+    const auto l = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto h = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    return __hiloint2double(h[0], l[0]) + __hiloint2double(h[1], l[1]);
+  }
+  const auto l = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  const auto h = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  return __hiloint2double(h[0], l[0]) + __hiloint2double(h[1], l[1]);
+}
 __device__ __forceinline__ double xrow_sum(double v) {
-  v += __shfl_xor(v, 16, 64);
-  return v + __shfl_xor(v, 32, 64);
+  return pl_pair_sum(pl_pair_sum(v, false), true);
 }
 // sum within each 16-lane row (DPP; result in every lane of the row)
 __device__ __forceinline__ double row16_sum(double v) {

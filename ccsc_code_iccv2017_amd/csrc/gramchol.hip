@@ -7,8 +7,9 @@
 // G is held as 16 x 16 tiles (T = ceil(K / 16) <= 7 per dimension, the T(T+1)/2
 // lower tiles dealt round-robin to the four waves) in v_mfma_f64_16x16x4_f64
 // accumulators for the whole kernel:
-//   Gram     per 4 patches and tile (I, J): Re += Ar_I^T Ar_J + Ai_I^T Ai_J,
-//            Im += Ar_I^T Ai_J - Ai_I^T Ar_J  (4 MFMAs); the code spectra are
+//   Gram     per 4 patches and tile (I, J): Re G = Ar_I^T Ar_J + Ai_I^T Ai_J,
+//            Im G = Ar_I^T Ai_J - Ai_I^T Ar_J from three real products (Gauss, 3 MFMAs,
+//            gram_kstep); the code spectra are
 //            staged through LDS in chunks of 16 patches, double-buffered, the next
 //            chunk's (strided) global loads in flight under the current chunk's MFMAs;
 //   Cholesky blocked right-looking over the T tile columns j:
@@ -37,6 +38,8 @@ struct GcShape {
   static constexpr int KP = 16 * TM;           // padded filter count of a staged row
   static constexpr int LD = KP + 1;            // staged row stride (complex)
   static constexpr int WGS = TM <= 7 ? 2 : 1;  // workgroups per CU
+  // the third accumulator set of the Gauss Gram fits the registers up to TM = 8
+  static constexpr bool Gauss = TM <= 8;
 };
 constexpr int kGcMaxTM = 12;
 constexpr int kGcPC = 16;                   // patches per staged chunk
@@ -66,10 +69,14 @@ __device__ __forceinline__ void gc_tile(int t, int& I, int& J) {
 // Gram MFMAs of wave w for one k-step (4 patches: lane l takes patch l >> 4 of the
 // step and filter 16 T + (l & 15) of tile row/column T).  Tile coordinates are
 // wave-uniform runtime values: operands are loaded per tile from LDS, so no
-// register array is indexed at run time.
+// register array is indexed at run time.  Three real products per complex tile
+// (Gauss): t1 = sum ax bx, t2 = sum ay by, t3 = sum (ax - ay)(bx + by), so that
+// Re G = t1 + t2 and Im G = sum (ax by - ay bx) = t3 - t1 + t2 (gram_gauss_fold) --
+// 3 MFMAs per tile and k-step instead of 4 (the Gram is matrix-core bound).
 template <int TM>
 __device__ __forceinline__ void gram_kstep(const cpx<double>* row, int w, int Tn,
-                                           d4 (&gr)[GcShape<TM>::TW], d4 (&gi)[GcShape<TM>::TW]) {
+                                           d4 (&t1)[GcShape<TM>::TW], d4 (&t2)[GcShape<TM>::TW],
+                                           d4 (&t3)[GcShape<TM>::Gauss ? GcShape<TM>::TW : 1]) {
   const int lane = threadIdx.x & 63;
 #pragma unroll
   for (int s = 0; s < GcShape<TM>::TW; ++s) {
@@ -79,10 +86,31 @@ __device__ __forceinline__ void gram_kstep(const cpx<double>* row, int w, int Tn
     if (t < GcShape<TM>::Tiles && I < Tn) {
       const cpx<double> a = row[16 * I + (lane & 15)];
       const cpx<double> b = row[16 * J + (lane & 15)];
-      gr[s] = mfma(a.x, b.x, gr[s]);
-      gr[s] = mfma(a.y, b.y, gr[s]);
-      gi[s] = mfma(a.x, b.y, gi[s]);
-      gi[s] = mfma(-a.y, b.x, gi[s]);
+      if constexpr (GcShape<TM>::Gauss) {
+        t1[s] = mfma(a.x, b.x, t1[s]);
+        t2[s] = mfma(a.y, b.y, t2[s]);
+        t3[s] = mfma(a.x - a.y, b.x + b.y, t3[s]);
+      } else {   // Re, Im directly (4 MFMAs; t1 = Re, t2 = Im)
+        t1[s] = mfma(a.x, b.x, t1[s]);
+        t1[s] = mfma(a.y, b.y, t1[s]);
+        t2[s] = mfma(a.x, b.y, t2[s]);
+        t2[s] = mfma(-a.y, b.x, t2[s]);
+      }
+    }
+  }
+}
+template <int TM>
+__device__ __forceinline__ void gram_gauss_fold(d4 (&t1)[GcShape<TM>::TW], d4 (&t2)[GcShape<TM>::TW],
+                                                const d4 (&t3)[GcShape<TM>::Gauss ? GcShape<TM>::TW : 1]) {
+  if constexpr (!GcShape<TM>::Gauss) return;
+#pragma unroll
+  for (int s = 0; s < GcShape<TM>::TW; ++s) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const double re = t1[s][r] + t2[s][r];
+      const double im = (t3[s][r] - t1[s][r]) + t2[s][r];
+      t1[s][r] = re;
+      t2[s][r] = im;
     }
   }
 }
@@ -162,7 +190,8 @@ __device__ __forceinline__ void fix_diag(int w, int K, int Tn, double rho,
   }
 }
 
-template <int TM>
+// HP: right-hand-side entries of h per thread (1 when K NV <= kGcNT: the headline's one)
+template <int TM, int HP>
 __global__ __launch_bounds__(kGcNT, GcShape<TM>::WGS) void k_gram_chol_mf(const cpx<double>* __restrict__ Zh,
                                                            const cpx<double>* __restrict__ Bh,
                                                            cpx<double>* __restrict__ L,
@@ -181,12 +210,14 @@ __global__ __launch_bounds__(kGcNT, GcShape<TM>::WGS) void k_gram_chol_mf(const 
   int Tn = (K + 15) >> 4;
   const int KV = K * NV;
 
-  d4 gr[kGcTW], gi[kGcTW];
+  d4 gr[kGcTW], gi[kGcTW], g3[S::Gauss ? kGcTW : 1];   // Gram: Gauss products t1, t2, t3
 #pragma unroll
   for (int s = 0; s < kGcTW; ++s) gr[s] = gi[s] = (d4){0.0, 0.0, 0.0, 0.0};
-  cpx<double> hacc[kGcHPT];
 #pragma unroll
-  for (int i = 0; i < kGcHPT; ++i) hacc[i] = {0.0, 0.0};
+  for (int s = 0; s < (S::Gauss ? kGcTW : 1); ++s) g3[s] = (d4){0.0, 0.0, 0.0, 0.0};
+  cpx<double> hacc[HP];
+#pragma unroll
+  for (int i = 0; i < HP; ++i) hacc[i] = {0.0, 0.0};
 
   // ---- Gram + h: chunks of kGcPC patches, double-buffered ----
   constexpr int kPer = (kGcPC * kGcKP + kGcNT - 1) / kGcNT;   // staged values per thread
@@ -230,11 +261,11 @@ __global__ __launch_bounds__(kGcNT, GcShape<TM>::WGS) void k_gram_chol_mf(const 
 #pragma unroll
     for (int kk = 0; kk < kGcPC / 4; ++kk) {
       const cpx<double>* row = a + (4 * kk + (lane >> 4)) * kGcLD;
-      if (kk < kvalid) gram_kstep<TM>(row, wave, Tn, gr, gi);
+      if (kk < kvalid) gram_kstep<TM>(row, wave, Tn, gr, gi, g3);
     }
     const cpx<double>* b = sB + buf * kGcPC * NV;
 #pragma unroll
-    for (int i = 0; i < kGcHPT; ++i) {
+    for (int i = 0; i < HP; ++i) {
       const int q = tid + i * kGcNT;   // q = uv * K + k
       if (q < KV) {
         const int uv = q / K, k = q - uv * K;
@@ -248,10 +279,11 @@ __global__ __launch_bounds__(kGcNT, GcShape<TM>::WGS) void k_gram_chol_mf(const 
     __syncthreads();
   }
 #pragma unroll
-  for (int i = 0; i < kGcHPT; ++i) {
+  for (int i = 0; i < HP; ++i) {
     const int q = tid + i * kGcNT;
     if (q < KV) h[(int64_t)f * KV + q] = hacc[i];
   }
+  gram_gauss_fold<TM>(gr, gi, g3);   // gr, gi <- Re G, Im G
   fix_diag<TM>(wave, K, Tn, rho, gr, gi);
 
   // ---- blocked Cholesky over the tile columns ----
@@ -330,12 +362,12 @@ size_t gram_chol_mf_smem(int NV, int K) {
   return stage > chol ? stage : chol;
 }
 
-template <int TM>
+template <int TM, int HP>
 static void gram_chol_mf_go(const cpx<double>* Zh, const cpx<double>* Bh, cpx<double>* L,
                             cpx<double>* h, int F, int K, int ni, double rho, int NV,
                             hipStream_t st) {
   const int grid = ((F + 7) / 8) * 8;
-  hipLaunchKernelGGL(k_gram_chol_mf<TM>, dim3(grid), dim3(kGcNT), gram_chol_mf_smem(NV, K), st,
+  hipLaunchKernelGGL((k_gram_chol_mf<TM, HP>), dim3(grid), dim3(kGcNT), gram_chol_mf_smem(NV, K), st,
                      Zh, Bh, L, h, F, K, ni, rho, NV);
 }
 
@@ -344,10 +376,13 @@ hipError_t launch_gram_chol_mf(const cpx<double>* Zh, const cpx<double>* Bh, cpx
                                hipStream_t st) {
   if (!gram_chol_mf_ok(K, NV)) return hipErrorInvalidValue;
   switch (gc_tm(K)) {
-    case 7: gram_chol_mf_go<7>(Zh, Bh, L, h, F, K, ni, rho, NV, st); break;
-    case 8: gram_chol_mf_go<8>(Zh, Bh, L, h, F, K, ni, rho, NV, st); break;
-    case 10: gram_chol_mf_go<10>(Zh, Bh, L, h, F, K, ni, rho, NV, st); break;
-    default: gram_chol_mf_go<12>(Zh, Bh, L, h, F, K, ni, rho, NV, st); break;
+    case 7:
+      if (K * NV <= kGcNT) gram_chol_mf_go<7, 1>(Zh, Bh, L, h, F, K, ni, rho, NV, st);
+      else gram_chol_mf_go<7, kGcHPT>(Zh, Bh, L, h, F, K, ni, rho, NV, st);
+      break;
+    case 8: gram_chol_mf_go<8, kGcHPT>(Zh, Bh, L, h, F, K, ni, rho, NV, st); break;
+    case 10: gram_chol_mf_go<10, kGcHPT>(Zh, Bh, L, h, F, K, ni, rho, NV, st); break;
+    default: gram_chol_mf_go<12, kGcHPT>(Zh, Bh, L, h, F, K, ni, rho, NV, st); break;
   }
   return hipGetLastError();
 }
