@@ -50,10 +50,12 @@ __device__ __forceinline__ cpx<T> readlane_c(cpx<T> v, int l) {
 // half-row and row mirrors leave each 16-lane row's sum in all its lanes; the
 // four row sums are combined through v_readlane.  Result in every lane.  The
 // xor-shuffle form (wave_sum) costs 12 ds_bpermute round trips per double.
+// (mov_dpp: every control used here gives each lane a valid source, so the old value is
+// dead -- update_dpp(0, ...) spent a v_mov of the zero per DPP move)
 template <int CTRL>
 __device__ __forceinline__ double dpp_mov(double v) {
-  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, true);
   return __hiloint2double(hi, lo);
 }
 __device__ __forceinline__ double wave_sum_dpp(double v) {
@@ -573,12 +575,38 @@ __device__ __forceinline__ double pl_pair_sum(double v, bool r32) {
 __device__ __forceinline__ double xrow_sum(double v) {
   return pl_pair_sum(pl_pair_sum(v, false), true);
 }
-// sum within each 16-lane row (DPP; result in every lane of the row)
-__device__ __forceinline__ double row16_sum(double v) {
-  v += dpp_mov<0xB1>(v);    // quad_perm [1,0,3,2]
-  v += dpp_mov<0x4E>(v);    // quad_perm [2,3,0,1]
-  v += dpp_mov<0x141>(v);   // row_half_mirror
-  return v + dpp_mov<0x140>(v);   // row_mirror
+// Row sums of four complex values p[0..3] over each 16-lane row, reduce-scatter form:
+// the eight doubles halve at each DPP level (ror 8, half-mirror, xor 2) and the last
+// level sums one value (xor 1) -- 26 DPP moves and 15 adds instead of the 64 and 32 of
+// eight row16_sums.  Lane r of the row ends with the sum of double (r >> 1) & 7, i.e.
+// component (r >> 1) & 1 of p[r >> 2]; the even lanes store it to out[r >> 2].
+__device__ __forceinline__ void row16_sum4_store(const cpx<double> (&p)[4], int r,
+                                                 cpx<double>* out) {
+  double v[8];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    v[2 * q] = p[q].x;
+    v[2 * q + 1] = p[q].y;
+  }
+  const bool b3 = (r & 8) != 0, b2 = (r & 4) != 0, b1 = (r & 2) != 0;
+  double w1[4], w2[2];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {   // partner r ^ 8
+    const double keep = b3 ? v[k + 4] : v[k], send = b3 ? v[k] : v[k + 4];
+    w1[k] = keep + dpp_mov<0x128>(send);   // row_ror:8
+  }
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {   // partner (r & 8) | (7 - (r & 7)): bit 2 flipped
+    const double keep = b2 ? w1[k + 2] : w1[k], send = b2 ? w1[k] : w1[k + 2];
+    w2[k] = keep + dpp_mov<0x141>(send);   // row_half_mirror
+  }
+  double w3;
+  {                               // partner r ^ 2
+    const double keep = b1 ? w2[1] : w2[0], send = b1 ? w2[0] : w2[1];
+    w3 = keep + dpp_mov<0x4E>(send);       // quad_perm [2,3,0,1]
+  }
+  w3 += dpp_mov<0xB1>(w3);                 // quad_perm [1,0,3,2]
+  if ((r & 1) == 0) reinterpret_cast<double*>(out)[r >> 1] = w3;
 }
 __device__ __forceinline__ void wave_sync_lds() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -618,7 +646,12 @@ __global__ __launch_bounds__(256) void k_dsolve_tile(const cpx<double>* __restri
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int R = 16 * tI[s] + row, C = 16 * tJ[s] + 4 * cg + q;
-      Lt[s][q] = (tI[s] >= 0 && R < K && C <= R) ? Lf[C * K - (C * (C - 1)) / 2 + R - C] : zero;
+      if (tI[s] >= 0 && R < K && C <= R) {   // one 16-B load (cpx<double> is 8-B aligned)
+        const auto v = *reinterpret_cast<const vec2_t<double>::type*>(Lf + C * K - (C * (C - 1)) / 2 + R - C);
+        Lt[s][q] = {v.x, v.y};
+      } else {
+        Lt[s][q] = zero;
+      }
     }
   }
   if (tid < 16 * Tn) {
@@ -672,12 +705,10 @@ __global__ __launch_bounds__(256) void k_dsolve_tile(const cpx<double>* __restri
       if (tI[s] == J && tJ[s] == J) {
         cpx<double> v = sy[16 * J + row];
         for (int I = J + 1; I < Tn; ++I) v = csub(v, sp[pb][I][row]);
+        cpx<double> p[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const cpx<double> p = cmulc(Lt[s][q], v);   // conj(M[row][c]) v[row]
-          const cpx<double> ps = {row16_sum(p.x), row16_sum(p.y)};
-          if (row == 0) sx[16 * J + 4 * cg + q] = ps;
-        }
+        for (int q = 0; q < 4; ++q) p[q] = cmulc(Lt[s][q], v);   // conj(M[row][c]) v[row]
+        row16_sum4_store(p, row, sx + 16 * J + 4 * cg);
         wave_sync_lds();
       }
     }
@@ -687,12 +718,10 @@ __global__ __launch_bounds__(256) void k_dsolve_tile(const cpx<double>* __restri
     for (int s = 0; s < kDtTW; ++s) {
       if (tJ[s] == J - 1 && tI[s] >= J) {
         const cpx<double> xr = sx[16 * tI[s] + row];
+        cpx<double> p[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const cpx<double> p = cmulc(Lt[s][q], xr);   // conj(L[row][c]) x[row]
-          const cpx<double> ps = {row16_sum(p.x), row16_sum(p.y)};
-          if (row == 0) sp[pb ^ 1][tI[s]][4 * cg + q] = ps;
-        }
+        for (int q = 0; q < 4; ++q) p[q] = cmulc(Lt[s][q], xr);   // conj(L[row][c]) x[row]
+        row16_sum4_store(p, row, &sp[pb ^ 1][tI[s]][4 * cg]);
       }
     }
     __syncthreads();
