@@ -7,7 +7,17 @@
 
 namespace ccsc {
 
-template <typename T> struct cpx { T x, y; };
+// 16-B aligned (fp64): every complex array of the engine starts 16-B aligned with
+// complex-sized elements, so one 16-B access per element instead of two 8-B ones
+template <typename T> struct alignas(2 * sizeof(T)) cpx { T x, y; };
+// predicated complex load as one 16-B access (a `c ? p[i] : zero` select is split by the
+// compiler into two 8-B loads)
+template <typename T>
+__device__ __forceinline__ cpx<T> ldc_if(bool c, const cpx<T>* p) {
+  cpx<T> v = {(T)0, (T)0};
+  if (c) v = *p;
+  return v;
+}
 template <typename T> struct vec2_t;
 template <> struct vec2_t<double> { using type = double2; };
 template <> struct vec2_t<float> { using type = float2; };

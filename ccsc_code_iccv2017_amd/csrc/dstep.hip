@@ -830,7 +830,7 @@ __global__ __launch_bounds__(64 * kWbWG) void k_gram_wb(const cpx<T>* __restrict
 #pragma unroll
     for (int u = 0; u < RPL; ++u) {
       const int i = lane + 64 * u;
-      a[p][u] = (p < ni && i < K) ? Zh[((int64_t)p * K + i) * F + f] : zero;
+      a[p][u] = ldc_if(p < ni && i < K, Zh + ((int64_t)p * K + i) * F + f);
     }
   cpx<T>* slot = L + (int64_t)f * Kp;
 #pragma unroll
@@ -926,7 +926,7 @@ __global__ __launch_bounds__(64 * kWbWG) void k_dsolve_wb(const cpx<T>* __restri
 #pragma unroll
     for (int u = 0; u < RPL; ++u) {
       const int i = lane + 64 * u;
-      a[p][u] = (p < ni && i < K) ? slot[p * K + i] : zero;
+      a[p][u] = ldc_if(p < ni && i < K, slot + p * K + i);
     }
   // lane p: row p and column p of L_M, 1 / L_M[p][p]
   const cpx<T>* lm = slot + ni * K;
@@ -934,8 +934,8 @@ __global__ __launch_bounds__(64 * kWbWG) void k_dsolve_wb(const cpx<T>* __restri
   const bool lp = lane < ni;
 #pragma unroll
   for (int q = 0; q < kWbMaxNi; ++q) {
-    lrow[q] = (lp && q < ni) ? lm[lane * ni + q] : zero;
-    lcol[q] = (lp && q < ni) ? lm[q * ni + lane] : zero;
+    lrow[q] = ldc_if(lp && q < ni, lm + lane * ni + q);
+    lcol[q] = ldc_if(lp && q < ni, lm + q * ni + lane);
   }
   const T dinv = lp ? (T)1 / lm[lane * ni + lane].x : (T)0;
   const T irho = (T)1 / rho;
