@@ -90,9 +90,33 @@ void k_plane_fwd(int mode, const T* __restrict__ a,
   for (int f = threadIdx.x; f < GF; f += kNT) out[f] = lds_cpx(S.slice + Q::bin(f, G), 1);
 }
 
+// ---- compile-time t transforms of C4 (T = 42 = 7 * 3 * 2 radix passes) ----------------
+// The t lines of an LDS tile are interleaved complex columns (line stride 2, element stride
+// RS = 2 NL): fft_fixed.hpp's y-direction pass with this geometry, index math and strides
+// compile-time (the runtime fft_dir's arithmetic, bit for bit).  tline42_ok() checks the
+// runtime plan (radix order, twiddle offsets) the fixed passes assume.
+template <int NL>
+struct TLines42 {
+  static constexpr int X = 1, Y = 42, Yp = 42, Xh = NL, RS = 2 * NL;
+};
+__host__ inline bool tline42_ok(const Grid2D& Gt, int nl) {
+  const Plan1D& p = Gt.py;
+  return Gt.Y == 42 && Gt.Xh == nl && Gt.RS == 2 * nl && p.n == 42 && p.npass == 3 &&
+         p.rad[0] == 7 && p.rad[1] == 3 && p.rad[2] == 2 && p.twoff[0] == 0 && p.twoff[1] == 6 &&
+         p.twoff[2] == 20;
+}
+template <typename T, int NL, int SIGN>
+__device__ __forceinline__ void tfft42(T* lds, const cpx<T>* tw) {
+  using FG = TLines42<NL>;
+  const int tid = threadIdx.x;
+  fpass<T, FG, kNT, false, 7, 1, SIGN, kModePlain>(lds, tw, tid);
+  fpass<T, FG, kNT, false, 3, 7, SIGN, kModePlain>(lds, tw + 6, tid);
+  fpass<T, FG, kNT, false, 2, 21, SIGN, kModePlain>(lds, tw + 20, tid);
+}
+
 // ---- t-direction complex FFT (src may equal dst); one workgroup per (slice, y)
 // Gt describes the T x Xh tile: Gt.Y = T (plan Gt.py), Gt.Xh = lines, Gt.RS = row stride.
-template <typename T, int SIGN, int RM>
+template <typename T, int SIGN, int RM, int FNL = 0>
 __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(slice_waves<RM>())))
 void k_tfft(const cpx<T>* src, cpx<T>* dst, int Yn, int F2,
                                               const cpx<T>* __restrict__ twg, Grid2D Gt) {
@@ -110,7 +134,8 @@ void k_tfft(const cpx<T>* src, cpx<T>* dst, int Yn, int F2,
   }
   lds_sync();
   const LineGeom g = {Xh, 2, Gt.RS, 1};
-  fft_dir<T, kMaxB, SIGN, kMaxPass, kNT, 1, 1, RM>(lds, kModePlain, g, g, Gt, Gt.py, s_tw);
+  if constexpr (FNL > 0) tfft42<T, FNL, SIGN>(lds, s_tw);   // C4's 42 x 38 tiles
+  else fft_dir<T, kMaxB, SIGN, kMaxPass, kNT, 1, 1, RM>(lds, kModePlain, g, g, Gt, Gt.py, s_tw);
   for (int e = threadIdx.x; e < Tn * Xh; e += kNT) {
     const int t = e / Xh, x = e - t * Xh;
     dst[base + (int64_t)t * F2 + x] = lds_cpx(lds + t * Gt.RS + 2 * x, 1);
@@ -245,7 +270,8 @@ __global__ void k_zsolve3(cpx<T>* __restrict__ C, const cpx<T>* __restrict__ Bha
 // workgroup -- the solve of every patch reads them there instead of from L2 (two exposed
 // global round trips per patch otherwise) -- and each patch's B^ values are loaded before
 // its forward t-FFT, consumed after it.
-template <typename T, int RM, int LD, int KMAX, bool DL>
+// FNL > 0: the t transforms on the compile-time 42-point plan over FNL = K TC lines (C4)
+template <typename T, int RM, int LD, int KMAX, bool DL, int FNL>
 __global__ __launch_bounds__(kNT) void k_tsolve3(cpx<T>* __restrict__ C,
                                                  const cpx<T>* __restrict__ Bhat,
                                                  const cpx<T>* __restrict__ dhat,
@@ -257,12 +283,16 @@ __global__ __launch_bounds__(kNT) void k_tsolve3(cpx<T>* __restrict__ C,
   cpx<T>* s_tw = reinterpret_cast<cpx<T>*>(smem);
   T* lds = reinterpret_cast<T*>(s_tw + Gt.ntw);
   for (int i = threadIdx.x; i < Gt.ntw; i += kNT) s_tw[i] = twg[i];
+  if constexpr (FNL > 0) {   // C4: TC = 2, T = 42, K = FNL / 2 -- the index math compile-time
+    TC = 2;
+    K = FNL / 2;
+  }
   const int tile = blockIdx.x % xtiles;
   const int64_t rest = blockIdx.x / xtiles;
   const int y = (int)(rest % Yn);
   const int64_t p0 = (rest / Yn) * ppw;
   const int64_t p1 = min(npatch, p0 + ppw);
-  const int Tn = Gt.Y;
+  const int Tn = FNL > 0 ? 42 : Gt.Y;
   const int nc = min(TC, Xh - tile * TC);
   const int NL = K * TC;
   const int TT = Tn * TC;                                   // one (slice, y, tile) block
@@ -330,7 +360,8 @@ __global__ __launch_bounds__(kNT) void k_tsolve3(cpx<T>* __restrict__ C,
       const int b = tid % nb, grp = tid / nb;
       if (grp < G && b - (b / TC) * TC < nc) bh = Bhat[p * F3t + blk + b];
     }
-    fft_dir<T, kMaxB, -1, kMaxPass, kNT, 1, 1, RM>(lds, kModePlain, g, g, Gt, Gt.py, s_tw);
+    if constexpr (FNL > 0) tfft42<T, FNL, -1>(lds, s_tw);
+    else fft_dir<T, kMaxB, -1, kMaxPass, kNT, 1, 1, RM>(lds, kModePlain, g, g, Gt, Gt.py, s_tw);
     // per bin (t, c): w = (B - sum_k d_k C_k) sden, C_k <- C_k / P3 + conj(d_k) w; the
     // d_k of a thread's k range stay in registers between the two sweeps, partial sums
     // meet in LDS past the spectra
@@ -376,7 +407,8 @@ __global__ __launch_bounds__(kNT) void k_tsolve3(cpx<T>* __restrict__ C,
       }
     }
     lds_sync();
-    fft_dir<T, kMaxB, +1, kMaxPass, kNT, 1, 1, RM>(lds, kModePlain, g, g, Gt, Gt.py, s_tw);
+    if constexpr (FNL > 0) tfft42<T, FNL, +1>(lds, s_tw);
+    else fft_dir<T, kMaxB, +1, kMaxPass, kNT, 1, 1, RM>(lds, kModePlain, g, g, Gt, Gt.py, s_tw);
     tid = (int)threadIdx.x;
     asm volatile("" : "+v"(tid));
 #pragma unroll
@@ -505,11 +537,14 @@ hipError_t launch_tfft(const cpx<T>* src, cpx<T>* dst, int64_t nslices, int Yn, 
                        Yn, F2, tw, Gt);
   };
   const bool r42 = rm_fits(kRm42, Gt.py, Gt.Xh);
+  const bool f38 = r42 && tline42_ok(Gt, 38);
   if (sign < 0) {
-    if (r42) go(k_tfft<T, -1, kRm42>);
+    if (f38) go(k_tfft<T, -1, kRm42, 38>);
+    else if (r42) go(k_tfft<T, -1, kRm42>);
     else go(k_tfft<T, -1, kRmAll>);
   } else {
-    if (r42) go(k_tfft<T, 1, kRm42>);
+    if (f38) go(k_tfft<T, 1, kRm42, 38>);
+    else if (r42) go(k_tfft<T, 1, kRm42>);
     else go(k_tfft<T, 1, kRmAll>);
   }
   return hipGetLastError();
@@ -560,13 +595,14 @@ hipError_t launch_tsolve3(cpx<T>* C, const cpx<T>* Bhat, const cpx<T>* dhat, con
   };
   const bool r42 = rm_fits(kRm42, Gt2.py, Gt2.Xh);
   const bool small = tsolve3_ld(Gt2.Y, K, TC) <= 5 && tsolve3_kg(Gt2.Y, K, TC) <= 8;
-  if (r42 && small && dl) go(k_tsolve3<T, kRm42, 5, 8, true>);   // C4
-  else if (r42 && small) go(k_tsolve3<T, kRm42, 5, 8, false>);
-  else if (r42) go(k_tsolve3<T, kRm42, 8, 16, false>);
-  else if (small && dl) go(k_tsolve3<T, kRmAll, 5, 8, true>);
-  else if (small) go(k_tsolve3<T, kRmAll, 5, 8, false>);
-  else if (dl) go(k_tsolve3<T, kRmAll, 8, 16, true>);
-  else go(k_tsolve3<T, kRmAll, 8, 16, false>);
+  if (r42 && small && dl && TC == 2 && tline42_ok(Gt2, 98)) go(k_tsolve3<T, kRm42, 5, 8, true, 98>);   // C4
+  else if (r42 && small && dl) go(k_tsolve3<T, kRm42, 5, 8, true, 0>);
+  else if (r42 && small) go(k_tsolve3<T, kRm42, 5, 8, false, 0>);
+  else if (r42) go(k_tsolve3<T, kRm42, 8, 16, false, 0>);
+  else if (small && dl) go(k_tsolve3<T, kRmAll, 5, 8, true, 0>);
+  else if (small) go(k_tsolve3<T, kRmAll, 5, 8, false, 0>);
+  else if (dl) go(k_tsolve3<T, kRmAll, 8, 16, true, 0>);
+  else go(k_tsolve3<T, kRmAll, 8, 16, false, 0>);
   return hipGetLastError();
 }
 
