@@ -79,7 +79,7 @@ __device__ __forceinline__ void chol_blocked(cpx<T>* sG, int K) {
 #pragma unroll
         for (int c = 0; c < kCholNB; ++c) {
           const int j = j0 + c;
-          P[t][c] = (c < jb && r < K && r >= j) ? sG[pk_off(j, K) + r - j] : cpx<T>{(T)0, (T)0};
+          P[t][c] = ldc_if(c < jb && r < K && r >= j, sG + pk_off(j, K) + r - j);
         }
       }
 #pragma unroll
@@ -861,7 +861,7 @@ __global__ __launch_bounds__(64 * kWbWG) void k_gram_wb(const cpx<T>* __restrict
   cpx<T> m[kWbMaxNi];
 #pragma unroll
   for (int q = 0; q < kWbMaxNi; ++q)
-    m[q] = (lane < ni && q <= lane) ? sM[wave][min(lane, kWbMaxNi - 1) * kWbMaxNi + q] : zero;
+    m[q] = ldc_if(lane < ni && q <= lane, &sM[wave][min(lane, kWbMaxNi - 1) * kWbMaxNi + q]);
   // right-looking Cholesky M = L_M L_M^H across the lanes
 #pragma unroll
   for (int j = 0; j < kWbMaxNi; ++j) {
@@ -882,7 +882,11 @@ __global__ __launch_bounds__(64 * kWbWG) void k_gram_wb(const cpx<T>* __restrict
   if (lane < ni) {
 #pragma unroll
     for (int q = 0; q < kWbMaxNi; ++q)
-      if (q < ni) slot[ni * K + lane * ni + q] = (q <= lane) ? m[q] : zero;
+      if (q < ni) {
+        cpx<T> v = zero;
+        if (q <= lane) v = m[q];
+        slot[ni * K + lane * ni + q] = v;
+      }
   }
   // h[f][uv][k] = sum_p conj(A[p][k]) B[p][uv][f]
   for (int uv = 0; uv < NV; ++uv) {

@@ -378,7 +378,7 @@ __global__ __launch_bounds__(kNT) void k_tsolve3(cpx<T>* __restrict__ C,
     for (int j = 0; j < KMAX; ++j) {
       const int k = grp * kg + j;
       const bool ok = on && j < kg && k < K;
-      if constexpr (DL) dv[j] = ok ? sD[k * nb + b] : cpx<T>{(T)0, (T)0};
+      if constexpr (DL) dv[j] = ldc_if(ok, sD + k * nb + b);
       else dv[j] = ok ? dhat[(int64_t)k * F3t + f3] : cpx<T>{(T)0, (T)0};
     }
 #pragma unroll
