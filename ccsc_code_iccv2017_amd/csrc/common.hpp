@@ -33,6 +33,25 @@ __host__ __device__ __forceinline__ cpx<T> cmulc(cpx<T> a, cpx<T> b) {
 }
 template <typename T>
 __host__ __device__ __forceinline__ cpx<T> cadd(cpx<T> a, cpx<T> b) { return {a.x + b.x, a.y + b.y}; }
+// acc + a b and acc + conj(a) b as four FMAs (cadd(acc, cmul(a, b)) compiles to a mul, an FMA
+// and an add per component: the sum cannot be reassociated into the product)
+template <typename T>
+__host__ __device__ __forceinline__ cpx<T> cmac(cpx<T> acc, cpx<T> a, cpx<T> b) {
+  return {fma(a.x, b.x, fma(-a.y, b.y, acc.x)), fma(a.x, b.y, fma(a.y, b.x, acc.y))};
+}
+template <typename T>
+__host__ __device__ __forceinline__ cpx<T> cmacc(cpx<T> acc, cpx<T> a, cpx<T> b) {
+  return {fma(a.x, b.x, fma(a.y, b.y, acc.x)), fma(a.x, b.y, fma(-a.y, b.x, acc.y))};
+}
+// acc - a b and acc - conj(a) b, likewise
+template <typename T>
+__host__ __device__ __forceinline__ cpx<T> cmsub(cpx<T> acc, cpx<T> a, cpx<T> b) {
+  return {fma(-a.x, b.x, fma(a.y, b.y, acc.x)), fma(-a.x, b.y, fma(-a.y, b.x, acc.y))};
+}
+template <typename T>
+__host__ __device__ __forceinline__ cpx<T> cmsubc(cpx<T> acc, cpx<T> a, cpx<T> b) {
+  return {fma(-a.x, b.x, fma(-a.y, b.y, acc.x)), fma(-a.x, b.y, fma(a.y, b.x, acc.y))};
+}
 template <typename T>
 __host__ __device__ __forceinline__ cpx<T> csub(cpx<T> a, cpx<T> b) { return {a.x - b.x, a.y - b.y}; }
 template <typename T>

@@ -237,7 +237,7 @@ __global__ __launch_bounds__(kGramNT) void k_gram_chol(const cpx<T>* __restrict_
 #pragma unroll
         for (int u = 0; u < kGramTS; ++u)
 #pragma unroll
-          for (int v = 0; v < kGramTS; ++v) acc[u][v] = cadd(acc[u][v], cmulc(ai[u], aj[v]));
+          for (int v = 0; v < kGramTS; ++v) acc[u][v] = cmacc(acc[u][v], ai[u], aj[v]);
       }
     }
 #pragma unroll
@@ -246,7 +246,7 @@ __global__ __launch_bounds__(kGramNT) void k_gram_chol(const cpx<T>* __restrict_
       if (q < KV) {
         const int uv = q / K, k = q - uv * K;
         for (int pp = 0; pp < pc; ++pp)
-          hacc[i] = cadd(hacc[i], cmulc(sA[pp * K + k], sB[pp * NV + uv]));
+          hacc[i] = cmacc(hacc[i], sA[pp * K + k], sB[pp * NV + uv]);
       }
     }
   }
@@ -398,7 +398,7 @@ __global__ __launch_bounds__(256) void k_dsolve(const cpx<T>* __restrict__ L,
 #pragma unroll
           for (int u = 0; u < RPL; ++u) {
             const int i = lane + 64 * u;
-            if (i > j && i < K) x[v][u] = csub(x[v][u], cmul(lc[jj][u], xj));
+            if (i > j && i < K) x[v][u] = cmsub(x[v][u], lc[jj][u], xj);
           }
         }
       }
@@ -433,7 +433,7 @@ __global__ __launch_bounds__(256) void k_dsolve(const cpx<T>* __restrict__ L,
 #pragma unroll
           for (int u = 0; u < RPL; ++u) {
             const int i = lane + 64 * u;
-            if (i > j && i < K) part = cadd(part, cmulc(lc[jj][u], x[v][u]));
+            if (i > j && i < K) part = cmacc(part, lc[jj][u], x[v][u]);
           }
           part.x = wave_sum_dpp(part.x);
           part.y = wave_sum_dpp(part.y);
@@ -469,7 +469,7 @@ __global__ __launch_bounds__(256) void k_dsolve(const cpx<T>* __restrict__ L,
           if (lane == src) put_reg<T, RPL>(x[v], tp, xp);
 #pragma unroll
           for (int u = 0; u < RPL; ++u)
-            if (lane + 64 * u < p) x[v][u] = csub(x[v][u], cmulc(lr[jj][u], xp));
+            if (lane + 64 * u < p) x[v][u] = cmsubc(x[v][u], lr[jj][u], xp);
         }
       }
     }
@@ -668,7 +668,7 @@ __global__ __launch_bounds__(256) void k_dsolve_tile(const cpx<double>* __restri
   auto diag_fwd = [&](const cpx<double> (&Mt)[4], const cpx<double>* vbuf, cpx<double>* ybuf) {
     cpx<double> v = zero;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) v = cadd(v, cmul(Mt[q], vbuf[4 * cg + q]));
+    for (int q = 0; q < 4; ++q) v = cmac(v, Mt[q], vbuf[4 * cg + q]);
     v = {xrow_sum(v.x), xrow_sum(v.y)};
     if (cg == 0) ybuf[row] = v;
   };
@@ -684,7 +684,7 @@ __global__ __launch_bounds__(256) void k_dsolve_tile(const cpx<double>* __restri
       if (tJ[s] == J && tI[s] > J) {
         cpx<double> v = zero;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) v = cadd(v, cmul(Lt[s][q], yJ[4 * cg + q]));
+        for (int q = 0; q < 4; ++q) v = cmac(v, Lt[s][q], yJ[4 * cg + q]);
         v = {xrow_sum(v.x), xrow_sum(v.y)};
         cpx<double>* rI = sr + 16 * tI[s];
         if (cg == 0) rI[row] = csub(rI[row], v);
@@ -850,7 +850,7 @@ __global__ __launch_bounds__(64 * kWbWG) void k_gram_wb(const cpx<T>* __restrict
       if (p < ni) {
         cpx<T> part = zero;
 #pragma unroll
-        for (int u = 0; u < RPL; ++u) part = cadd(part, cmulc(a[q][u], a[p][u]));
+        for (int u = 0; u < RPL; ++u) part = cmacc(part, a[q][u], a[p][u]);
         cpx<T> v = {wave_sum_dpp(part.x), wave_sum_dpp(part.y)};
         if (p == q) v = {v.x + rho, (T)0};
         if (lane == 0) sM[wave][p * kWbMaxNi + q] = v;
@@ -874,7 +874,7 @@ __global__ __launch_bounds__(64 * kWbWG) void k_gram_wb(const cpx<T>* __restrict
       for (int q = 0; q < kWbMaxNi; ++q) {
         if (q > j && q < ni) {
           const cpx<T> lq = readlane_c(m[j], q);                      // L[q][j]
-          if (lane >= q && lane < ni) m[q] = csub(m[q], cmul(m[j], cpx<T>{lq.x, -lq.y}));
+          if (lane >= q && lane < ni) m[q] = cmsub(m[q], m[j], cpx<T>{lq.x, -lq.y});
         }
       }
     }
@@ -898,7 +898,7 @@ __global__ __launch_bounds__(64 * kWbWG) void k_gram_wb(const cpx<T>* __restrict
       if (p < ni) {
         const cpx<T> b = Bh[((int64_t)p * NV + uv) * F + f];
 #pragma unroll
-        for (int u = 0; u < RPL; ++u) acc[u] = cadd(acc[u], cmulc(a[p][u], b));
+        for (int u = 0; u < RPL; ++u) acc[u] = cmacc(acc[u], a[p][u], b);
       }
     }
 #pragma unroll
@@ -972,7 +972,7 @@ __global__ __launch_bounds__(64 * kWbWG) void k_dsolve_wb(const cpx<T>* __restri
         for (int v = 0; v < NVB; ++v) {
           cpx<T> part = zero;
 #pragma unroll
-          for (int u = 0; u < RPL; ++u) part = cadd(part, cmul(a[p][u], r[v][u]));
+          for (int u = 0; u < RPL; ++u) part = cmac(part, a[p][u], r[v][u]);
           const cpx<T> s = {wave_sum_dpp(part.x), wave_sum_dpp(part.y)};
           if (lane == p) t[v] = s;
         }
@@ -987,7 +987,7 @@ __global__ __launch_bounds__(64 * kWbWG) void k_dsolve_wb(const cpx<T>* __restri
         for (int v = 0; v < NVB; ++v) {
           const cpx<T> yj = cscale(readlane_c(t[v], j), dj);
           if (lane == j) t[v] = yj;
-          if (lane > j && lane < ni) t[v] = csub(t[v], cmul(lrow[j], yj));
+          if (lane > j && lane < ni) t[v] = cmsub(t[v], lrow[j], yj);
         }
       }
     }
@@ -999,7 +999,7 @@ __global__ __launch_bounds__(64 * kWbWG) void k_dsolve_wb(const cpx<T>* __restri
         for (int v = 0; v < NVB; ++v) {
           const cpx<T> sj = cscale(readlane_c(t[v], j), dj);
           if (lane == j) t[v] = sj;
-          if (lane < j) t[v] = csub(t[v], cmulc(lcol[j], sj));         // conj(L_M[j][lane])
+          if (lane < j) t[v] = cmsubc(t[v], lcol[j], sj);         // conj(L_M[j][lane])
         }
       }
     }
@@ -1011,7 +1011,7 @@ __global__ __launch_bounds__(64 * kWbWG) void k_dsolve_wb(const cpx<T>* __restri
         for (int v = 0; v < NVB; ++v) {
           const cpx<T> sp = readlane_c(t[v], p);
 #pragma unroll
-          for (int u = 0; u < RPL; ++u) r[v][u] = csub(r[v][u], cmulc(a[p][u], sp));
+          for (int u = 0; u < RPL; ++u) r[v][u] = cmsubc(r[v][u], a[p][u], sp);
         }
       }
     }
@@ -1153,7 +1153,7 @@ __global__ __launch_bounds__(64 * kWbWG) __attribute__((amdgpu_waves_per_eu(KR <
       t[j] = cscale(t[j], dinv[j]);
 #pragma unroll
       for (int q = j + 1; q < kWbMaxNi; ++q)
-        if (q < ni) t[q] = csub(t[q], cmul(lm[q * ni + j], t[j]));
+        if (q < ni) t[q] = cmsub(t[q], lm[q * ni + j], t[j]);
     }
   }
 #pragma unroll
@@ -1161,7 +1161,7 @@ __global__ __launch_bounds__(64 * kWbWG) __attribute__((amdgpu_waves_per_eu(KR <
     if (j < ni) {
       t[j] = cscale(t[j], dinv[j]);
 #pragma unroll
-      for (int q = 0; q < j; ++q) t[q] = csub(t[q], cmulc(lm[j * ni + q], t[j]));   // conj(L_M[j][q])
+      for (int q = 0; q < j; ++q) t[q] = cmsubc(t[q], lm[j * ni + q], t[j]);   // conj(L_M[j][q])
     }
   }
 #pragma unroll

@@ -272,7 +272,7 @@ __global__ __launch_bounds__(kGcNT, GcShape<TM>::WGS) void k_gram_chol_mf(const 
         const int pv = min(kGcPC, ni - c * kGcPC);
 #pragma unroll 4
         for (int pp = 0; pp < pv; ++pp)
-          hacc[i] = cadd(hacc[i], cmulc(a[pp * kGcLD + k], b[pp * NV + uv]));
+          hacc[i] = cmacc(hacc[i], a[pp * kGcLD + k], b[pp * NV + uv]);
       }
     }
     if (c + 1 < nch) stage(buf ^ 1);
@@ -311,7 +311,7 @@ __global__ __launch_bounds__(kGcNT, GcShape<TM>::WGS) void k_gram_chol_mf(const 
       cpx<double> x[16];
 #pragma unroll
       for (int c = 0; c < 16; ++c)
-        x[c] = mine ? P[ti * kGcTSZ + c * kGcTS + row] : cpx<double>{1.0, 0.0};
+        x[c] = mine ? ldc_if(true, P + ti * kGcTSZ + c * kGcTS + row) : cpx<double>{1.0, 0.0};
       // right-looking in registers: once column c is final, every row r loses
       // L[r][c] conj(L[c2][c]) from its column c2 > c, L[c2][c] broadcast from lane c2 by
       // v_readlane -- no LDS round trip on the column-to-column chain; 1/sqrt of the
@@ -327,8 +327,10 @@ __global__ __launch_bounds__(kGcNT, GcShape<TM>::WGS) void k_gram_chol_mf(const 
 #pragma unroll
         for (int c2 = c + 1; c2 < 16; ++c2) {
           const double lx = rdl(x[c].x, c2), ly = rdl(x[c].y, c2);   // L[c2][c]
-          x[c2].x -= x[c].x * lx + x[c].y * ly;
-          x[c2].y -= x[c].y * lx - x[c].x * ly;
+          // x[c2] -= x[c] conj(L[c2][c]) as four FMAs (the expression form compiled to
+          // mul + fma + add per component)
+          x[c2].x = fma(-x[c].x, lx, fma(-x[c].y, ly, x[c2].x));
+          x[c2].y = fma(-x[c].y, lx, fma(x[c].x, ly, x[c2].y));
         }
       }
       const int gr_ = 16 * ti + row;

@@ -245,12 +245,12 @@ __global__ void k_zsolve3(cpx<T>* __restrict__ C, const cpx<T>* __restrict__ Bha
   if (f >= F3) return;
   cpx<T>* Cp = C + p * K * F3 + f;
   cpx<T> acc = {(T)0, (T)0};
-  for (int k = 0; k < K; ++k) acc = cadd(acc, cmul(dhat[(int64_t)k * F3 + f], Cp[(int64_t)k * F3]));
+  for (int k = 0; k < K; ++k) acc = cmac(acc, dhat[(int64_t)k * F3 + f], Cp[(int64_t)k * F3]);
   const cpx<T> w = cscale(csub(Bhat[p * F3 + f], acc), sden[f]);
   for (int k = 0; k < K; ++k) {
     const cpx<T> c = Cp[(int64_t)k * F3];
     const cpx<T> d = dhat[(int64_t)k * F3 + f];
-    Cp[(int64_t)k * F3] = cadd(cscale(c, invP3), cmulc(d, w));
+    Cp[(int64_t)k * F3] = cmacc(cscale(c, invP3), d, w);
   }
 }
 
@@ -384,7 +384,7 @@ __global__ __launch_bounds__(kNT) void k_tsolve3(cpx<T>* __restrict__ C,
 #pragma unroll
     for (int j = 0; j < KMAX; ++j) {
       const int k = grp * kg + j;
-      if (on && j < kg && k < K) acc = cadd(acc, cmul(dv[j], lds_cpx(row + 2 * k * TC, 1)));
+      if (on && j < kg && k < K) acc = cmac(acc, dv[j], lds_cpx(row + 2 * k * TC, 1));
     }
     if (grp < G) part[grp * nb + b] = acc;
     lds_sync();
@@ -402,7 +402,7 @@ __global__ __launch_bounds__(kNT) void k_tsolve3(cpx<T>* __restrict__ C,
         const int k = grp * kg + j;
         if (j < kg && k < K) {
           const cpx<T> cv = lds_cpx(row + 2 * k * TC, 1);
-          lds_cpx_store(row + 2 * k * TC, 1, cadd(cscale(cv, invP3), cmulc(dv[j], w)));
+          lds_cpx_store(row + 2 * k * TC, 1, cmacc(cscale(cv, invP3), dv[j], w));
         }
       }
     }
@@ -451,7 +451,7 @@ __global__ void k_corr_sum(const cpx<T>* __restrict__ Zh, const cpx<T>* __restri
   const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (f >= F3) return;
   cpx<T> acc = {(T)0, (T)0};
-  for (int k = 0; k < K; ++k) acc = cadd(acc, cmul(Zh[(int64_t)k * F3 + f], dhat[(int64_t)k * F3 + f]));
+  for (int k = 0; k < K; ++k) acc = cmac(acc, Zh[(int64_t)k * F3 + f], dhat[(int64_t)k * F3 + f]);
   out[f] = acc;
 }
 

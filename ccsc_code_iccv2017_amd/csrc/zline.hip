@@ -468,7 +468,7 @@ __global__ __launch_bounds__(zl::NT) __attribute__((amdgpu_waves_per_eu(3, 3))) 
       const cpx<T>* dk = dhat + (int64_t)k * zl::F;
       const uint32_t bo = (uint32_t)(c * 11 + s9) * 16u;
       fwd_line<T, zl::RS, true>(col, Ey, s9, [&](int k1, cpx<T> cb) {
-        acc[k1] = cadd(acc[k1], cmul(fld<cpx<T>>(dk, bo, k1 * 616 * 16), cb));
+        acc[k1] = cmac(acc[k1], fld<cpx<T>>(dk, bo, k1 * 616 * 16), cb);
       });
     }
   }
