@@ -72,6 +72,13 @@ __device__ __forceinline__ double clamp_t(double a, double theta) {
   return r;
 }
 
+// the z-step's LDS as bytes (32-bit offsets: no 64-bit address arithmetic)
+template <typename T>
+__device__ __forceinline__ cpx<T>& lds_cpx_at(uint32_t byte_off) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  return *reinterpret_cast<cpx<T>*>(smem + byte_off);
+}
+
 template <typename T, int R, int SIGN, typename Sink>
 __device__ __forceinline__ void zdft(cpx<T> (&v)[R], Sink&& sink) {
   dft_sink<T, R, SIGN>(v, sink);
@@ -84,8 +91,9 @@ __device__ __forceinline__ void wave_lds_fence() {
 }
 
 // Forward 110-point transform of one line, layout A (v[n2], lane n1 = s < 10)
-// -> layout B (out[k1], lane k2 = s <= 10).  E: the line's 110 exchange slots,
-// slot n1*11 + k2 at E[(n1*11 + k2) * ES].
+// -> layout B (out[k1], lane k2 = s <= 10).  eb: LDS byte offset of the line's 110
+// exchange slots, slot n1*11 + k2 at complex (n1*11 + k2) * ES from it (32-bit offsets:
+// the slot's constant part folds into the instruction's offset field).
 // Idle lanes (lane 10 of a line in layout A, lanes 55..63, the clamped lines of the
 // last wave) run on clamped indices and so duplicate a real lane exactly: their
 // LDS and global stores write the same value to the same address, no guards.
@@ -94,14 +102,15 @@ __device__ __forceinline__ void wave_lds_fence() {
 // separation of the odd rows, see P7): in layout B they are register n1 (compile time),
 // so the factor -i is a free swap + negate of the DFT-10's operands.
 template <typename T, int ES, bool ODDROT = false, typename Sink>
-__device__ __forceinline__ void fwd_line(cpx<T> (&v)[11], cpx<T>* E, int s, Sink&& sink) {
+__device__ __forceinline__ void fwd_line(cpx<T> (&v)[11], uint32_t eb, int s, Sink&& sink) {
   const int sa = min(s, 9);
-  zdft<T, 11, -1>(v, [&](int k2, cpx<T> val) { E[(sa * 11 + k2) * ES] = val; });
+  const uint32_t ea = eb + (uint32_t)(sa * 11 * ES) * 16u, es = eb + (uint32_t)(s * ES) * 16u;
+  zdft<T, 11, -1>(v, [&](int k2, cpx<T> val) { lds_cpx_at<T>(ea + (uint32_t)(k2 * ES * 16)) = val; });
   wave_lds_fence();
   cpx<T> in[10];
 #pragma unroll
   for (int n1 = 0; n1 < 10; ++n1) {
-    const cpx<T> w = E[(n1 * 11 + s) * ES];
+    const cpx<T> w = lds_cpx_at<T>(es + (uint32_t)(n1 * 11 * ES * 16));
     in[n1] = (ODDROT && (n1 & 1)) ? cpx<T>{w.y, -w.x} : w;
   }
   zdft<T, 10, -1>(in, sink);
@@ -110,13 +119,15 @@ __device__ __forceinline__ void fwd_line(cpx<T> (&v)[11], cpx<T>* E, int s, Sink
 // Inverse (unnormalised) 110-point transform, layout B (in[k1], lane k2 = s)
 // -> layout A (out[n2], lane n1 = s < 10).
 template <typename T, int ES, typename Sink>
-__device__ __forceinline__ void inv_line(cpx<T> (&in)[10], cpx<T>* E, int s, Sink&& sink) {
-  zdft<T, 10, +1>(in, [&](int n1, cpx<T> val) { E[(n1 * 11 + s) * ES] = val; });
+__device__ __forceinline__ void inv_line(cpx<T> (&in)[10], uint32_t eb, int s, Sink&& sink) {
+  const uint32_t es = eb + (uint32_t)(s * ES) * 16u;
+  zdft<T, 10, +1>(in, [&](int n1, cpx<T> val) { lds_cpx_at<T>(es + (uint32_t)(n1 * 11 * ES * 16)) = val; });
   wave_lds_fence();
   const int sa = min(s, 9);
+  const uint32_t ea = eb + (uint32_t)(sa * 11 * ES) * 16u;
   cpx<T> v[11];
 #pragma unroll
-  for (int k2 = 0; k2 < 11; ++k2) v[k2] = E[(sa * 11 + k2) * ES];
+  for (int k2 = 0; k2 < 11; ++k2) v[k2] = lds_cpx_at<T>(ea + (uint32_t)(k2 * ES * 16));
   zdft<T, 11, +1>(v, sink);
 }
 
@@ -142,12 +153,6 @@ __device__ __forceinline__ int xoff(int l) { return 110 * l + (l < 2 ? 0 : l == 
 __device__ __forceinline__ int zoff(int l) { return 110 * l + (l < 1 ? 0 : l < 4 ? 5 + l : 11); }
 constexpr int kZlWR = 10 * zl::RS;   // complex slots of a wave's ten T rows
 
-// the z-step's LDS as bytes (32-bit offsets: no 64-bit address arithmetic)
-template <typename T>
-__device__ __forceinline__ cpx<T>& lds_cpx_at(uint32_t byte_off) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  return *reinterpret_cast<cpx<T>*>(smem + byte_off);
-}
 // 16-B global access at a 32-bit byte offset from a wave-uniform base (saddr form:
 // SGPR base + one VGPR offset, no 64-bit VGPR address per access).
 template <typename V>
@@ -196,7 +201,8 @@ typedef double nt_d2 __attribute__((ext_vector_type(2)));
 template <typename V>
 __device__ __forceinline__ void sst2(void* base, uint32_t lane, uint32_t reg, V v) {
   const nt_d2 r = {v.x, v.y};
-  __builtin_nontemporal_store(r, reinterpret_cast<nt_d2*>(reinterpret_cast<char*>(base) + lane + reg));
+  // one 32-bit offset: the saddr form (SGPR base + VGPR offset), no 64-bit address add per store
+  __builtin_nontemporal_store(r, reinterpret_cast<nt_d2*>(reinterpret_cast<char*>(base) + (uint32_t)(lane + reg)));
 }
 
 // an opaque copy of a lane index: per-lane address math is redone where it is used
@@ -287,8 +293,10 @@ __global__ __launch_bounds__(zl::NT) __attribute__((amdgpu_waves_per_eu(3, 3))) 
     const int sb = min(s, 10), sa = min(s, 9);
     const int c = min(5 * wave + l, 55);   // y-line (column)
     const int j = min(5 * wave + l, 54);   // x-line (row pair)
-    cpx<T>* Ey = sT + tcol(c);   // the line's own T column (where P1 stores): slot i at row i
-    cpx<T>* Ex = sT + kZlWR * min(wave, 10) + xoff(l);   // the wave's rows, line l
+    // the line's own T column (where P1 stores; slot i at row i) and the x-line's slots in
+    // the wave's rows, as LDS byte offsets
+    const uint32_t Ey = (uint32_t)tcol(c) * 16u;
+    const uint32_t Ex = (uint32_t)(kZlWR * min(wave, 10) + xoff(l)) * 16u;
     const int64_t sl = (p * K + k) * zl::P;
     cpx<T> zc[11];   // c = u - y of the row pair (x-lines, layout A) for the R2C
     const uint32_t po = (uint32_t)(j * 10 + fresh(sa)) * 16u;   // pair n2 at po + n2*550*16
@@ -318,7 +326,7 @@ __global__ __launch_bounds__(zl::NT) __attribute__((amdgpu_waves_per_eu(3, 3))) 
 #pragma unroll
       for (int k1 = 0; k1 < 10; ++k1) b[k1] = cmulc(b[k1], wv[k1]);
       inv_line<T, zl::RS>(b, Ey, sb, [&](int n2, cpx<T> val) {
-        sT[mod110(11 * sa + 10 * n2) * zl::RS + tcol(c)] = val;
+        lds_cpx_at<T>((uint32_t)(mod110(11 * sa + 10 * n2) * zl::RS) * 16u + Ey) = val;
       });
       zl_sync();   // P2
       if (xwave) {
@@ -432,8 +440,9 @@ __global__ __launch_bounds__(zl::NT) __attribute__((amdgpu_waves_per_eu(3, 3))) 
     // ---- P5: x-R2C of the row pair -> Z_j into rows 2j, 2j+1 of T ----
     if (xwave) {
       const int s5 = fresh(sb);
-      cpx<T>* r0 = sT + kZlWR * min(wave, 10) + zoff(l);   // Z_j in layout-B slot order (zslot)
-      fwd_line<T, 1>(zc, Ex, s5, [&](int k1, cpx<T> val) { r0[k1 * 11 + s5] = val; });
+      // Z_j in layout-B slot order (zslot)
+      const uint32_t r0 = (uint32_t)(kZlWR * min(wave, 10) + zoff(l) + s5) * 16u;
+      fwd_line<T, 1>(zc, Ex, s5, [&](int k1, cpx<T> val) { lds_cpx_at<T>(r0 + (uint32_t)(k1 * 176)) = val; });
     }
     zl_sync();   // P6
     // ---- P7: column c, rows y = n1 + 10 n2: two-for-one separation ----
@@ -449,12 +458,17 @@ __global__ __launch_bounds__(zl::NT) __attribute__((amdgpu_waves_per_eu(3, 3))) 
       // all 22 reads first, then the arithmetic: the scheduler otherwise interleaves them
       // pairwise with a full lgkmcnt wait each (eleven LDS round trips per wave)
       cpx<T> z1[11], z2[11];
+      // row y = (11 n1 + 10 n2) mod 110: pair y >> 1 is line n1 >> 1 of wave (n1 + n2) mod 11,
+      // i.e. wave n1 + n2 stepping by one per n2 and wrapping once (at n2 = 11 - n1): the
+      // bases b1, b2 plus a compile-time step, minus one wrap where n1 >= 11 - n2
+      const uint32_t e0 = (uint32_t)(kZlWR * n1 + zoff(n1 >> 1)) * 16u;
+      const uint32_t b1 = e0 + a1, b2 = e0 + a2;
+      constexpr uint32_t kStep = kZlWR * 16u, kWrap = 11u * kZlWR * 16u;
 #pragma unroll
       for (int n2 = 0; n2 < 11; ++n2) {
-        // row y = (11 n1 + 10 n2) mod 110: pair y >> 1 is line n1 >> 1 of wave (n1 + n2) mod 11
-        const uint32_t e7 = (uint32_t)((kZlWR * (n1 + n2 >= 11 ? n1 + n2 - 11 : n1 + n2) + zoff(n1 >> 1)) * 16);
-        z1[n2] = lds_cpx_at<T>(e7 + a1);
-        z2[n2] = lds_cpx_at<T>(e7 + a2);
+        const uint32_t w = (n2 > 0 && n1 >= 11 - n2) ? kWrap : 0u;
+        z1[n2] = lds_cpx_at<T>(b1 - w + n2 * kStep);
+        z2[n2] = lds_cpx_at<T>(b2 - w + n2 * kStep);
       }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -565,8 +579,8 @@ __global__ __launch_bounds__(zl::NT) void k_zhat_line(const T* __restrict__ A,
     const int sb = min(s, 10), sa = min(s, 9);
     const int c = min(5 * wave + l, 55);
     const int j = min(5 * wave + l, 54);
-    cpx<T>* Ey = sT + tcol(c);
-    cpx<T>* Ex = sT + 10 * min(wave, 10) * zl::RS + l * 110;
+    const uint32_t Ey = (uint32_t)tcol(c) * 16u;
+    const uint32_t Ex = (uint32_t)(10 * min(wave, 10) * zl::RS + l * 110) * 16u;
     const int64_t sl = (p * K + k) * zl::P;
     if (xwave) {
       // ---- P4/P5: c = u - y of row pair j (layout A) -> x-R2C -> rows 2j, 2j+1 of T ----
@@ -578,8 +592,8 @@ __global__ __launch_bounds__(zl::NT) void k_zhat_line(const T* __restrict__ A,
         zc[n2] = {fma((T)-2, clamp_t(a.x, theta), a.x), fma((T)-2, clamp_t(a.y, theta), a.y)};
       }
       const int s5 = fresh(sb);
-      cpx<T>* r0 = sT + kZlWR * min(wave, 10) + zoff(l);
-      fwd_line<T, 1>(zc, Ex, s5, [&](int k1, cpx<T> val) { r0[k1 * 11 + s5] = val; });
+      const uint32_t r0 = (uint32_t)(kZlWR * min(wave, 10) + zoff(l) + s5) * 16u;
+      fwd_line<T, 1>(zc, Ex, s5, [&](int k1, cpx<T> val) { lds_cpx_at<T>(r0 + (uint32_t)(k1 * 176)) = val; });
     }
     lds_sync();
     // ---- P7: column c, rows y = n1 + 10 n2: two-for-one separation ----
