@@ -1082,12 +1082,15 @@ __global__ __launch_bounds__(64 * kWbWG) __attribute__((amdgpu_waves_per_eu(KR <
   auto at = [](const cpx<T>* base, uint32_t boff) -> const cpx<T>& {
     return *reinterpret_cast<const cpx<T>*>(reinterpret_cast<const char*>(base) + boff);
   };
-  // lane offsets of row i of the lane's segment: hf + i, Cb + i cs (segment start folded in)
+  // row i of the lane's segment is k = min(k0 + i, K - 1) (rows past K are clamped and
+  // zeroed); the wave-uniform base takes row u = min(i, K - 1) and the lane offset the
+  // difference k - u >= 0 (min is monotone and k0 >= 0), so the 32-bit offset never wraps
+  auto urow = [&](int i) { return min(i, K - 1); };
   auto offh = [&](int i) {
-    return (uint32_t)(lv * K + min(k0 + i, K - 1) - i) * (uint32_t)sizeof(cpx<T>);
+    return (uint32_t)(lv * K + min(k0 + i, K - 1) - urow(i)) * (uint32_t)sizeof(cpx<T>);
   };
   auto offc = [&](int i) {
-    return (uint32_t)(lv * F + (min(k0 + i, K - 1) - i) * cs) * (uint32_t)sizeof(cpx<T>);
+    return (uint32_t)(lv * F + (min(k0 + i, K - 1) - urow(i)) * cs) * (uint32_t)sizeof(cpx<T>);
   };
   // r = h + rho c in chunks of kWbvCH rows (sched_barrier: the compiler would otherwise
   // hoist every load of r to the top, 8 KR registers in flight)
@@ -1107,8 +1110,8 @@ __global__ __launch_bounds__(64 * kWbWG) __attribute__((amdgpu_waves_per_eu(KR <
 #pragma unroll
     for (int i = 0; i < kWbvCH; ++i) {
       const int ii = ch * kWbvCH + i;
-      cb[i] = at(Cb + ii * cs, offc(ii));
-      hb[i] = at(hf + ii, offh(ii));
+      cb[i] = at(Cb + urow(ii) * cs, offc(ii));
+      hb[i] = at(hf + urow(ii), offh(ii));
     }
   };
   load(0);
@@ -1186,7 +1189,7 @@ __global__ __launch_bounds__(64 * kWbWG) __attribute__((amdgpu_waves_per_eu(KR <
           x.y = fma(-a.x, t[p].y, fma(a.y, t[p].x, x.y));
         }
         __builtin_amdgcn_sched_barrier(0);
-        *reinterpret_cast<cpx<T>*>(reinterpret_cast<char*>(Db + ii * cs) + offc(ii)) = cscale(x, irho);
+        *reinterpret_cast<cpx<T>*>(reinterpret_cast<char*>(Db + urow(ii) * cs) + offc(ii)) = cscale(x, irho);
       }
     }
   }

@@ -98,7 +98,12 @@ def test_learn_2d_matches_oracle(gpu_ctx, variant, sb, psf, K, n, ni):
 
 @pytest.mark.parametrize("sb,UV,psf,K,n", [((10, 9), 2, 5, 3, 4), ((9, 9), 3, 5, 2, 9),
                                            ((64, 64), 5, 11, 4, 4),
-                                           ((10, 9), 2, 5, 8, 4)])     # Woodbury, 4 views
+                                           ((10, 9), 2, 5, 8, 4),      # Woodbury, 4 views
+                                           # Woodbury d-solve over the views (dstep.hip
+                                           # k_dsolve_wbv): 36 views = whole-wave lanes
+                                           # (H = 1), K = 40 = two row segments of 20
+                                           ((8, 8), 6, 3, 8, 4), ((8, 8), 6, 3, 40, 4),
+                                           ((8, 7), 2, 3, 40, 4)])
 def test_learn_4d_matches_oracle(gpu_ctx, sb, UV, psf, K, n):
     """4D light-field learner (L4:1-212): spatial-only convolution over U x V views,
     per-view D-solves sharing one factor, diagonal z-solve (Q7), per-slice projection (Q10)."""
