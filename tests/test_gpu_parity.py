@@ -96,6 +96,29 @@ def test_learn_2d_matches_oracle(gpu_ctx, variant, sb, psf, K, n, ni):
     np.testing.assert_allclose(it_e["trace"]["obj_z"], np.array(tr_o["obj_z"]), rtol=1e-9)
 
 
+def test_learn_4d_cholesky_many_views_matches_oracle(gpu_ctx):
+    """The K x K D-factor with many right-hand sides per frequency (4D, 25 views, K = 12,
+    CCSC_DFACTOR_CHOLESKY): K NV = 300 > 256 takes gramchol.hip's eight h slots per thread
+    (HP = 8) beside the Gauss Gram; against the oracle's pinv form."""
+    from ccsc_code_iccv2017_amd import learners as E
+    rng = np.random.default_rng(12)
+    sb, UV, psf, K, n = (8, 8), 5, 3, 12, 4
+    r = psf // 2
+    X, Y = sb[0] + 2 * r, sb[1] + 2 * r
+    b = rng.standard_normal((sb[0], sb[1], UV, UV, n))
+    init = {"d": rng.standard_normal((psf, psf, UV, UV, K)),
+            "z": rng.standard_normal((X, Y, 1, 1, K, n))}
+    ks = [psf, psf, UV, UV, K]
+    d_o, z_o, DZ_o, obj_o, it_o, tr_o = O.learn_4d(b, ks, 1.0, 1.0, 2, 0.0, "all", init,
+                                                   trace_objective=True)
+    d_e, z_e, DZ_e, obj_e, it_e = E.admm_learn_conv4D_lightfield(b, ks, 1.0, 1.0, 2, 0.0, "all",
+                                                                 init, trace_objective=True,
+                                                                 ctx=gpu_ctx, dfactor="cholesky")
+    assert _rel(d_e, d_o) < 1e-7
+    assert _rel(z_e.real, z_o.real) < 1e-7
+    np.testing.assert_allclose(it_e["trace"]["obj_z"], np.array(tr_o["obj_z"]), rtol=1e-9)
+
+
 @pytest.mark.parametrize("sb,UV,psf,K,n", [((10, 9), 2, 5, 3, 4), ((9, 9), 3, 5, 2, 9),
                                            ((64, 64), 5, 11, 4, 4),
                                            ((10, 9), 2, 5, 8, 4),      # Woodbury, 4 views
