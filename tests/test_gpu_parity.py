@@ -97,12 +97,13 @@ def test_learn_2d_matches_oracle(gpu_ctx, variant, sb, psf, K, n, ni):
 
 
 def test_learn_4d_cholesky_many_views_matches_oracle(gpu_ctx):
-    """The K x K D-factor with many right-hand sides per frequency (4D, 25 views, K = 12,
-    CCSC_DFACTOR_CHOLESKY): K NV = 300 > 256 takes gramchol.hip's eight h slots per thread
-    (HP = 8) beside the Gauss Gram; against the oracle's pinv form."""
+    """The K x K D-factor with many right-hand sides per frequency (4D, 16 views, K = 20,
+    CCSC_DFACTOR_CHOLESKY): K NV = 320 > 256 takes gramchol.hip's eight h slots per thread
+    (HP = 8) beside the Gauss Gram (NV <= 16: the MFMA kernel; more views take the VALU
+    k_gram_chol); against the oracle's pinv form."""
     from ccsc_code_iccv2017_amd import learners as E
     rng = np.random.default_rng(12)
-    sb, UV, psf, K, n = (8, 8), 5, 3, 12, 4
+    sb, UV, psf, K, n = (8, 8), 4, 3, 20, 4
     r = psf // 2
     X, Y = sb[0] + 2 * r, sb[1] + 2 * r
     b = rng.standard_normal((sb[0], sb[1], UV, UV, n))
