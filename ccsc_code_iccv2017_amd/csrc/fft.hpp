@@ -477,8 +477,10 @@ __host__ __device__ constexpr int pfa_slots(int nlines, int M, int QP) {
   return ((M - 1) / 2 + QP - 1) / QP * 2 * ((nlines + 63) / 64 * 64);
 }
 
+// gi: where the radix-2 pass left the inputs (the fixed 74-point x pass stores them
+// line-minor so the 37 reads per task are lane-contiguous; g otherwise); g: the output.
 template <typename T, int M, int SIGN, int QP, int NT>
-__device__ __forceinline__ void fft_pass_pfa(T* lds, const LineGeom& g) {
+__device__ __forceinline__ void fft_pass_pfa(T* lds, const LineGeom& g, const LineGeom& gi) {
   constexpr int H = (M - 1) / 2;
   constexpr int NG = (H + QP - 1) / QP;
   const int nl = g.nlines;
@@ -490,6 +492,7 @@ __device__ __forceinline__ void fft_pass_pfa(T* lds, const LineGeom& g) {
   const int line = o % lpad;
   const bool on = grp < NG && line < nl;
   T* base = lds + line * g.lstride;
+  const T* ibase = lds + line * gi.lstride;
   const int es = g.estride, im = g.imoff;
   cpx<T> A[QP], S[QP], dc = {(T)0, (T)0};
 #pragma unroll
@@ -497,7 +500,7 @@ __device__ __forceinline__ void fft_pass_pfa(T* lds, const LineGeom& g) {
   auto in = [&](auto n2c, auto k1c) {
     constexpr int n2 = decltype(n2c)::value, kk = decltype(k1c)::value;
     constexpr int j = (2 * n2) % M;
-    cpx<T> v = lds_cpx(base + (2 * j + kk) * es, im);
+    cpx<T> v = lds_cpx(ibase + (2 * j + kk) * gi.estride, gi.imoff);
     if constexpr (kk == 1 && 2 * n2 >= M) v = {-v.x, -v.y};
     return v;
   };
@@ -566,6 +569,11 @@ __device__ __forceinline__ void fft_pass_pfa(T* lds, const LineGeom& g) {
     });
   }
   lds_sync();
+}
+
+template <typename T, int M, int SIGN, int QP, int NT>
+__device__ __forceinline__ void fft_pass_pfa(T* lds, const LineGeom& g) {
+  fft_pass_pfa<T, M, SIGN, QP, NT>(lds, g, g);
 }
 
 // Pass kinds a kernel instantiation compiles (RM): bit R for the native radix R, plus the

@@ -82,7 +82,12 @@ __device__ __forceinline__ cpx<T> fload(const T* lds, int line, int e) {
 // XD: x direction (row-pair lines, consecutive lanes -> consecutive
 // butterflies of a line); else y direction (interleaved columns, consecutive
 // lanes -> consecutive lines).  `tid` is the caller's laundered thread index.
-template <typename T, class FG, int NT, bool XD, int R, int NS, int SIGN, int MODE>
+// XPERM (x passes only): store the outputs line-minor, element e of line l as
+// interleaved complex at 2 (NL e + l), for a next pass whose lanes run over the lines
+// (fft_pass_pfa's gi); the natural row-pair layout puts those lanes 2 RS apart, a 4-way
+// LDS bank conflict on each of its 37 reads per task.
+template <typename T, class FG, int NT, bool XD, int R, int NS, int SIGN, int MODE,
+          bool XPERM = false>
 __device__ __forceinline__ void fpass(T* lds, const cpx<T>* __restrict__ tw, int tid) {
   constexpr int N = XD ? FG::X : FG::Y;
   constexpr int NL = XD ? FG::Yp / 2 : FG::Xh;
@@ -92,6 +97,9 @@ __device__ __forceinline__ void fpass(T* lds, const cpx<T>* __restrict__ tw, int
   constexpr int LSTR = XD ? 2 * FG::RS : 2;
   constexpr int ESTR = XD ? 1 : FG::RS;
   static_assert(NB * R == N, "radix does not divide the line length");
+  static_assert(!XPERM || XD, "line-minor output is an x-pass layout");
+  constexpr int OLSTR = XPERM ? 2 : LSTR;
+  constexpr int OESTR = XPERM ? 2 * NL : ESTR;
   // a fresh opaque copy of the thread index per pass: the pass's index math
   // cannot be scheduled ahead of the previous pass's barrier and kept live
   asm volatile("" : "+v"(tid));
@@ -111,7 +119,7 @@ __device__ __forceinline__ void fpass(T* lds, const cpx<T>* __restrict__ tw, int
         line = bf - j * NL;
       }
       const int k = j % NS;
-      outbase[b] = line * LSTR + ((j - k) * R + k) * ESTR;
+      outbase[b] = line * OLSTR + ((j - k) * R + k) * OESTR;
       v[b][0] = fload<T, FG, XD, MODE>(lds, line, j);
 #pragma unroll
       for (int r = 1; r < R; ++r) {
@@ -132,11 +140,11 @@ __device__ __forceinline__ void fpass(T* lds, const cpx<T>* __restrict__ tw, int
     if (outbase[b] >= 0) {
       T* base = lds + outbase[b];
       dft_sink<T, R, SIGN>(v[b], [&](int q, cpx<T> val) {
-        if constexpr (XD) {
+        if constexpr (XD && !XPERM) {
           base[q * NS * ESTR] = val.x;
           base[q * NS * ESTR + FG::RS] = val.y;
         } else {
-          lds_cpx_store(base + q * NS * ESTR, 1, val);
+          lds_cpx_store(base + q * NS * OESTR, 1, val);
         }
       });
     }

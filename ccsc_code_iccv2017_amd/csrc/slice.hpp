@@ -97,7 +97,8 @@ __device__ __forceinline__ void pfa74(T* lds, bool xdir) {
   using FG = Grid74;
   constexpr LineGeom gx = {FG::Yp / 2, 2 * FG::RS, 1, FG::RS};
   constexpr LineGeom gy = {FG::Xh, 2, FG::RS, 1};
-  if (xdir) fft_pass_pfa<T, kPfaM, SIGN, kPfaQP, kNT>(lds, gx);
+  constexpr LineGeom gxi = {FG::Yp / 2, 2, FG::Yp, 1};   // fpass<XPERM> layout
+  if (xdir) fft_pass_pfa<T, kPfaM, SIGN, kPfaQP, kNT>(lds, gx, gxi);
   else fft_pass_pfa<T, kPfaM, SIGN, kPfaQP, kNT>(lds, gy);
 }
 
@@ -107,7 +108,7 @@ __device__ __forceinline__ void slice_r2c_rm(T* lds, const Grid2D& G, const cpx<
   if constexpr (RM == kRm74F) {
     lds_sync();
     const int tid = threadIdx.x;
-    fpass<T, Grid74, kNT, true, 2, 1, -1, kModePlain>(lds, tw, tid);
+    fpass<T, Grid74, kNT, true, 2, 1, -1, kModePlain, true>(lds, tw, tid);
     pfa74<T, -1>(lds, true);
     fpass<T, Grid74, kNT, false, 2, 1, -1, kModeSplitToHalf>(lds, tw, tid);
     pfa74<T, -1>(lds, false);
@@ -122,7 +123,7 @@ __device__ __forceinline__ void slice_c2r_rm(T* lds, const Grid2D& G, const cpx<
     const int tid = threadIdx.x;
     fpass<T, Grid74, kNT, false, 2, 1, +1, kModePlain>(lds, tw, tid);
     pfa74<T, +1>(lds, false);
-    fpass<T, Grid74, kNT, true, 2, 1, +1, kModeHermPair>(lds, tw, tid);
+    fpass<T, Grid74, kNT, true, 2, 1, +1, kModeHermPair, true>(lds, tw, tid);
     pfa74<T, +1>(lds, true);
   } else {
     slice_c2r<T, kMaxB, RM>(lds, G, tw);
