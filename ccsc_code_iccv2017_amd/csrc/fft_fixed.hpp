@@ -43,10 +43,12 @@ struct FixedGrid {
 using Grid110 = FixedGrid<11, 10, 11, 10>;
 
 // Element load of a fixed-geometry pass (modes as fft.hpp's load_elem).
-template <typename T, class FG, bool XD, int MODE>
+template <typename T, class FG, bool XD, int MODE, bool XPERM = false>
 __device__ __forceinline__ cpx<T> fload(const T* lds, int line, int e) {
   if constexpr (MODE == kModePlain) {
-    if constexpr (XD) {  // row pair: re in row 2j, im in row 2j+1
+    if constexpr (XD && XPERM) {   // the line-minor layout: (x, y) at Yp x + y
+      return lds_cpx(lds + e * FG::Yp + 2 * line, 1);
+    } else if constexpr (XD) {  // row pair: re in row 2j, im in row 2j+1
       const T* p = lds + line * (2 * FG::RS) + e;
       return {p[0], p[FG::RS]};
     } else {             // interleaved complex column
@@ -56,10 +58,16 @@ __device__ __forceinline__ cpx<T> fload(const T* lds, int line, int e) {
     const int j = e >> 1;
     const int x1 = line;
     const int x2 = (line == 0) ? 0 : FG::X - line;
-    const T* r0 = lds + (2 * j) * FG::RS;
-    const T* r1 = r0 + FG::RS;
-    const cpx<T> z1 = {r0[x1], r1[x1]};
-    const cpx<T> z2 = {r0[x2], r1[x2]};
+    cpx<T> z1, z2;
+    if constexpr (XPERM) {   // row pair j, column x at 2 (NL x + j) (fpass XPERM)
+      z1 = lds_cpx(lds + x1 * FG::Yp + 2 * j, 1);
+      z2 = lds_cpx(lds + x2 * FG::Yp + 2 * j, 1);
+    } else {
+      const T* r0 = lds + (2 * j) * FG::RS;
+      const T* r1 = r0 + FG::RS;
+      z1 = {r0[x1], r1[x1]};
+      z2 = {r0[x2], r1[x2]};
+    }
     if ((e & 1) == 0) return {(T)0.5 * (z1.x + z2.x), (T)0.5 * (z1.y - z2.y)};
     return {(T)0.5 * (z1.y + z2.y), (T)-0.5 * (z1.x - z2.x)};
   } else {  // kModeHermPair
@@ -82,12 +90,15 @@ __device__ __forceinline__ cpx<T> fload(const T* lds, int line, int e) {
 // XD: x direction (row-pair lines, consecutive lanes -> consecutive
 // butterflies of a line); else y direction (interleaved columns, consecutive
 // lanes -> consecutive lines).  `tid` is the caller's laundered thread index.
-// XPERM (x passes only): store the outputs line-minor, element e of line l as
-// interleaved complex at 2 (NL e + l), for a next pass whose lanes run over the lines
-// (fft_pass_pfa's gi); the natural row-pair layout puts those lanes 2 RS apart, a 4-way
-// LDS bank conflict on each of its 37 reads per task.
-template <typename T, class FG, int NT, bool XD, int R, int NS, int SIGN, int MODE,
-          bool XPERM = false>
+// LM (the line-minor layout: element e of row-pair line l as interleaved complex at
+// 2 (NL e + l), i.e. the real plane's (x, y) at Yp x + y): bit kLmIn, the inputs are read
+// from it (x passes in plain mode, the split-to-half y pass); bit kLmOut, an x pass
+// stores its outputs there.  A next pass whose lanes run over the row-pair lines
+// (fft_pass_pfa) then reads lane-contiguous: the natural layout puts those lanes 2 RS
+// apart, a 4-way LDS bank conflict on each of its 37 reads per task.  An x pass with
+// both bits runs its lanes over the lines (as the y passes): contiguous reads and stores.
+constexpr int kLmIn = 1, kLmOut = 2;
+template <typename T, class FG, int NT, bool XD, int R, int NS, int SIGN, int MODE, int LM = 0>
 __device__ __forceinline__ void fpass(T* lds, const cpx<T>* __restrict__ tw, int tid) {
   constexpr int N = XD ? FG::X : FG::Y;
   constexpr int NL = XD ? FG::Yp / 2 : FG::Xh;
@@ -97,9 +108,12 @@ __device__ __forceinline__ void fpass(T* lds, const cpx<T>* __restrict__ tw, int
   constexpr int LSTR = XD ? 2 * FG::RS : 2;
   constexpr int ESTR = XD ? 1 : FG::RS;
   static_assert(NB * R == N, "radix does not divide the line length");
-  static_assert(!XPERM || XD, "line-minor output is an x-pass layout");
-  constexpr int OLSTR = XPERM ? 2 : LSTR;
-  constexpr int OESTR = XPERM ? 2 * NL : ESTR;
+  constexpr bool IPERM = (LM & kLmIn) != 0, OPERM = (LM & kLmOut) != 0;
+  static_assert(!IPERM || (XD ? MODE == kModePlain : MODE == kModeSplitToHalf),
+                "line-minor inputs: the plain x pass or the split-to-half y pass");
+  static_assert(!OPERM || XD, "line-minor outputs: x passes");
+  constexpr int OLSTR = OPERM ? 2 : LSTR;
+  constexpr int OESTR = OPERM ? 2 * NL : ESTR;
   // a fresh opaque copy of the thread index per pass: the pass's index math
   // cannot be scheduled ahead of the previous pass's barrier and kept live
   asm volatile("" : "+v"(tid));
@@ -111,7 +125,7 @@ __device__ __forceinline__ void fpass(T* lds, const cpx<T>* __restrict__ tw, int
     outbase[b] = -1;
     if (bf < TOTAL) {
       int line, j;
-      if constexpr (XD) {
+      if constexpr (XD && !(IPERM && OPERM)) {
         line = bf / NB;
         j = bf - line * NB;
       } else {
@@ -120,10 +134,10 @@ __device__ __forceinline__ void fpass(T* lds, const cpx<T>* __restrict__ tw, int
       }
       const int k = j % NS;
       outbase[b] = line * OLSTR + ((j - k) * R + k) * OESTR;
-      v[b][0] = fload<T, FG, XD, MODE>(lds, line, j);
+      v[b][0] = fload<T, FG, XD, MODE, IPERM>(lds, line, j);
 #pragma unroll
       for (int r = 1; r < R; ++r) {
-        const cpx<T> x = fload<T, FG, XD, MODE>(lds, line, j + r * NB);
+        const cpx<T> x = fload<T, FG, XD, MODE, IPERM>(lds, line, j + r * NB);
         if constexpr (NS > 1) {
           cpx<T> w = tw[(r - 1) * NS + k];
           if (SIGN > 0) w.y = -w.y;
@@ -140,7 +154,7 @@ __device__ __forceinline__ void fpass(T* lds, const cpx<T>* __restrict__ tw, int
     if (outbase[b] >= 0) {
       T* base = lds + outbase[b];
       dft_sink<T, R, SIGN>(v[b], [&](int q, cpx<T> val) {
-        if constexpr (XD && !XPERM) {
+        if constexpr (XD && !OPERM) {
           base[q * NS * ESTR] = val.x;
           base[q * NS * ESTR + FG::RS] = val.y;
         } else {

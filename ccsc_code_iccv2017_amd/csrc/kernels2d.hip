@@ -86,7 +86,7 @@ void k_dual_r2c(const T* __restrict__ D, T* __restrict__ yD,
   extern __shared__ __attribute__((aligned(16))) char smem[];
   Smem<T> S = carve<T>(smem, G);
   using Q = SG<RM>;
-  const int GX = Q::X(G), GY = Q::Y(G), RS = Q::RS(G), GF = Q::F(G);
+  const int GX = Q::X(G), GY = Q::Y(G), GF = Q::F(G);
   if constexpr (!Q::fixed) load_twiddles(S.tw, twg, G.ntw);
   const int slice = blockIdx.x;
   const int g = slice % K;   // K here = KG filter slices per block
@@ -101,7 +101,7 @@ void k_dual_r2c(const T* __restrict__ D, T* __restrict__ yD,
     const T uv = (sxx < s && syy < s) ? u[syy * s + sxx] : (T)0;
     const T yv = yD[off + e] + D[off + e] - uv;
     yD[off + e] = yv;
-    S.slice[y * RS + x] = uv - yv;
+    S.slice[Q::px(x, y, G)] = uv - yv;
   }
   zero_pad_row(S.slice, G);
   slice_r2c_rm<T, RM>(S.slice, G, S.tw);
@@ -126,7 +126,7 @@ void k_c2r_dout(const cpx<T>* __restrict__ Dh,
   extern __shared__ __attribute__((aligned(16))) char smem[];
   Smem<T> S = carve<T>(smem, G);
   using Q = SG<RM>;
-  const int GX = Q::X(G), GY = Q::Y(G), RS = Q::RS(G), GF = Q::F(G);
+  const int GX = Q::X(G), GY = Q::Y(G), GF = Q::F(G);
   if constexpr (!Q::fixed) load_twiddles(S.tw, twg, G.ntw);
   const int slice = blockIdx.x;
   const cpx<T>* in = Dh + (int64_t)slice * GF;
@@ -143,7 +143,7 @@ void k_c2r_dout(const cpx<T>* __restrict__ Dh,
   T acc_d = 0, acc_n = 0;
   for (int e = threadIdx.x; e < P; e += kNT) {
     const int y = e / GX, x = e - y * GX;
-    const T v = S.slice[y * RS + x] * invP;
+    const T v = S.slice[Q::px(x, y, G)] * invP;
     if (first) {
       const T o = D[off + e];
       acc_d += (v - o) * (v - o);
@@ -156,7 +156,7 @@ void k_c2r_dout(const cpx<T>* __restrict__ Dh,
   for (int q = threadIdx.x; q < s * s; q += kNT) {
     const int sy = q / s, sx = q - sy * s;
     const int x = (sx - r + GX) % GX, y = (sy - r + GY) % GY;
-    sp[q] = S.slice[y * RS + x] * invP + yD[off + y * GX + x];
+    sp[q] = S.slice[Q::px(x, y, G)] * invP + yD[off + y * GX + x];
   }
   if (first) {
     acc_d = block_sum(acc_d, S.red);

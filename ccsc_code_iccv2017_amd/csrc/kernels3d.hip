@@ -54,7 +54,7 @@ void k_plane_fwd(int mode, const T* __restrict__ a,
       const T* in = a + ((int64_t)slice * st + tt) * sx * sy;
       for (int e = threadIdx.x; e < sx * sy; e += kNT) {
         const int y = e / sx, x = e - y * sx;
-        S.slice[(y + o) * RS + x + o] = in[e];
+        S.slice[Q::px(x + o, y + o, G)] = in[e];
       }
     }
   } else {
@@ -74,7 +74,7 @@ void k_plane_fwd(int mode, const T* __restrict__ a,
         b[off + e] = yn;
         c = uv - yn;
       }
-      S.slice[y * RS + x] = c;
+      S.slice[Q::px(x, y, G)] = c;
     }
     zero_pad_row(S.slice, G);
   }
@@ -162,7 +162,7 @@ void k_plane_inv(int mode, const cpx<T>* src,
   extern __shared__ __attribute__((aligned(16))) char smem[];
   Smem<T> S = carve<T>(smem, G);
   using Q = SG<RM>;
-  const int GX = Q::X(G), GY = Q::Y(G), RS = Q::RS(G), GF = Q::F(G), GXh = Q::Xh(G);
+  const int GX = Q::X(G), GY = Q::Y(G), GF = Q::F(G), GXh = Q::Xh(G);
   if constexpr (!Q::fixed) load_twiddles(S.tw, twg, G.ntw);
   const int64_t slice = blockIdx.x / Tn;
   const int t = blockIdx.x - (int)(slice * Tn);
@@ -182,7 +182,7 @@ void k_plane_inv(int mode, const cpx<T>* src,
   T acc_d = 0, acc_n = 0;
   for (int e = threadIdx.x; e < P; e += kNT) {
     const int y = e / GX, x = e - y * GX;
-    const T v = S.slice[y * RS + x] * scale;
+    const T v = S.slice[Q::px(x, y, G)] * scale;
     if (nrm) {
       const T o = dst[off + e];
       acc_d += (v - o) * (v - o);
@@ -193,7 +193,7 @@ void k_plane_inv(int mode, const cpx<T>* src,
       const T an = v + fmax(-theta, fmin(q, theta));
       state[off + e] = an;
       if (wz) dst[off + e] = v;
-      if (nxt) S.slice[y * RS + x] = fma((T)-2, fmax(-theta, fmin(an, theta)), an);
+      if (nxt) S.slice[Q::px(x, y, G)] = fma((T)-2, fmax(-theta, fmin(an, theta)), an);
     } else {
       dst[off + e] = v;
     }
@@ -206,7 +206,7 @@ void k_plane_inv(int mode, const cpx<T>* src,
       for (int q = threadIdx.x; q < s * s; q += kNT) {
         const int sy = q / s, sx = q - sy * s;
         const int x = (sx - r + GX) % GX, y = (sy - r + GY) % GY;
-        sp[q] = S.slice[y * RS + x] * scale + yv[off + y * GX + x];
+        sp[q] = S.slice[Q::px(x, y, G)] * scale + yv[off + y * GX + x];
       }
     }
   }

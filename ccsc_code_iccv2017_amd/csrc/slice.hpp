@@ -86,19 +86,27 @@ struct SG {
   __device__ static int RS(const Grid2D& G) { if constexpr (fixed) return Grid74::RS; else return G.RS; }
   __device__ static int Yp(const Grid2D& G) { if constexpr (fixed) return Grid74::Yp; else return G.Yp; }
   __device__ static int F(const Grid2D& G) { if constexpr (fixed) return Grid74::F; else return G.F; }
+  // LDS offset of the real plane's (x, y): line-minor on the fixed 74 grid (the layout
+  // its x passes read and write, fpass LM), natural rows otherwise
+  __device__ static int px(int x, int y, const Grid2D& G) {
+    if constexpr (fixed) return x * Grid74::Yp + y;
+    else return y * RS(G) + x;
+  }
   __device__ static int bin(int f, const Grid2D& G) {
     const int y = f / Xh(G);
     return y * RS(G) + 2 * (f - y * Xh(G));
   }
 };
 
+// the x passes read and write the line-minor layout (fpass LM): the forward one for the
+// split-to-half y pass, the inverse one, the last pass of the C2R, for the kernels' real
+// planes (SG<kRm74F>::px)
 template <typename T, int SIGN>
 __device__ __forceinline__ void pfa74(T* lds, bool xdir) {
   using FG = Grid74;
-  constexpr LineGeom gx = {FG::Yp / 2, 2 * FG::RS, 1, FG::RS};
   constexpr LineGeom gy = {FG::Xh, 2, FG::RS, 1};
-  constexpr LineGeom gxi = {FG::Yp / 2, 2, FG::Yp, 1};   // fpass<XPERM> layout
-  if (xdir) fft_pass_pfa<T, kPfaM, SIGN, kPfaQP, kNT>(lds, gx, gxi);
+  constexpr LineGeom gxi = {FG::Yp / 2, 2, FG::Yp, 1};   // line-minor
+  if (xdir) fft_pass_pfa<T, kPfaM, SIGN, kPfaQP, kNT>(lds, gxi, gxi);
   else fft_pass_pfa<T, kPfaM, SIGN, kPfaQP, kNT>(lds, gy);
 }
 
@@ -108,9 +116,9 @@ __device__ __forceinline__ void slice_r2c_rm(T* lds, const Grid2D& G, const cpx<
   if constexpr (RM == kRm74F) {
     lds_sync();
     const int tid = threadIdx.x;
-    fpass<T, Grid74, kNT, true, 2, 1, -1, kModePlain, true>(lds, tw, tid);
+    fpass<T, Grid74, kNT, true, 2, 1, -1, kModePlain, kLmIn | kLmOut>(lds, tw, tid);
     pfa74<T, -1>(lds, true);
-    fpass<T, Grid74, kNT, false, 2, 1, -1, kModeSplitToHalf>(lds, tw, tid);
+    fpass<T, Grid74, kNT, false, 2, 1, -1, kModeSplitToHalf, kLmIn>(lds, tw, tid);
     pfa74<T, -1>(lds, false);
   } else {
     slice_r2c<T, kMaxB, RM>(lds, G, tw);
@@ -123,7 +131,7 @@ __device__ __forceinline__ void slice_c2r_rm(T* lds, const Grid2D& G, const cpx<
     const int tid = threadIdx.x;
     fpass<T, Grid74, kNT, false, 2, 1, +1, kModePlain>(lds, tw, tid);
     pfa74<T, +1>(lds, false);
-    fpass<T, Grid74, kNT, true, 2, 1, +1, kModeHermPair, true>(lds, tw, tid);
+    fpass<T, Grid74, kNT, true, 2, 1, +1, kModeHermPair, kLmOut>(lds, tw, tid);
     pfa74<T, +1>(lds, true);
   } else {
     slice_c2r<T, kMaxB, RM>(lds, G, tw);

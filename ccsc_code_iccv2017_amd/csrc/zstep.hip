@@ -30,7 +30,7 @@ void k_zstep_diag(T* __restrict__ z, T* __restrict__ as,
   extern __shared__ __attribute__((aligned(16))) char smem[];
   Smem<T> S = carve<T>(smem, G);
   using Q = SG<RM>;
-  const int GX = Q::X(G), RS = Q::RS(G);
+  const int GX = Q::X(G);
   if constexpr (!Q::fixed) load_twiddles(S.tw, twg, G.ntw);
   const int64_t slice = blockIdx.x;
   const int P = GX * Q::Y(G);
@@ -41,7 +41,7 @@ void k_zstep_diag(T* __restrict__ z, T* __restrict__ as,
   for (int e = threadIdx.x; e < P; e += kNT) {
     const int y = e / GX, x = e - y * GX;
     const T a = as[off + e];
-    S.slice[y * RS + x] = fma((T)-2, fmax(-theta, fmin(a, theta)), a);
+    S.slice[Q::px(x, y, G)] = fma((T)-2, fmax(-theta, fmin(a, theta)), a);
   }
   zero_pad_row(S.slice, G);
   slice_r2c_rm<T, RM>(S.slice, G, S.tw);
@@ -57,7 +57,7 @@ void k_zstep_diag(T* __restrict__ z, T* __restrict__ as,
   T nd = 0, nz = 0;
   for (int e = threadIdx.x; e < P; e += kNT) {
     const int y = e / GX, x = e - y * GX;
-    const T zn = S.slice[y * RS + x];
+    const T zn = S.slice[Q::px(x, y, G)];
     if (TOL) {
       const T zo = z[off + e];
       nd += (zn - zo) * (zn - zo);
