@@ -20,9 +20,10 @@ CCSC_E_UNSUPPORTED = -5
 CCSC_E_STATE = -6
 
 CCSC_DPAR, CCSC_DZPAR, CCSC_L3D, CCSC_L4D, CCSC_HS23 = 0, 1, 2, 3, 4
-ABI_VERSION = 6
+ABI_VERSION = 7
 VERBOSE = {"none": 0, "brief": 1, "all": 2}
 CCSC_FP64 = 0
+CCSC_FP32 = 1  # deprecated: CCSC_E_UNSUPPORTED
 DFACTOR = {"auto": 0, "cholesky": 1, "woodbury": 2}
 TRANSPORT = {0: "none", 1: "rccl", 2: "host"}
 

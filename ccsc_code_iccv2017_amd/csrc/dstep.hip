@@ -646,12 +646,7 @@ __global__ __launch_bounds__(256) void k_dsolve_tile(const cpx<double>* __restri
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int R = 16 * tI[s] + row, C = 16 * tJ[s] + 4 * cg + q;
-      if (tI[s] >= 0 && R < K && C <= R) {   // one 16-B load (cpx<double> is 8-B aligned)
-        const auto v = *reinterpret_cast<const vec2_t<double>::type*>(Lf + C * K - (C * (C - 1)) / 2 + R - C);
-        Lt[s][q] = {v.x, v.y};
-      } else {
-        Lt[s][q] = zero;
-      }
+      Lt[s][q] = ldc_if(tI[s] >= 0 && R < K && C <= R, Lf + C * K - (C * (C - 1)) / 2 + R - C);
     }
   }
   if (tid < 16 * Tn) {

@@ -271,6 +271,8 @@ static void resolve_problem(ccsc_problem& p) {
                                   std::to_string(p.ni) + "); the reference floors n/ni silently (Q13)");
   if (p.verbose < CCSC_VERBOSE_NONE || p.verbose > CCSC_VERBOSE_ALL)
     throw Err(CCSC_E_INVALID, "bad verbose");
+  if (p.precision == CCSC_FP32)
+    throw Err(CCSC_E_UNSUPPORTED, "CCSC_FP32 was never built and is deprecated (ABI 7): use CCSC_FP64");
   if (p.precision != CCSC_FP64) throw Err(CCSC_E_INVALID, "precision must be CCSC_FP64 (double, as the reference)");
   if (p.dfactor < CCSC_DFACTOR_AUTO || p.dfactor > CCSC_DFACTOR_WOODBURY)
     throw Err(CCSC_E_INVALID, "bad dfactor");
@@ -419,6 +421,14 @@ static void wait_comm(ncclComm_t c, const std::atomic<bool>* abort) {
 // non-blocking so that no collective call can stall inside RCCL: abort_group relies on
 // it to abort them only while no rank is inside a call.
 static void init_group_comms(std::vector<ncclComm_t>& comms, const int32_t* devices, int nd) {
+  // NCCL_COMM_BLOCKING=1 overrides cfg.blocking = 0 per communicator: a surviving rank could
+  // then block inside a collective waiting on a failed one and abort_group would wait on it
+  // forever -- refuse it instead of deadlocking later
+  if (const char* b = std::getenv("NCCL_COMM_BLOCKING"))
+    if (std::atoi(b) != 0)
+      throw Err(CCSC_E_INVALID,
+                "NCCL_COMM_BLOCKING=1 is not supported for multi-device contexts: their RCCL "
+                "communicators must be non-blocking so a failed rank can be aborted");
   ncclUniqueId id;
   NCCLCHK(ncclGetUniqueId(&id));
   ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
@@ -783,7 +793,7 @@ struct Session2D {
   // in a multi-device group every collective first checks that no rank has failed.
   template <typename Fn>
   void collective(int op, double* buf, size_t count, Fn&& rccl) {
-    if (ctx->nranks <= 1) return;
+    if (ctx->nranks <= 1 && !ctx->rccl_self) return;
     if (ctx->hostfn) {   // the exchange itself returns an error once the group aborted
       host_exchange(op, buf, count);
       return;
@@ -2092,7 +2102,9 @@ ccsc_ctx* ccsc_create_multi(const int32_t* devices, int32_t ndev, char* err, siz
     c->devices.assign(devices, devices + ndev);
     HIPCHK(hipSetDevice(devices[0]));
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    if (ndev > 1) {
+    const char* self_ev = std::getenv("CCSC_TEST_RCCL_SELF");
+    const bool rccl_self = ndev == 1 && self_ev && std::atoi(self_ev) != 0;
+    if (ndev > 1 || rccl_self) {
       bool distinct = true;
       for (int i = 0; i < ndev; ++i)
         for (int j = 0; j < i; ++j) distinct = distinct && devices[i] != devices[j];
@@ -2107,6 +2119,7 @@ ccsc_ctx* ccsc_create_multi(const int32_t* devices, int32_t ndev, char* err, siz
         u->device = devices[i];
         u->rank = i;
         u->nranks = ndev;
+        u->rccl_self = rccl_self;
         u->grp = c->grp;
         if (c->hg) {
           c->hg_ranks[i] = HostGroupRank{c->hg.get(), i};
@@ -2141,7 +2154,7 @@ int32_t ccsc_comm_ranks(ccsc_ctx* ctx, int32_t* ranks, int32_t* transport, char*
     if (u->nranks > 1 && u->hostfn) {
       t = CCSC_TRANSPORT_HOST;
       n = u->nranks;
-    } else if (u->nranks > 1) {
+    } else if (u->nranks > 1 || u->rccl_self) {
       if (!u->comm) throw Err(CCSC_E_STATE, "the communicator was aborted (a rank failed)");
       int c = 0;
       NCCLCHK(ncclCommCount(u->comm, &c));

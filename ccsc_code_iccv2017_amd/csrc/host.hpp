@@ -170,4 +170,8 @@ struct ccsc_ctx {
   std::vector<ccsc::HostGroupRank> hg_ranks;
   std::vector<int32_t> devices;                  // the device list (ranks 0..ndev-1)
   std::shared_ptr<ccsc::CommGroup> grp;          // parent and subs of a multi-device context
+  // test-only (CCSC_TEST_RCCL_SELF=1 on a one-device ccsc_create_multi): a 1-rank RCCL
+  // communicator that every collective goes through, so the RCCL path (non-blocking init,
+  // enqueue + wait_comm, abort / re-init) executes on a one-GPU box
+  bool rccl_self = false;
 };

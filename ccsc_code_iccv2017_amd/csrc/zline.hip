@@ -57,7 +57,65 @@ namespace ccsc {
 
 constexpr int kZlWL = 7;   // waves whose w bins stay in LDS (35 columns x 110 bins, 61.6 KB)
 constexpr size_t kZlWBytes = (size_t)kZlWL * 5 * zl::Y * 16;
-constexpr size_t kZlSmem = zl::kSmem + kZlWBytes;
+
+// Region-major transpose buffer of k_zline (round 5).  Row pair j (rows 2j, 2j+1) owns
+// region (m, r) = (j mod 5, 9j mod 11) of 112 complex slots at A(m) + r PS; inside it,
+// slot (a, b) sits at TAU(a) + b:
+//   * (x mod 10, x mod 11) = zslot(x) holds Z_j(x), the x-R2C of the packed pair (x->y
+//     direction, written by P5), and in the y->x direction H_2j(c) at zslot(c) and
+//     H_2j+1(c) at zslot(110 - c), the odd rows of the self-conjugate columns c = 0, 55 at
+//     (10, 0) / (10, 1);
+//   * so an x-line touches only its own region and a y-line (column c) only the slots
+//     zslot(c), zslot(110 - c) (or (10, 0/1)) of every region: P3..P5 of a pair and P7,
+//     P9, P1 of a column are private to their lines (their wave-local exchanges live in
+//     those slots too), and a slice needs two workgroup barriers (the two transposes)
+//     instead of four;
+//   * every access is a per-lane base plus a compile-time register offset: a y-line's
+//     layout-A lane n1 owns rows (11 n1 + 10 n2) mod 110, i.e. region (n1 >> 1, n2 + (n1 & 1))
+//     (one wrap, at n2 = 10 on the odd lanes) -- no per-element row or column index math.
+// PS, A and TAU come from a search over the gfx950 bank model (tools/lds_anneal.py,
+// tools/lds_sim2.py): 16.0k LDS-array cycles per slice and workgroup, the same as the
+// round-4 column layout (16.1k).
+namespace zr {
+constexpr int PS = 113;
+__host__ __device__ constexpr int A(int m) { return m * 1245 + (m >= 3 ? 5 : 0) + (m >= 4 ? 29 : 0); }
+__host__ __device__ constexpr int TAU(int a) { return 11 * a + 5 + (a >= 2 ? 1 : 0); }
+__host__ __device__ constexpr int SL(int a, int b) { return TAU(a) + b; }
+constexpr int kSize = A(4) + 10 * PS + SL(10, 1) + 1;   // complex slots
+// column c's slots: H_2j(c) / Z_j(c), Z_j(110 - c) (x->y), H_2j+1(c) (y->x)
+__device__ __forceinline__ int ze(int c) { return SL(c % 10, c % 11); }
+__device__ __forceinline__ int zm(int c) {
+  const int x = c == 0 ? 0 : 110 - c;
+  return SL(x % 10, x % 11);
+}
+__device__ __forceinline__ int zo(int c) { return c == 0 ? SL(10, 0) : c == 55 ? SL(10, 1) : zm(c); }
+__device__ __forceinline__ int region(int j) { return A(j % 5) + ((9 * j) % 11) * PS; }
+// bit k1 set: bin x = elem_b(k2, k1) > 55 of an x-line's layout-B lane k2 (its P3 value
+// is the swapped combination of the two slots it reads); as 64-bit lane masks of the
+// wave's lane layout (five 11-lane lines, lanes 55..63 duplicating k2 = 10)
+constexpr bool hi_bin(int k2, int k1) { return (11 * k1 + 100 * k2) % 110 > 55; }
+constexpr unsigned long long hi_mask(int k1) {
+  unsigned long long m = 0;
+  for (int lane = 0; lane < 64; ++lane) {
+    const int l = lane / 11 < 4 ? lane / 11 : 4;
+    const int s = lane - 11 * l;
+    if (hi_bin(s < 10 ? s : 10, k1)) m |= 1ull << lane;
+  }
+  return m;
+}
+// evaluated at compile time (a namespace-scope constexpr table: as a call in the kernel
+// the lane loop was left to run on the scalar unit)
+struct HiMasks {
+  unsigned long long m[10];
+};
+constexpr HiMasks make_hi_masks() {
+  HiMasks h{};
+  for (int k1 = 0; k1 < 10; ++k1) h.m[k1] = hi_mask(k1);
+  return h;
+}
+constexpr HiMasks kHi = make_hi_masks();
+}  // namespace zr
+constexpr size_t kZlSmem = (size_t)zr::kSize * 16 + kZlWBytes;
 static_assert(kZlSmem <= 160 * 1024, "z-step LDS");
 
 // clamp(a, -theta, theta): the prox and the dual update of a z-iteration are
@@ -129,6 +187,42 @@ __device__ __forceinline__ void inv_line(cpx<T> (&in)[10], uint32_t eb, int s, S
 #pragma unroll
   for (int k2 = 0; k2 < 11; ++k2) v[k2] = lds_cpx_at<T>(ea + (uint32_t)(k2 * ES * 16));
   zdft<T, 11, +1>(v, sink);
+}
+
+// The same line transforms with the exchange slot of each register given by a caller's
+// address function (byte offsets, compile-time register index): the region-major buffer
+// places a y-line's 110 exchange slots over all regions, an x-line's inside its own.
+template <typename T, typename WA, typename RA, typename Sink>
+__device__ __forceinline__ void inv_line_r(cpx<T> (&in)[10], WA&& waddr, RA&& raddr, Sink&& sink) {
+  zdft<T, 10, +1>(in, [&](int n1, cpx<T> val) { lds_cpx_at<T>(waddr(n1)) = val; });
+  wave_lds_fence();
+  cpx<T> v[11];
+#pragma unroll
+  for (int k2 = 0; k2 < 11; ++k2) v[k2] = lds_cpx_at<T>(raddr(k2));
+  zdft<T, 11, +1>(v, sink);
+}
+template <typename T, bool ODDROT, typename WA, typename RA, typename Sink>
+__device__ __forceinline__ void fwd_line_r(cpx<T> (&v)[11], WA&& waddr, RA&& raddr, Sink&& sink) {
+  zdft<T, 11, -1>(v, [&](int k2, cpx<T> val) { lds_cpx_at<T>(waddr(k2)) = val; });
+  wave_lds_fence();
+  cpx<T> in[10];
+#pragma unroll
+  for (int n1 = 0; n1 < 10; ++n1) {
+    const cpx<T> w = lds_cpx_at<T>(raddr(n1));
+    in[n1] = (ODDROT && (n1 & 1)) ? cpx<T>{w.y, -w.x} : w;
+  }
+  zdft<T, 10, -1>(in, sink);
+}
+
+// select between two doubles on a compile-time lane mask (two v_cndmask_b32 with the mask
+// in an SGPR pair: no per-lane condition arithmetic)
+__device__ __forceinline__ double lane_sel(double a_if_set, double b, unsigned long long mask) {
+  const int alo = __double2loint(a_if_set), ahi = __double2hiint(a_if_set);
+  const int blo = __double2loint(b), bhi = __double2hiint(b);
+  int lo, hi;
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(lo) : "v"(blo), "v"(alo), "s"(mask));
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(hi) : "v"(bhi), "v"(ahi), "s"(mask));
+  return __hiloint2double(hi, lo);
 }
 
 __device__ __forceinline__ void zl_sync() { lds_sync(); }
@@ -272,7 +366,7 @@ __global__ __launch_bounds__(zl::NT) __attribute__((amdgpu_waves_per_eu(3, 3))) 
   // w is the same for every slice of the patch: the y-lines of waves 0..kZlWL-1 (columns
   // 0..5 kZlWL - 1) keep their bins in the LDS left over beside T, each lane its own ten
   // (slot k1 * 385 + c * 11 + k2; written and read back by the same lane, so no barrier)
-  cpx<T>* sW = sT + zl::TSZ;
+  cpx<T>* sW = sT + zr::kSize;
   if constexpr (MODE >= 2) {
     if (__builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6) < kZlWL) {
       const int lane = threadIdx.x & 63, l = min(lane / 11, 4), s = lane - 11 * l;
@@ -283,6 +377,7 @@ __global__ __launch_bounds__(zl::NT) __attribute__((amdgpu_waves_per_eu(3, 3))) 
       for (int k1 = 0; k1 < 10; ++k1) sW[k1 * 385 + c * 11 + sb] = zld<cpx<T>>(Wp, bo + k1 * 616 * 16);
     }
   }
+  constexpr uint32_t kPSB = (uint32_t)zr::PS * 16u;   // region stride per n2, bytes
 
   for (int k = 0; k < K; ++k) {
     // lane roles, recomputed per slice from an opaque thread index (see fresh())
@@ -293,16 +388,19 @@ __global__ __launch_bounds__(zl::NT) __attribute__((amdgpu_waves_per_eu(3, 3))) 
     const int sb = min(s, 10), sa = min(s, 9);
     const int c = min(5 * wave + l, 55);   // y-line (column)
     const int j = min(5 * wave + l, 54);   // x-line (row pair)
-    // the line's own T column (where P1 stores; slot i at row i) and the x-line's slots in
-    // the wave's rows, as LDS byte offsets
-    const uint32_t Ey = (uint32_t)tcol(c) * 16u;
-    const uint32_t Ex = (uint32_t)(kZlWR * min(wave, 10) + xoff(l)) * 16u;
     const int64_t sl = (p * K + k) * zl::P;
     cpx<T> zc[11];   // c = u - y of the row pair (x-lines, layout A) for the R2C
     const uint32_t po = (uint32_t)(j * 10 + fresh(sa)) * 16u;   // pair n2 at po + n2*550*16
     V2 av[11];   // the state a of row pair j (layout A), mode 2
+    // the y-line's exchange bases (region-major buffer, zr): DFT-10 side (lanes k2) at
+    // wE / wO + A(n1 mod 5) for n1 < 5 / >= 5, DFT-11 side (lanes n1) at yX + k2 PS
+    const int yzE = zr::ze(c), yzO = zr::zo(c);
+    const uint32_t ywE = (uint32_t)(sb * zr::PS + yzE) * 16u, ywO = (uint32_t)(sb * zr::PS + yzO) * 16u;
+    const uint32_t yX = (uint32_t)(zr::A(sa < 5 ? sa : sa - 5) + (sa < 5 ? yzE : yzO)) * 16u;
+    auto yw = [&](int n1) { return (n1 < 5 ? ywE : ywO) + (uint32_t)zr::A(n1 % 5) * 16u; };
+    auto yr = [&](int k2) { return yX + (uint32_t)k2 * kPSB; };
     if constexpr (MODE >= 2) {
-      // ---- P1: y-C2R of conj(dcorr_k) w from bins to T[y][c] ----
+      // ---- P1: y-C2R of conj(dcorr_k) w from bins to column c of every region ----
       const cpx<T>* dk = dcorr + (int64_t)k * zl::F;
       const uint32_t bo = (uint32_t)(c * 11 + sb) * 16u;
       const bool wl = __builtin_amdgcn_readfirstlane(wave) < kZlWL;
@@ -325,90 +423,98 @@ __global__ __launch_bounds__(zl::NT) __attribute__((amdgpu_waves_per_eu(3, 3))) 
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int k1 = 0; k1 < 10; ++k1) b[k1] = cmulc(b[k1], wv[k1]);
-      inv_line<T, zl::RS>(b, Ey, sb, [&](int n2, cpx<T> val) {
-        lds_cpx_at<T>((uint32_t)(mod110(11 * sa + 10 * n2) * zl::RS) * 16u + Ey) = val;
+      // row (11 n1 + 10 n2) mod 110 of lane n1 = sa: region (sa >> 1, n2 + (sa & 1)), its
+      // column slot ze (even rows) / zo (odd rows); the odd lanes wrap at n2 = 10
+      const uint32_t ys = (uint32_t)(zr::A(sa >> 1) + ((sa & 1) ? zr::PS + yzO : yzE)) * 16u;
+      const uint32_t ys10 = ys - ((sa & 1) ? 11u * kPSB : 0u);
+      inv_line_r<T>(b, yw, yr, [&](int n2, cpx<T> val) {
+        lds_cpx_at<T>((n2 == 10 ? ys10 : ys) + (uint32_t)n2 * kPSB) = val;
       });
       zl_sync();   // P2
       if (xwave) {
-        // ---- P3: x-C2R of row pair j: Z(x) = R_2j(x) + i R_2j+1(x), Hermitian ext. ----
+        // ---- P3: x-C2R of row pair j from its region: Z(x) = H_2j(x) + i H_2j+1(x) ----
         const int s3 = fresh(sb);
-        const int xb = s3 ? 110 - 10 * s3 : 0;   // elem_b(k2, 0)
-        cpx<T> zb[10], zr[10];
-        uint32_t e3[10];   // byte offset of the T column of x = elem_b(s3, k1), + 1 if x > 55
-        const uint32_t r0 = (uint32_t)(2 * j * zl::RS) * 16u;
-        // the 20 reads first, then the rebuild (as P7: no pairwise lgkmcnt waits)
+        const int R = zr::region(j);
+        const uint32_t xa = (uint32_t)(R + s3) * 16u;                  // slot (k1, s3) + TAU(k1)
+        const uint32_t xb = (uint32_t)(R + (s3 == 0 ? 0 : 11 - s3)) * 16u;   // (10-k1, 11-s3)
+        // lane k2 = 0's bins x = 0, 55 take their odd-row value from (10, 0) / (10, 1)
+        const uint32_t xb0 = xb + (s3 == 0 ? (uint32_t)(zr::TAU(10) - zr::TAU(0)) * 16u : 0u);
+        const uint32_t xb5 = xb + (s3 == 0 ? (uint32_t)(zr::SL(10, 1) - zr::TAU(5)) * 16u : 0u);
+        cpx<T> zb[10], zr_[10];
+        // the 20 reads first, then the combination (no pairwise lgkmcnt waits)
 #pragma unroll
         for (int k1 = 0; k1 < 10; ++k1) {
-          const int x = mod110(xb + 11 * k1);
-          e3[k1] = (uint32_t)(tcol(x >= zl::Xh ? zl::X - x : x) * 16) | (x >= zl::Xh ? 1u : 0u);
-          const uint32_t o = r0 + (e3[k1] & ~15u);
-          zb[k1] = lds_cpx_at<T>(o);
-          zr[k1] = lds_cpx_at<T>(o + zl::RS * 16);
+          zb[k1] = lds_cpx_at<T>(xa + (uint32_t)zr::TAU(k1) * 16u);
+          const uint32_t bb = k1 == 0 ? xb0 : k1 == 5 ? xb5 : xb;
+          zr_[k1] = lds_cpx_at<T>(bb + (uint32_t)zr::TAU((10 - k1) % 10) * 16u);
         }
         __builtin_amdgcn_sched_barrier(0);
+        // x <= 55: u + i v (u = H_2j(x), v = H_2j+1(x)); x > 55: conj(v) + i conj(u) with
+        // u, v the values of column 110 - x -- the same two sums, re and im swapped
 #pragma unroll
         for (int k1 = 0; k1 < 10; ++k1) {
-          // conjugate both rows above Xh: flip the sign bits of their imaginary parts
-          const uint32_t m = e3[k1] << 31;
-          const T ay = __hiloint2double(__double2hiint(zb[k1].y) ^ (int)m, __double2loint(zb[k1].y));
-          const T by = __hiloint2double(__double2hiint(zr[k1].y) ^ (int)m, __double2loint(zr[k1].y));
-          zb[k1] = {zb[k1].x - by, ay + zr[k1].x};
+          const T p_ = zb[k1].x - zr_[k1].y, q_ = zb[k1].y + zr_[k1].x;
+          zb[k1] = {lane_sel(q_, p_, zr::kHi.m[k1]), lane_sel(p_, q_, zr::kHi.m[k1])};
         }
         // ---- P4: state (row 2j, row 2j+1) at x = elem_a(n1, n2), in flight under the C2R;
         // each corr value is consumed as the last inverse stage forms it ----
 #pragma unroll
         for (int n2 = 0; n2 < 11; ++n2) av[n2] = sld2<V2>(A + sl, po, n2 * 550 * 16);
-        V2 zo[kCmp ? 11 : 1];
+        V2 zo_[kCmp ? 11 : 1];
         if constexpr (kCmp) {
 #pragma unroll
-          for (int n2 = 0; n2 < 11; ++n2) zo[n2] = sld2<V2>(Zt + sl, po, n2 * 550 * 16);
+          for (int n2 = 0; n2 < 11; ++n2) zo_[n2] = sld2<V2>(Zt + sl, po, n2 * 550 * 16);
         }
         // lanes that own their elements (not a clamped duplicate) count in the norms
         const T own = (s < 10 && lane < 55) ? (T)1 : (T)0;
-        inv_line<T, 1>(zb, Ex, s3, [&](int n2, cpx<T> corr) {
-          V2 a = av[n2];
-          const T tx = clamp_t(a.x, theta), ty = clamp_t(a.y, theta);
-          const T sx = a.x - tx, sy = a.y - ty;                          // u = soft(a)
-          const T ctx = fma((T)-2, tx, a.x), cty = fma((T)-2, ty, a.y);   // c_t = u - y
-          if constexpr (kStore) {   // z_cur = (u - y)(A) + corr
-            V2 zn;
-            zn.x = ctx + corr.x;
-            zn.y = cty + corr.y;
-            if constexpr (kCmp) {
-              const T ex = zn.x - zo[n2].x, ey = zn.y - zo[n2].y;
-              nd += own * (ex * ex + ey * ey);
-              nz += own * (zn.x * zn.x + zn.y * zn.y);
-            }
-            sst2<V2>(Zt + sl, po, n2 * 550 * 16, zn);
-          }
-          if constexpr (MODE == 2) {
-            a.x = sx + corr.x;
-            a.y = sy + corr.y;
-            sst2<V2>(Ao + sl, po, n2 * 550 * 16, a);
-            zc[n2] = {fma((T)-2, clamp_t(a.x, theta), a.x), fma((T)-2, clamp_t(a.y, theta), a.y)};
-            if constexpr (kForm) {   // c_t+1 - c_t and c_t+1 of the lanes' own elements
-              const T dx = zc[n2].x - ctx, dy = zc[n2].y - cty;
-              fd += own * (dx * dx + dy * dy);
-              fz += own * (zc[n2].x * zc[n2].x + zc[n2].y * zc[n2].y);
-            }
-          }
-        });
+        const uint32_t xn = (uint32_t)(R + zr::TAU(fresh(sa))) * 16u;   // lanes n1: + k2
+        inv_line_r<T>(
+            zb, [&](int n1) { return xa + (uint32_t)zr::TAU(n1) * 16u; },
+            [&](int k2) { return xn + (uint32_t)k2 * 16u; },
+            [&](int n2, cpx<T> corr) {
+              V2 a = av[n2];
+              const T tx = clamp_t(a.x, theta), ty = clamp_t(a.y, theta);
+              const T sx = a.x - tx, sy = a.y - ty;                          // u = soft(a)
+              const T ctx = fma((T)-2, tx, a.x), cty = fma((T)-2, ty, a.y);   // c_t = u - y
+              if constexpr (kStore) {   // z_cur = (u - y)(A) + corr
+                V2 zn;
+                zn.x = ctx + corr.x;
+                zn.y = cty + corr.y;
+                if constexpr (kCmp) {
+                  const T ex = zn.x - zo_[n2].x, ey = zn.y - zo_[n2].y;
+                  nd += own * (ex * ex + ey * ey);
+                  nz += own * (zn.x * zn.x + zn.y * zn.y);
+                }
+                sst2<V2>(Zt + sl, po, n2 * 550 * 16, zn);
+              }
+              if constexpr (MODE == 2) {
+                a.x = sx + corr.x;
+                a.y = sy + corr.y;
+                sst2<V2>(Ao + sl, po, n2 * 550 * 16, a);
+                zc[n2] = {fma((T)-2, clamp_t(a.x, theta), a.x), fma((T)-2, clamp_t(a.y, theta), a.y)};
+                if constexpr (kForm) {   // c_t+1 - c_t and c_t+1 of the lanes' own elements
+                  const T dx = zc[n2].x - ctx, dy = zc[n2].y - cty;
+                  fd += own * (dx * dx + dy * dy);
+                  fz += own * (zc[n2].x * zc[n2].x + zc[n2].y * zc[n2].y);
+                }
+              }
+            });
       }
     } else {
       // ---- P4 (mode 0): a = z + y from the materialised natural layout ----
-      V2 av[11];
+      V2 av0[11];
       if (xwave) {
         const T* z0 = Zn + sl + 2 * j * zl::X;
         const T* y0 = Yn + sl + 2 * j * zl::X;
 #pragma unroll
         for (int n2 = 0; n2 < 11; ++n2) {
           const int x = mod110(11 * sa + 10 * n2);
-          av[n2].x = z0[x] + y0[x];
-          av[n2].y = z0[zl::X + x] + y0[zl::X + x];
+          av0[n2].x = z0[x] + y0[x];
+          av0[n2].y = z0[zl::X + x] + y0[zl::X + x];
         }
 #pragma unroll
         for (int n2 = 0; n2 < 11; ++n2) {
-          const V2 a = av[n2];
+          const V2 a = av0[n2];
           zc[n2] = {fma((T)-2, clamp_t(a.x, theta), a.x), fma((T)-2, clamp_t(a.y, theta), a.y)};
         }
       }
@@ -428,60 +534,57 @@ __global__ __launch_bounds__(zl::NT) __attribute__((amdgpu_waves_per_eu(3, 3))) 
       if (xwave) {
 #pragma unroll
         for (int n2 = 0; n2 < 11; ++n2) {
-          zst<V2>(Ao + sl, po + n2 * 550 * 16, av[n2]);
+          zst<V2>(Ao + sl, po + n2 * 550 * 16, av0[n2]);
           if constexpr (kStore) zst<V2>(Zt + sl, po + n2 * 550 * 16, zv[n2]);
         }
       }
     }
     if constexpr (MODE == 3) {
-      lds_sync();   // T is rewritten by the next slice's P1
+      lds_sync();   // the next slice's P1 rewrites every region's column slots
       continue;
     }
-    // ---- P5: x-R2C of the row pair -> Z_j into rows 2j, 2j+1 of T ----
+    // ---- P5: x-R2C of the row pair -> Z_j(x) at slot zslot(x) of its region ----
     if (xwave) {
-      const int s5 = fresh(sb);
-      // Z_j in layout-B slot order (zslot)
-      const uint32_t r0 = (uint32_t)(kZlWR * min(wave, 10) + zoff(l) + s5) * 16u;
-      fwd_line<T, 1>(zc, Ex, s5, [&](int k1, cpx<T> val) { lds_cpx_at<T>(r0 + (uint32_t)(k1 * 176)) = val; });
+      const int R = zr::region(j);
+      const uint32_t xa = (uint32_t)(R + fresh(sb)) * 16u;
+      const uint32_t xn = (uint32_t)(R + zr::TAU(fresh(sa))) * 16u;
+      fwd_line_r<T, false>(
+          zc, [&](int k2) { return xn + (uint32_t)k2 * 16u; },
+          [&](int n1) { return xa + (uint32_t)zr::TAU(n1) * 16u; },
+          [&](int k1, cpx<T> val) { lds_cpx_at<T>(xa + (uint32_t)zr::TAU(k1) * 16u) = val; });
     }
     zl_sync();   // P6
-    // ---- P7: column c, rows y = n1 + 10 n2: two-for-one separation ----
+    // ---- P7: column c, rows y = (11 n1 + 10 n2) mod 110: two-for-one separation of
+    // Z_j(c), Z_j(110 - c) of pair y >> 1 (region (n1 >> 1, n2 + (n1 & 1))) ----
     cpx<T> col[11];
     {
       const int n1 = fresh(sa);
-      const uint32_t a1 = (uint32_t)zslot(c) * 16u, a2 = (uint32_t)zslot((c == 0) ? 0 : zl::X - c) * 16u;
+      const T sg = (n1 & 1) ? (T)-1 : (T)1;
+      const uint32_t rb = (uint32_t)(zr::A(n1 >> 1) + (n1 & 1) * zr::PS) * 16u;
+      const uint32_t rb10 = rb - ((n1 & 1) ? 11u * kPSB : 0u);
+      const uint32_t a1 = (uint32_t)zr::ze(c) * 16u, a2 = (uint32_t)zr::zm(c) * 16u;
       // even rows z1 + conj z2, odd rows z1 - conj z2 -- twice the row spectra (the 1/2 is
       // applied once to the patch's accumulated bins), the odd rows' times i (the -i is
-      // applied in P9's DFT-10, where the odd rows are compile-time registers -- fwd_line
-      // ODDROT); row parity = n1's
-      const T sg = (n1 & 1) ? (T)-1 : (T)1;
-      // all 22 reads first, then the arithmetic: the scheduler otherwise interleaves them
-      // pairwise with a full lgkmcnt wait each (eleven LDS round trips per wave)
+      // applied in P9's DFT-10, where the odd rows are compile-time registers -- ODDROT)
       cpx<T> z1[11], z2[11];
-      // row y = (11 n1 + 10 n2) mod 110: pair y >> 1 is line n1 >> 1 of wave (n1 + n2) mod 11,
-      // i.e. wave n1 + n2 stepping by one per n2 and wrapping once (at n2 = 11 - n1): the
-      // bases b1, b2 plus a compile-time step, minus one wrap where n1 >= 11 - n2
-      const uint32_t e0 = (uint32_t)(kZlWR * n1 + zoff(n1 >> 1)) * 16u;
-      const uint32_t b1 = e0 + a1, b2 = e0 + a2;
-      constexpr uint32_t kStep = kZlWR * 16u, kWrap = 11u * kZlWR * 16u;
 #pragma unroll
       for (int n2 = 0; n2 < 11; ++n2) {
-        const uint32_t w = (n2 > 0 && n1 >= 11 - n2) ? kWrap : 0u;
-        z1[n2] = lds_cpx_at<T>(b1 - w + n2 * kStep);
-        z2[n2] = lds_cpx_at<T>(b2 - w + n2 * kStep);
+        const uint32_t r = (n2 == 10 ? rb10 : rb) + (uint32_t)n2 * kPSB;
+        z1[n2] = lds_cpx_at<T>(r + a1);
+        z2[n2] = lds_cpx_at<T>(r + a2);
       }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int n2 = 0; n2 < 11; ++n2)
         col[n2] = {fma(sg, z2[n2].x, z1[n2].x), fma(-sg, z2[n2].y, z1[n2].y)};
     }
-    zl_sync();   // P8
+    // no barrier: P9's exchange reuses the slots this line alone just read
     // ---- P9: y-R2C of column c -> bins, accumulate sum_k dhat_k C_k ----
     {
       const int s9 = fresh(sb);
       const cpx<T>* dk = dhat + (int64_t)k * zl::F;
       const uint32_t bo = (uint32_t)(c * 11 + s9) * 16u;
-      fwd_line<T, zl::RS, true>(col, Ey, s9, [&](int k1, cpx<T> cb) {
+      fwd_line_r<T, true>(col, yr, yw, [&](int k1, cpx<T> cb) {
         acc[k1] = cmac(acc[k1], fld<cpx<T>>(dk, bo, k1 * 616 * 16), cb);
       });
     }

@@ -27,6 +27,7 @@ too; ``n % ni != 0`` is an error here rather than a silent floor, Q13).
 from __future__ import annotations
 
 import ctypes as C
+import os
 import math
 
 import numpy as np
@@ -79,11 +80,16 @@ class Context:
             raise L.CCSCError(L.CCSC_E_HIP, eb.value.decode(errors="replace"))
         self.device, self.rank, self.nranks = devices[0], 0, 1
         self.devices = list(devices)
+        # ccsc_create_multi builds a rank group for several devices, and for one under the
+        # test hook CCSC_TEST_RCCL_SELF=1 (a 1-rank RCCL communicator); such a context
+        # serves ccsc_learn only, not sessions
+        selftest = os.environ.get("CCSC_TEST_RCCL_SELF", "0").strip()
+        self._group = len(devices) > 1 or (selftest.isdigit() and int(selftest) != 0)
         return self
 
     @property
     def group(self):
-        return len(getattr(self, "devices", ())) > 1
+        return getattr(self, "_group", False)
 
     def comm_ranks(self):
         """(ranks, transport) of the context's communicator (ccsc_comm_ranks): RCCL

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define CCSC_ABI_VERSION 6
+#define CCSC_ABI_VERSION 7
 
 /* status codes */
 #define CCSC_OK 0
@@ -69,8 +69,10 @@ extern "C" {
 /* arithmetic and storage precision: double only, as the reference computes (MATLAB
  * double; the 4D driver's single-precision b, learn_kernels_4D_extract_patches.m:46,
  * is widened on input).  A reduced-precision storage mode was declared in earlier
- * rounds and never built; it is not part of the ABI. */
+ * rounds and never built.  ABI 7 keeps its value as a deprecated name so callers built
+ * against ABI <= 6 still compile; requesting it returns CCSC_E_UNSUPPORTED. */
 #define CCSC_FP64 0
+#define CCSC_FP32 1 /* deprecated (ABI <= 6): always CCSC_E_UNSUPPORTED */
 
 /* form of the per-frequency D-step factor (precompute_H_hat_D, dP:221-237).
  * AUTO: Woodbury when blocks hold few patches (ni <= 8 and 4 ni <= K), else the

@@ -29,7 +29,7 @@ def test_every_header_symbol_is_exported(L):
     missing = [s for s in header_symbols() if not hasattr(lib, s)]
     assert not missing, missing
     assert set(header_symbols()) == set(L.SIGNATURES), "ctypes table out of sync with ccsc.h"
-    assert L.lib().ccsc_abi_version() == L.ABI_VERSION == 6
+    assert L.lib().ccsc_abi_version() == L.ABI_VERSION == 7
 
 
 def _problem(L, variant, sb=(100, 100), n=10000, K=100, psf=11, **kw):
@@ -75,6 +75,18 @@ def test_invalid_shapes_are_errors(L):
     p.views[0], p.views[1] = 5, 4
     with pytest.raises(L.CCSCError):
         resolve(p)                          # Q9: U != V
+
+
+def test_precision_codes(L):
+    """ABI 7: CCSC_FP32 stays a (deprecated) name and reports UNSUPPORTED, any other value
+    than CCSC_FP64 is INVALID (the removal was an ABI change)."""
+    from ccsc_code_iccv2017_amd.learners import resolve
+    for prec, code in [(L.CCSC_FP32, L.CCSC_E_UNSUPPORTED), (7, L.CCSC_E_INVALID)]:
+        p = _problem(L, 1)
+        p.precision = prec
+        with pytest.raises(L.CCSCError) as e:
+            resolve(p)
+        assert e.value.code == code
 
 
 def test_supported_reports_reasons(L):

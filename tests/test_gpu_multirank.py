@@ -169,6 +169,52 @@ def test_failing_rank_aborts_group_and_context_recovers(gpu_ctx, monkeypatch, fa
     np.testing.assert_allclose(it2["obj_vals_z"], it1["obj_vals_z"], rtol=1e-10)
 
 
+@pytest.mark.parametrize("variant", ["dz", "dp"])
+def test_rccl_self_group_executes_and_recovers(gpu_ctx, monkeypatch, variant):
+    """The RCCL transport on a one-GPU box: a one-device multi context
+    under the test hook CCSC_TEST_RCCL_SELF=1 carries a 1-rank RCCL communicator created
+    non-blocking (ncclCommInitRankConfig), and every consensus exchange goes through
+    collective(): ncclAllReduce per d-iteration, ncclBroadcast per outer iteration
+    (dP:114-121, :143), each polled by wait_comm.  A 1-rank all-reduce and broadcast are
+    identities, so the learn must equal the transport-free one bit for bit.  Then an injected
+    failure aborts the communicator (abort_group -> ncclCommAbort) and the same context
+    re-creates it (reset_group) and learns the same result again."""
+    from ccsc_code_iccv2017_amd import _lib as L
+    from ccsc_code_iccv2017_amd import learners as E
+    args, ni = _small_dz(nblk=3)
+    fn = (E.admm_learn_conv2D_large_dzParallel if variant == "dz"
+          else E.admm_learn_conv2D_large_dParallel)
+    if variant == "dp":
+        b, ks, lr, lp, mi, tol, vb, init = args
+        rng = np.random.default_rng(5)
+        init = {"d": init["d"], "z": rng.standard_normal((16, 15, ks[2], b.shape[2]))}
+        args = (b, ks, lr, lp, mi, tol, vb, init)
+    d1, z1, DZ1, it1 = fn(*args, ni=ni, ctx=gpu_ctx)
+    monkeypatch.setenv("CCSC_TEST_RCCL_SELF", "1")
+    mctx = E.Context.multi([0])
+    monkeypatch.delenv("CCSC_TEST_RCCL_SELF")
+    try:
+        assert mctx.comm_ranks() == (1, "rccl")
+        d2, z2, DZ2, it2 = fn(*args, ni=ni, ctx=mctx)
+        np.testing.assert_array_equal(d2, d1)
+        np.testing.assert_array_equal(z2, z1)
+        np.testing.assert_array_equal(DZ2, DZ1)
+        np.testing.assert_array_equal(it2["obj_vals_z"], it1["obj_vals_z"])
+        monkeypatch.setenv("CCSC_TEST_FAIL_RANK", "0:1")
+        with pytest.raises(L.CCSCError) as ei:
+            fn(*args, ni=ni, ctx=mctx)
+        assert "injected fault" in str(ei.value)
+        monkeypatch.delenv("CCSC_TEST_FAIL_RANK")
+        with pytest.raises(L.CCSCError):
+            mctx.comm_ranks()                 # aborted until the next learn re-creates it
+        d3, _, _, it3 = fn(*args, ni=ni, ctx=mctx)
+        assert mctx.comm_ranks() == (1, "rccl")
+        np.testing.assert_array_equal(d3, d1)
+        np.testing.assert_array_equal(it3["obj_vals_z"], it1["obj_vals_z"])
+    finally:
+        mctx.close()
+
+
 def test_one_rank_context_reports_no_transport(gpu_ctx):
     assert gpu_ctx.comm_ranks() == (1, "none")
 

@@ -190,6 +190,54 @@ def test_learn_3d_matches_oracle(gpu_ctx, sb, psf, K, n, tol):
             np.testing.assert_allclose(tr["z_diff"][i, :len(zd)], zd, rtol=1e-6)
 
 
+@pytest.mark.parametrize("sb,psf,K,n", [((10, 10, 6), 5, 4, 9),
+                                        ((20, 20, 12), 11, 8, 4),     # Woodbury
+                                        ((64, 64, 32), 11, 2, 1),     # C4 grid 74x74x42
+                                        # K T = 8400 > 8 * 1024: no k_tsolve3 plan fits
+                                        # (tsolve_tc = 0), the three-kernel z-solve
+                                        ((6, 6, 40), 3, 200, 1)])
+def test_learn_3d_production_path_matches_oracle(gpu_ctx, sb, psf, K, n):
+    """The benchmarked 3D path: verbose 'none' and no objective trace, so the
+    z-iterations skip the z store, fuse the next forward plane transform into k_plane_inv
+    and reuse its spectra (c_ready); only the last z-iteration stores z.  d, z and DZ
+    against the oracle."""
+    from ccsc_code_iccv2017_amd import learners as E
+    rng = np.random.default_rng(23)
+    r = psf // 2
+    g = tuple(s + 2 * r for s in sb)
+    b = rng.standard_normal(sb + (n,))
+    init = {"d": rng.standard_normal((psf, psf, psf, K)), "z": rng.standard_normal(g + (K, n))}
+    ks = [psf, psf, psf, K]
+    d_o, z_o, DZ_o, _, _, _ = O.learn_3d(b, ks, 1.0, 0.1, 2, 0.0, "none", init)
+    d_e, z_e, DZ_e, _, _ = E.admm_learn_conv3D_large(b, ks, 1.0, 0.1, 2, 0.0, "none", init,
+                                                      ctx=gpu_ctx)
+    assert _rel(d_e, d_o) < 1e-7
+    assert _rel(z_e, z_o) < 1e-7
+    assert _rel(DZ_e, DZ_o) < 1e-7
+
+
+@pytest.mark.parametrize("sb,UV,psf,K,n", [((10, 9), 2, 5, 3, 4),
+                                           ((64, 64), 5, 11, 4, 4),    # C5 grid 74x74, 25 views
+                                           ((8, 8), 6, 3, 40, 4)])     # Woodbury over the views
+def test_learn_4d_production_path_matches_oracle(gpu_ctx, sb, UV, psf, K, n):
+    """The benchmarked 4D path: verbose 'none', no objective trace (z stored only by the
+    last z-iteration); d, z and DZ against the oracle."""
+    from ccsc_code_iccv2017_amd import learners as E
+    rng = np.random.default_rng(24)
+    r = psf // 2
+    X, Y = sb[0] + 2 * r, sb[1] + 2 * r
+    b = rng.standard_normal((sb[0], sb[1], UV, UV, n))
+    init = {"d": rng.standard_normal((psf, psf, UV, UV, K)),
+            "z": rng.standard_normal((X, Y, 1, 1, K, n))}
+    ks = [psf, psf, UV, UV, K]
+    d_o, z_o, DZ_o, _, _, _ = O.learn_4d(b, ks, 1.0, 1.0, 2, 0.0, "none", init)
+    d_e, z_e, DZ_e, _, _ = E.admm_learn_conv4D_lightfield(b, ks, 1.0, 1.0, 2, 0.0, "none", init,
+                                                          ctx=gpu_ctx)
+    assert _rel(d_e, d_o) < 1e-7
+    assert _rel(z_e.real, z_o.real) < 1e-7
+    assert _rel(DZ_e, DZ_o) < 1e-7
+
+
 @pytest.mark.parametrize("verbose", ["brief", "none"])
 @pytest.mark.parametrize("variant", ["dp", "dz"])
 def test_headline_block_on_110_grid_matches_port(gpu_ctx, variant, verbose):
