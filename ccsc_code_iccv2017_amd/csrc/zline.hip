@@ -189,6 +189,16 @@ __device__ __forceinline__ void inv_line(cpx<T> (&in)[10], uint32_t eb, int s, S
   zdft<T, 11, +1>(v, sink);
 }
 
+// Consumption orders of the register DFTs (dft_sink): loads issued in these orders let the
+// in-order vmcnt / lgkmcnt waits release each value as soon as its own load is back (issued
+// 0..R-1, the DFT-11's third input -- register 10 -- waited for every load of the group).
+//   DFT-11 reads its inputs as v0 then the pairs (r, 11 - r); its outputs stream 0, (q, 11 - q)
+//   DFT-10 (2 x 5 prime-factor) reads the pairs (2 n2, 5 + 2 n2) mod 10
+// (same-box A/B at n = 1000: 5.874 -> 5.850 ms per launch; the filter spectrum's P9 loads
+// issued ahead of the DFT in its output order measured slower, 5.955)
+constexpr int kOrd11[11] = {0, 1, 10, 2, 9, 3, 8, 4, 7, 5, 6};
+constexpr int kOrd10in[10] = {0, 5, 2, 7, 4, 9, 6, 1, 8, 3};
+
 // The same line transforms with the exchange slot of each register given by a caller's
 // address function (byte offsets, compile-time register index): the region-major buffer
 // places a y-line's 110 exchange slots over all regions, an x-line's inside its own.
@@ -198,7 +208,7 @@ __device__ __forceinline__ void inv_line_r(cpx<T> (&in)[10], WA&& waddr, RA&& ra
   wave_lds_fence();
   cpx<T> v[11];
 #pragma unroll
-  for (int k2 = 0; k2 < 11; ++k2) v[k2] = lds_cpx_at<T>(raddr(k2));
+  for (int i = 0; i < 11; ++i) v[kOrd11[i]] = lds_cpx_at<T>(raddr(kOrd11[i]));
   zdft<T, 11, +1>(v, sink);
 }
 template <typename T, bool ODDROT, typename WA, typename RA, typename Sink>
@@ -207,7 +217,8 @@ __device__ __forceinline__ void fwd_line_r(cpx<T> (&v)[11], WA&& waddr, RA&& rad
   wave_lds_fence();
   cpx<T> in[10];
 #pragma unroll
-  for (int n1 = 0; n1 < 10; ++n1) {
+  for (int i = 0; i < 10; ++i) {
+    const int n1 = kOrd10in[i];
     const cpx<T> w = lds_cpx_at<T>(raddr(n1));
     in[n1] = (ODDROT && (n1 & 1)) ? cpx<T>{w.y, -w.x} : w;
   }
@@ -409,20 +420,22 @@ __global__ __launch_bounds__(zl::NT) __attribute__((amdgpu_waves_per_eu(3, 3))) 
       cpx<T> b[10], wv[10];
       if (wl) {
 #pragma unroll
-        for (int k1 = 0; k1 < 10; ++k1) {
+        for (int i = 0; i < 10; ++i) {
+          const int k1 = kOrd10in[i];
           b[k1] = fld<cpx<T>>(dk, bo, k1 * 616 * 16);
           wv[k1] = sW[k1 * 385 + c * 11 + sb];
         }
       } else {
 #pragma unroll
-        for (int k1 = 0; k1 < 10; ++k1) {
+        for (int i = 0; i < 10; ++i) {
+          const int k1 = kOrd10in[i];
           b[k1] = fld<cpx<T>>(dk, bo, k1 * 616 * 16);
           wv[k1] = wld<cpx<T>>(Wp, bo, k1 * 616 * 16);
         }
       }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int k1 = 0; k1 < 10; ++k1) b[k1] = cmulc(b[k1], wv[k1]);
+      for (int i = 0; i < 10; ++i) b[kOrd10in[i]] = cmulc(b[kOrd10in[i]], wv[kOrd10in[i]]);
       // row (11 n1 + 10 n2) mod 110 of lane n1 = sa: region (sa >> 1, n2 + (sa & 1)), its
       // column slot ze (even rows) / zo (odd rows); the odd lanes wrap at n2 = 10
       const uint32_t ys = (uint32_t)(zr::A(sa >> 1) + ((sa & 1) ? zr::PS + yzO : yzE)) * 16u;
@@ -443,7 +456,8 @@ __global__ __launch_bounds__(zl::NT) __attribute__((amdgpu_waves_per_eu(3, 3))) 
         cpx<T> zb[10], zr_[10];
         // the 20 reads first, then the combination (no pairwise lgkmcnt waits)
 #pragma unroll
-        for (int k1 = 0; k1 < 10; ++k1) {
+        for (int i = 0; i < 10; ++i) {
+          const int k1 = kOrd10in[i];
           zb[k1] = lds_cpx_at<T>(xa + (uint32_t)zr::TAU(k1) * 16u);
           const uint32_t bb = k1 == 0 ? xb0 : k1 == 5 ? xb5 : xb;
           zr_[k1] = lds_cpx_at<T>(bb + (uint32_t)zr::TAU((10 - k1) % 10) * 16u);
@@ -452,18 +466,19 @@ __global__ __launch_bounds__(zl::NT) __attribute__((amdgpu_waves_per_eu(3, 3))) 
         // x <= 55: u + i v (u = H_2j(x), v = H_2j+1(x)); x > 55: conj(v) + i conj(u) with
         // u, v the values of column 110 - x -- the same two sums, re and im swapped
 #pragma unroll
-        for (int k1 = 0; k1 < 10; ++k1) {
+        for (int i = 0; i < 10; ++i) {
+          const int k1 = kOrd10in[i];
           const T p_ = zb[k1].x - zr_[k1].y, q_ = zb[k1].y + zr_[k1].x;
           zb[k1] = {lane_sel(q_, p_, zr::kHi.m[k1]), lane_sel(p_, q_, zr::kHi.m[k1])};
         }
         // ---- P4: state (row 2j, row 2j+1) at x = elem_a(n1, n2), in flight under the C2R;
         // each corr value is consumed as the last inverse stage forms it ----
 #pragma unroll
-        for (int n2 = 0; n2 < 11; ++n2) av[n2] = sld2<V2>(A + sl, po, n2 * 550 * 16);
+        for (int i = 0; i < 11; ++i) av[kOrd11[i]] = sld2<V2>(A + sl, po, kOrd11[i] * 550 * 16);
         V2 zo_[kCmp ? 11 : 1];
         if constexpr (kCmp) {
 #pragma unroll
-          for (int n2 = 0; n2 < 11; ++n2) zo_[n2] = sld2<V2>(Zt + sl, po, n2 * 550 * 16);
+          for (int i = 0; i < 11; ++i) zo_[kOrd11[i]] = sld2<V2>(Zt + sl, po, kOrd11[i] * 550 * 16);
         }
         // lanes that own their elements (not a clamped duplicate) count in the norms
         const T own = (s < 10 && lane < 55) ? (T)1 : (T)0;
@@ -568,15 +583,18 @@ __global__ __launch_bounds__(zl::NT) __attribute__((amdgpu_waves_per_eu(3, 3))) 
       // applied in P9's DFT-10, where the odd rows are compile-time registers -- ODDROT)
       cpx<T> z1[11], z2[11];
 #pragma unroll
-      for (int n2 = 0; n2 < 11; ++n2) {
+      for (int i = 0; i < 11; ++i) {
+        const int n2 = kOrd11[i];
         const uint32_t r = (n2 == 10 ? rb10 : rb) + (uint32_t)n2 * kPSB;
         z1[n2] = lds_cpx_at<T>(r + a1);
         z2[n2] = lds_cpx_at<T>(r + a2);
       }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int n2 = 0; n2 < 11; ++n2)
+      for (int i = 0; i < 11; ++i) {
+        const int n2 = kOrd11[i];
         col[n2] = {fma(sg, z2[n2].x, z1[n2].x), fma(-sg, z2[n2].y, z1[n2].y)};
+      }
     }
     // no barrier: P9's exchange reuses the slots this line alone just read
     // ---- P9: y-R2C of column c -> bins, accumulate sum_k dhat_k C_k ----
