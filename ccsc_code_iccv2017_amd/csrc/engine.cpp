@@ -10,6 +10,7 @@
 //   z-loop      fused z-iteration kernel over the local patches   (dP:147-168)
 #include "../../include/ccsc.h"
 #include "host.hpp"
+#include "recon.hpp"
 
 #include <rccl/rccl.h>
 
@@ -42,70 +43,73 @@ static bool is_native_radix(int R) {
   return false;
 }
 
-// Fewest passes; native (unrolled) radices first, then at most one generic
-// prime radix <= kMaxGenericRadix (e.g. 74 = 2 * 37).  Register budget: a native
-// pass holds n/R butterflies per line (<= kMaxButterflies), a generic pass one
-// task (kGenericQP conjugate output pairs of one DFT) per thread.
+// Fewest passes over the native (unrolled) radices; lengths they cannot factor take
+// generic passes (fft_pass_generic: any odd prime length, one task of kGenericQP conjugate
+// output pairs per thread, inputs streamed from LDS, roots from the twiddle table) for
+// their other prime factors -- primes above 11 of any size (131 of a 262 grid) and several
+// of them (13 x 17) -- after the native passes: fewest generic passes, then fewest passes
+// (e.g. 74 = 2 * 37, the prime-factor pfa pass).  Register budget: a native pass holds
+// n/R butterflies per line (<= kMaxButterflies), a generic pass one task per thread.
 static int64_t generic_tasks(int n, int nlines, int p) {
   return (int64_t)nlines * (n / p) * (((p - 1) / 2 + kGenericQP - 1) / kGenericQP);
 }
 
+static bool is_prime(int p) {
+  if (p < 2) return false;
+  for (int d = 2; d * d <= p; ++d)
+    if (p % d == 0) return false;
+  return true;
+}
+
 static bool plan1d(int n, int nlines, Plan1D& out) {
-  Plan1D best{};
-  best.npass = 99;
-  std::vector<int> cur;
-  std::function<void(int, int)> dfs = [&](int rem, int start) {
-    if (rem == 1) {
-      if ((int)cur.size() < best.npass) {
-        best.n = n;
-        best.npass = (int)cur.size();
-        for (int i = 0; i < best.npass; ++i) best.rad[i] = cur[i];
-      }
-      return;
-    }
-    if ((int)cur.size() >= kMaxPass || (int)cur.size() + 1 >= best.npass) return;
-    for (int i = start; i < (int)(sizeof(kRadices) / sizeof(int)); ++i) {
-      const int R = kRadices[i];
-      if (rem % R) continue;
-      if ((int64_t)(n / R) * nlines > (int64_t)maxb_for_radix(R) * kNT) continue;  // registers
-      cur.push_back(R);
-      dfs(rem / R, i);
-      cur.pop_back();
-    }
-  };
   if (n == 1) {
     out = Plan1D{1, 0, {0}, {0}};
     return true;
   }
-  dfs(n, 0);
-  if (best.npass == 99) {
-    // one generic prime factor p, the rest native
-    for (int p = 13; p <= kMaxGenericRadix; ++p) {
-      bool prime = true;
-      for (int d = 2; d * d <= p; ++d)
-        if (p % d == 0) prime = false;
-      if (!prime || n % p) continue;
-      if (generic_tasks(n, nlines, p) > kNT) continue;
-      Plan1D rest{};
-      if (!plan1d(n / p, nlines, rest) && n / p != 1) continue;
-      if (rest.npass + 1 > kMaxPass) continue;
-      // the native passes keep their own budget at length n: re-check
-      bool ok = true;
-      for (int s = 0; s < rest.npass; ++s)
-        if ((int64_t)(n / rest.rad[s]) * nlines > (int64_t)maxb_for_radix(rest.rad[s]) * kNT)
-          ok = false;
-      if (!ok) continue;
-      best.n = n;
-      best.npass = rest.npass + 1;
-      for (int s = 0; s < rest.npass; ++s) best.rad[s] = rest.rad[s];
-      best.rad[rest.npass] = p;
-      // 2 * kPfaM: the prime-factor pass with immediate roots (fft_pass_pfa)
-      best.pfa = (n == 2 * kPfaM && p == kPfaM && best.npass == 2 &&
-                  pfa_slots(nlines, kPfaM, kPfaQP) <= kNT);
-      break;
+  constexpr int nrad = (int)(sizeof(kRadices) / sizeof(int));
+  Plan1D best{};
+  best.npass = 99;
+  int best_ng = 99;
+  std::vector<int> nat, gen;
+  // natives in kRadices order from `start`, generic primes non-decreasing
+  std::function<void(int, int, bool)> dfs = [&](int rem, int start, bool allow_gen) {
+    const int np = (int)(nat.size() + gen.size()), ng = (int)gen.size();
+    if (rem == 1) {
+      if (ng < best_ng || (ng == best_ng && np < best.npass)) {
+        best_ng = ng;
+        best = Plan1D{};
+        best.n = n;
+        best.npass = np;
+        for (int i = 0; i < (int)nat.size(); ++i) best.rad[i] = nat[i];
+        for (int i = 0; i < ng; ++i) best.rad[nat.size() + i] = gen[i];
+      }
+      return;
     }
-  }
+    if (np >= kMaxPass) return;
+    if (ng > best_ng || (ng == best_ng && np + 1 >= best.npass)) return;
+    for (int i = start; i < nrad; ++i) {
+      const int R = kRadices[i];
+      if (rem % R) continue;
+      if ((int64_t)(n / R) * nlines > (int64_t)maxb_for_radix(R) * kNT) continue;  // registers
+      nat.push_back(R);
+      dfs(rem / R, i, allow_gen);
+      nat.pop_back();
+    }
+    if (!allow_gen) return;
+    for (int R = gen.empty() ? 13 : gen.back(); R <= rem; ++R) {
+      if (rem % R || !is_prime(R)) continue;
+      if (generic_tasks(n, nlines, R) > kNT) continue;
+      gen.push_back(R);
+      dfs(rem / R, start, true);
+      gen.pop_back();
+    }
+  };
+  dfs(n, 0, false);   // native radices only (every plan of earlier rounds stays as it was)
+  if (best.npass == 99) dfs(n, 0, true);
   if (best.npass == 99) return false;
+  // 2 * kPfaM: the prime-factor pass with immediate roots (fft_pass_pfa)
+  best.pfa = (n == 2 * kPfaM && best.npass == 2 && best.rad[0] == 2 && best.rad[1] == kPfaM &&
+              pfa_slots(nlines, kPfaM, kPfaQP) <= kNT);
   out = best;
   return true;
 }
@@ -124,12 +128,12 @@ static bool make_grid2d(int X, int Y, Grid2D& G, std::string& why) {
   G.F = G.Xh * Y;
   if (!plan1d(X, G.Yp / 2, G.px)) {
     why = "grid length " + std::to_string(X) +
-          " has no radix plan (factors 2,3,5,7,11 plus at most one prime <= 127, within the register budget)";
+          " has no radix plan within kMaxPass passes and the per-thread task budget";
     return false;
   }
   if (!plan1d(Y, G.Xh, G.py)) {
     why = "grid length " + std::to_string(Y) +
-          " has no radix plan (factors 2,3,5,7,11 plus at most one prime <= 127, within the register budget)";
+          " has no radix plan within kMaxPass passes and the per-thread task budget";
     return false;
   }
   // per-pass twiddle tables, x passes then y passes
@@ -291,6 +295,9 @@ struct Geom {
   Grid2D G{};
   Grid2D Gt{};
   int Tn = 1;
+  // 2D slices past one CU's LDS (or past the slice planner): transforms as the global
+  // line passes of recon.hip, the elementwise stages in gslice.hip (G holds X, Y, Xh, F)
+  bool gp = false;
   int64_t P() const { return (int64_t)G.X * G.Y * Tn; }   // voxels per slice
   int64_t F() const { return (int64_t)G.F * Tn; }         // half-spectrum bins per slice
 };
@@ -312,8 +319,27 @@ static void check_supported(const ccsc_problem& p, Geom* Gout) {
   const int r = p.psf / 2;
   Geom g;
   std::string why;
-  if (!make_grid2d((int)(p.sb[0] + 2 * r), (int)(p.sb[1] + 2 * r), g.G, why))
-    throw Err(CCSC_E_UNSUPPORTED, why);
+  const int X = (int)(p.sb[0] + 2 * r), Y = (int)(p.sb[1] + 2 * r);
+  if (!make_grid2d(X, Y, g.G, why)) {
+    // the 2D consensus learners on any grid the reference accepts (dP:16,23-24): slices
+    // past one CU's LDS take the global line passes (the 4D / 3D / 2-3D learners do not)
+    const bool two_d = p.variant == CCSC_DPAR || p.variant == CCSC_DZPAR;
+    RowGeom rg{};
+    ColGeom cy{};
+    std::vector<cpx<double>> t1, t2;
+    if (!two_d) throw Err(CCSC_E_UNSUPPORTED, why);
+    if (!gfft_plan(X, Y, rg, cy, t1, t2))
+      throw Err(CCSC_E_UNSUPPORTED, why + "; no global line plan either");
+    g.gp = true;
+    g.G = Grid2D{};
+    g.G.X = X;
+    g.G.Y = Y;
+    g.G.Xh = X / 2 + 1;
+    g.G.Yp = Y + (Y & 1);
+    g.G.F = g.G.Xh * Y;
+    g.G.ntw = 1;   // (the slice twiddle table is unused)
+    if ((int64_t)g.G.F * 16 > INT32_MAX / 2) throw Err(CCSC_E_UNSUPPORTED, "2D half spectrum too large");
+  }
   if (p.variant == CCSC_L3D) {
     g.Tn = (int)(p.sb[2] + 2 * r);
     if (!make_gridt(g.Tn, g.G.Xh, g.Gt, why)) throw Err(CCSC_E_UNSUPPORTED, why);
@@ -344,9 +370,10 @@ static bool zline_usable(const Grid2D& G) { return zline_grid(G); }
 // memory plan shared by ccsc_plan_bytes and the session
 struct Plan2D {
   int64_t np, nbl, b0;
-  size_t z, yz, cbuf, W, dhw, D, yD, Bhat, b, L, h, Ch, Dh, Zh, E, zl, big, misc;
+  size_t z, yz, cbuf, W, dhw, D, yD, Bhat, b, L, h, Ch, Dh, Zh, E, zl, big, misc, gr;
   size_t total() const {
-    return z + yz + cbuf + W + dhw + D + yD + Bhat + b + L + h + Ch + Dh + Zh + E + zl + big + misc;
+    return z + yz + cbuf + W + dhw + D + yD + Bhat + b + L + h + Ch + Dh + Zh + E + zl + big + misc +
+           gr;
   }
 };
 
@@ -367,10 +394,16 @@ static Plan2D plan2d(const ccsc_problem& p, const Geom& g, int rank, int nranks)
   // solved with; with tol > 0 a u buffer so z_old survives for the tol test
   // (the 4D and 3D z-steps compare per slice/plane; the register-line z-step of
   // the 110 grid keeps z_old in the y buffer, zline.hip)
-  const bool zline = !is4 && !is3 && zline_usable(G);
-  m.cbuf = (p.tol > 0 && !is4 && !is3 && !zline) ? m.z : 0;
-  m.W = (!is4 && !is3) ? m.np * F * 16 : 0;
-  m.dhw = (!is4 && !is3) ? K * F * 16 : 0;
+  const bool gp = g.gp;
+  const bool zline = !is4 && !is3 && !gp && zline_usable(G);
+  m.cbuf = (p.tol > 0 && !is4 && !is3 && !gp && !zline) ? m.z : 0;
+  m.W = (!is4 && !is3 && !gp) ? m.np * F * 16 : 0;
+  m.dhw = (!is4 && !is3 && !gp) ? K * F * 16 : 0;
+  // global-pass 2D slices: a real scratch of the largest transform batch (the z-step's
+  // np K slices, the D-step's nbl K, the precompute's ni K), the z-step spectra (E)
+  m.gr = gp ? (size_t)std::max<int64_t>({m.np * (int64_t)K, m.nbl * (int64_t)(K * NV),
+                                         (int64_t)(p.ni * K), m.np * (int64_t)NV}) * P * 8
+             : 0;
   m.D = m.nbl * K * NV * P * 8;
   m.yD = m.D;
   m.Bhat = m.np * NV * F * 16;
@@ -388,7 +421,7 @@ static Plan2D plan2d(const ccsc_problem& p, const Geom& g, int rank, int nranks)
   const size_t F3t = is3 ? (size_t)std::max<int64_t>(ttile_bins(g.Tn, G.Y, G.Xh, 4),
                                                      ttile_bins(g.Tn, G.Y, G.Xh, 2))
                          : 0;
-  m.E = is4 ? m.np * K * F * 16 : is3 ? m.np * K * std::max(F, F3t) * 16 : 0;
+  m.E = is4 || gp ? m.np * K * F * 16 : is3 ? m.np * K * std::max(F, F3t) * 16 : 0;
   // register-line z-step (zline.hip, 110 grid): B^ and the two filter spectra in
   // bin-slot order, sden in bin-slot order
   m.zl = zline ? m.np * F * 16 + 2 * K * F * 16 + F * 8 : 0;
@@ -396,7 +429,8 @@ static Plan2D plan2d(const ccsc_problem& p, const Geom& g, int rank, int nranks)
   if (zline) m.zl += m.Zh;
   m.misc = (2 * K * NV * F) * 16 + F * 8 + (m.nbl + 2) * K * NV * SS * 8 * 2 +
            (4 * m.np * NV * g.Tn + 4 * K * NV * g.Tn + 64) * 8 + (size_t)(G.ntw + g.Gt.ntw) * 16 +
-           (is3 ? F * 16 + P * 8 + (m.np + K) * F3t * 16 + F3t * 8 : 0);
+           (is3 ? F * 16 + P * 8 + (m.np + K) * F3t * 16 + F3t * 8 : 0) +
+           (gp ? F * 16 + P * 8 + 64 * 1024 : 0);   // objective scratch, line twiddles
   return m;
 }
 
@@ -511,7 +545,13 @@ struct Session2D {
   // current iterate's z (its test is done), ZT_NONE: nothing (y, or stale).
   enum { ZT_NONE, ZT_PREV, ZT_CUR };
   int zt = ZT_NONE;
-  DevBuf twt, oacc, odz;   // 3D: t-FFT twiddles, objective scratch
+  DevBuf twt, oacc, odz;   // 3D: t-FFT twiddles, objective scratch (also the global path's)
+  // 2D slices past one CU's LDS (Geom::gp): global line passes (recon.hip), their
+  // twiddles, and the real scratch the elementwise stages (gslice.hip) read and write
+  bool gp = false;
+  RowGeom grg{};
+  ColGeom gcy{};
+  DevBuf gtwr, gtwc, gR;
   int tsolve_tc = 0;       // 3D: x' columns per k_tsolve3 workgroup (0: three-kernel z-solve)
   Grid2D gt2{};            //     its t plan (K * tsolve_tc lines) and twiddles
   DevBuf twt2;
@@ -641,6 +681,7 @@ struct Session2D {
     }
     is4 = p.variant == CCSC_L4D;
     is3 = p.variant == CCSC_L3D;
+    gp = g.gp;
     N = p.n / ni;
     nbl = m.nbl;
     b0 = m.b0;
@@ -682,6 +723,17 @@ struct Session2D {
           break;
         }
       }
+    }
+    if (gp) {
+      std::vector<cpx<double>> t1, t2;
+      if (!gfft_plan(G.X, G.Y, grg, gcy, t1, t2)) throw Err(CCSC_E_UNSUPPORTED, "no global line plan");
+      gtwr.alloc(t1.size() * sizeof(cpx<double>));
+      gtwc.alloc(t2.size() * sizeof(cpx<double>));
+      HIPCHK(hipMemcpy(gtwr.p, t1.data(), gtwr.bytes, hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(gtwc.p, t2.data(), gtwc.bytes, hipMemcpyHostToDevice));
+      gR.alloc(m.gr);
+      oacc.alloc((size_t)F * 16);
+      odz.alloc((size_t)P * 8);
     }
     const size_t KP = (size_t)K * P;
     bdev.alloc(m.b);
@@ -761,8 +813,9 @@ struct Session2D {
         HIPCHK(launch_randn<double>(z.as<double>(), (int64_t)(np * KP), p.seed,
                                     (uint64_t)(b0 * ni) * KP, st));
     }
-    // 3D / 4D: `yz` holds the z-step state a = z + y (kernels3d.hip, zstep.hip), y = 0
-    if (is4 || is3) HIPCHK(hipMemcpyAsync(yz.p, z.p, m.z, hipMemcpyDeviceToDevice, st));
+    // 3D / 4D / global-pass 2D: `yz` holds the z-step state a = z + y (kernels3d.hip,
+    // zstep.hip, gslice.hip), y = 0
+    if (is4 || is3 || gp) HIPCHK(hipMemcpyAsync(yz.p, z.p, m.z, hipMemcpyDeviceToDevice, st));
     // dhat = fft2(d) of the initial filters (all blocks share d0, dP:41-42)
     fwd_embed(D.as<double>(), G.X, G.Y, Tn, 0, dhat.as<cpx<double>>(), KG);
     HIPCHK(hipStreamSynchronize(st));
@@ -833,11 +886,39 @@ struct Session2D {
   }
 
   // ---- transforms ------------------------------------------------------------
+  // global-pass 2D slices: real [count][Y][X] -> half spectra [count][Y][Xh], and back
+  // (unnormalised; src is overwritten by the inverse column pass)
+  void g_r2c(const double* src, cpx<double>* dst, int64_t count) {
+    RowArgs<double> a{};
+    a.S = dst;
+    a.src = src;
+    a.per_img = 1;
+    HIPCHK(launch_rows<double>(kRowFwd, a, count, grg, gtwr.as<cpx<double>>(), st));
+    HIPCHK(launch_cols<double>(dst, -1, count, gcy, gtwc.as<cpx<double>>(), st));
+  }
+  void g_c2r(cpx<double>* src, double* dst, int64_t count) {
+    HIPCHK(launch_cols<double>(src, +1, count, gcy, gtwc.as<cpx<double>>(), st));
+    RowArgs<double> a{};
+    a.S = src;
+    a.Z = dst;
+    a.per_img = 1;
+    HIPCHK(launch_rows<double>(kRowFinalZ, a, count, grg, gtwr.as<cpx<double>>(), st));
+  }
   // dst[count][F] = R2C of the zero-padded [sx, sy, st] sub-volumes of src placed at
   // offset o in every dimension (o = r: padarray of b, dP:23 / L3:23; o = 0: full grid)
   void fwd_embed(const double* src, int sx, int sy, int stt, int o, cpx<double>* dst,
                  int64_t count) {
     const auto* twc = tw.as<cpx<double>>();
+    if (gp) {
+      if (sx == G.X && sy == G.Y && o == 0) {
+        g_r2c(src, dst, count);
+        return;
+      }
+      HIPCHK(launch_gp_prolog<double>(0, src, nullptr, nullptr, sx, sy, o, 0.0, 1, r,
+                                      gR.as<double>(), G.X, G.Y, count, st));
+      g_r2c(gR.as<double>(), dst, count);
+      return;
+    }
     if (!is3) {
       HIPCHK(launch_r2c_embed<double>(src, (int64_t)sx * sy, sx, sy, o, o, dst, F, count, twc, G,
                                       st));
@@ -850,6 +931,12 @@ struct Session2D {
   // D-step dual + R2C of (u - y) into Ch (dP:107-111)
   void dual_fwd() {
     const auto* twc = tw.as<cpx<double>>();
+    if (gp) {
+      HIPCHK(launch_gp_prolog<double>(2, D.as<double>(), yD.as<double>(), Usup.as<double>(), 0, 0,
+                                      0, 0.0, KG, r, gR.as<double>(), G.X, G.Y, nbl * KG, st));
+      g_r2c(gR.as<double>(), Ch.as<cpx<double>>(), nbl * KG);
+      return;
+    }
     if (!is3) {
       HIPCHK(launch_dual_r2c<double>(D.as<double>(), yD.as<double>(), Usup.as<double>(),
                                      Ch.as<cpx<double>>(), nbl * KG, twc, G, KG, r, st));
@@ -863,6 +950,14 @@ struct Session2D {
   // C2R of Dh -> D, support of D + y, d-norms of block 1 (dP:112-121)
   void inv_dout() {
     const auto* twc = tw.as<cpx<double>>();
+    if (gp) {   // Dh stays intact (block 1's spectrum feeds the z-step): the inverse runs on Ch
+      HIPCHK(hipMemcpyAsync(Ch.p, Dh.p, (size_t)nbl * KG * F * 16, hipMemcpyDeviceToDevice, st));
+      g_c2r(Ch.as<cpx<double>>(), gR.as<double>(), nbl * KG);
+      HIPCHK(launch_gp_epilog<double>(2, gR.as<double>(), D.as<double>(), yD.as<double>(),
+                                      supp.as<double>(), dnorm.as<double>(), owner0 ? KG : 0,
+                                      1.0 / (double)P, r, G.X, G.Y, nbl * KG, nullptr, 0.0, 0, st));
+      return;
+    }
     if (!is3) {
       HIPCHK(launch_c2r_dout<double>(Dh.as<cpx<double>>(), D.as<double>(), yD.as<double>(),
                                      supp.as<double>(), dnorm.as<double>(), owner0 ? KG : 0,
@@ -942,6 +1037,19 @@ struct Session2D {
                                       Tn, twc, G, st, tsolve_tc, yz.as<double>(), theta,
                                       write_z || tol_on, more ? C : nullptr));
       c_ready = more;
+    } else if (gp) {
+      // global-pass 2D slices: c = a - 2 clamp(a) -> R2C -> closed-form solve per bin
+      // (k_zsolve3, the 1/P folded in) -> C2R -> a' = z' + clamp(a), z' when it is read
+      cpx<double>* C = E.as<cpx<double>>();
+      HIPCHK(launch_gp_prolog<double>(3, nullptr, yz.as<double>(), nullptr, 0, 0, 0, theta, 1, r,
+                                      gR.as<double>(), G.X, G.Y, np * K, st));
+      g_r2c(gR.as<double>(), C, np * K);
+      HIPCHK(launch_zsolve3<double>(C, Bhat.as<cpx<double>>(), dhat.as<cpx<double>>(),
+                                    sden.as<double>(), F, np, K, 1.0 / (double)P, st));
+      g_c2r(C, gR.as<double>(), np * K);
+      HIPCHK(launch_gp_epilog<double>(3, gR.as<double>(), z.as<double>(), nullptr, nullptr,
+                                      tol_on ? znorm.as<double>() : nullptr, 0, 1.0, r, G.X, G.Y,
+                                      np * K, yz.as<double>(), theta, write_z || tol_on, st));
     } else if (zl_on) {
       // register-line z-step (zline.hip): mode 0 reads (z, y) and leaves a in state order.
       // tol > 0: a launch whose starting w was solved with the current filters measures
@@ -1086,15 +1194,34 @@ struct Session2D {
       HIPCHK(launch_plane_inv<double>(0, oacc.as<cpx<double>>(), dzq, nullptr, nullptr, nullptr, 0,
                                       1.0 / (double)P, r, 1, Tn, twc, G, st));
       HIPCHK(launch_crop_sq<double>(dzq, bdev.as<double>() + (size_t)q * sbx * sby * sbt, sbx, sby,
-                                    sbt, r, G.X, G.Y, zq, (int64_t)K * P, pair.as<double>(), st));
+                                    sbt, r, r, G.X, G.Y, zq, (int64_t)K * P, pair.as<double>(), st));
     }
   }
 
 
   // objective with filter spectrum `dsp` (valid on every rank); DZ optional.
+  // global-pass 2D objective (dP:305-324), patch by patch through the z-step's spectra
+  void objective_gp_parts(const cpx<double>* dsp, double* DZdev) {
+    cpx<double>* C = E.as<cpx<double>>();
+    const int sbx = (int)p.sb[0], sby = (int)p.sb[1];
+    HIPCHK(hipMemsetAsync(pair.p, 0, 2 * sizeof(double), st));
+    for (int64_t q = 0; q < np; ++q) {
+      const double* zq = z.as<double>() + (size_t)q * K * P;
+      double* dzq = DZdev ? DZdev + (size_t)q * P : odz.as<double>();
+      g_r2c(zq, C, K);
+      HIPCHK(launch_corr_sum<double>(C, dsp, oacc.as<cpx<double>>(), F, K, st));
+      g_c2r(oacc.as<cpx<double>>(), gR.as<double>(), 1);
+      HIPCHK(launch_gp_epilog<double>(0, gR.as<double>(), dzq, nullptr, nullptr, nullptr, 0,
+                                      1.0 / (double)P, r, G.X, G.Y, 1, nullptr, 0.0, 0, st));
+      HIPCHK(launch_crop_sq<double>(dzq, bdev.as<double>() + (size_t)q * sbx * sby, sbx, sby, 1, r,
+                                    0, G.X, G.Y, zq, (int64_t)K * P, pair.as<double>(), st));
+    }
+  }
+
   double objective(const cpx<double>* dsp, double* DZdev) {
-    if (is3) {
-      objective3_parts(dsp, DZdev);
+    if (is3 || gp) {
+      if (gp) objective_gp_parts(dsp, DZdev);
+      else objective3_parts(dsp, DZdev);
       allreduce(pair.as<double>(), 2);
       double h2[2];
       pair_to_host(h2);

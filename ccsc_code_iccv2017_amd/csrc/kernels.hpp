@@ -195,8 +195,18 @@ template <typename T>
 hipError_t launch_corr_sum(const cpx<T>* Zh, const cpx<T>* dhat, cpx<T>* out, int64_t F3, int K,
                            hipStream_t stream);
 template <typename T>
-hipError_t launch_crop_sq(const T* Dz, const T* b, int sx, int sy, int st, int r, int X, int Y,
-                          const T* z, int64_t zcount, T* part, hipStream_t stream);
+hipError_t launch_crop_sq(const T* Dz, const T* b, int sx, int sy, int st, int r, int rt, int X,
+                          int Y, const T* z, int64_t zcount, T* part, hipStream_t stream);
+
+// ---- gslice.hip: elementwise stages of 2D slices past one CU's LDS (global-pass path) ----
+template <typename T>
+hipError_t launch_gp_prolog(int mode, const T* a, T* b, const T* usup, int sx, int sy, int o,
+                            T theta, int KG, int r, T* R, int X, int Y, int64_t count,
+                            hipStream_t st);
+template <typename T>
+hipError_t launch_gp_epilog(int mode, const T* R, T* dst, const T* yv, T* supp, T* norms,
+                            int64_t nfirst, T scale, int r, int X, int Y, int64_t count,
+                            T* state, T theta, int wz, hipStream_t st);
 
 // ---- hs23.hip: the 2-3D hyperspectral learner (L23) ----------------------------
 // Spectra slice-major [slice][F]: dhat [K][W], zhat [n][K], Xi1 / Yv [n][W]; h [F][W][K].

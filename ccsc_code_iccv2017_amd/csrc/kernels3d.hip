@@ -456,17 +456,17 @@ __global__ void k_corr_sum(const cpx<T>* __restrict__ Zh, const cpx<T>* __restri
 }
 
 // crop-diff squared sum and l1 of one patch: part[0] += ||crop(Dz) - b||^2 (over a
-// [X,Y,T] volume, crop r each side), part[1] += sum |z| over the K slices
+// [X,Y,T] volume, crop r in x and y, rt in t: 0 for a 2D slice), part[1] += sum |z| over the K slices
 template <typename T>
 __global__ void k_crop_sq(const T* __restrict__ Dz, const T* __restrict__ b, int sx, int sy,
-                          int st, int r, int X, int Y, const T* __restrict__ z, int64_t zcount,
+                          int st, int r, int rt, int X, int Y, const T* __restrict__ z, int64_t zcount,
                           T* __restrict__ part) {
   __shared__ T red[2][4];
   T sq = 0, l1 = 0;
   const int64_t nb = (int64_t)sx * sy * st;
   for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < nb; e += (int64_t)gridDim.x * 256) {
     const int x = (int)(e % sx), y = (int)((e / sx) % sy), t = (int)(e / ((int64_t)sx * sy));
-    const T d = Dz[((int64_t)(t + r) * Y + (y + r)) * X + (x + r)] - b[e];
+    const T d = Dz[((int64_t)(t + rt) * Y + (y + r)) * X + (x + r)] - b[e];
     sq += d * d;
   }
   for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < zcount; e += (int64_t)gridDim.x * 256)
@@ -643,9 +643,9 @@ hipError_t launch_corr_sum(const cpx<T>* Zh, const cpx<T>* dhat, cpx<T>* out, in
 }
 
 template <typename T>
-hipError_t launch_crop_sq(const T* Dz, const T* b, int sx, int sy, int st, int r, int X, int Y,
-                          const T* z, int64_t zcount, T* part, hipStream_t stream) {
-  hipLaunchKernelGGL(k_crop_sq<T>, dim3(256), dim3(256), 0, stream, Dz, b, sx, sy, st, r, X, Y, z,
+hipError_t launch_crop_sq(const T* Dz, const T* b, int sx, int sy, int st, int r, int rt, int X,
+                          int Y, const T* z, int64_t zcount, T* part, hipStream_t stream) {
+  hipLaunchKernelGGL(k_crop_sq<T>, dim3(256), dim3(256), 0, stream, Dz, b, sx, sy, st, r, rt, X, Y, z,
                      zcount, part);
   return hipGetLastError();
 }
@@ -674,6 +674,6 @@ template hipError_t launch_zsolve3<double>(cpx<double>*, const cpx<double>*, con
 template hipError_t launch_corr_sum<double>(const cpx<double>*, const cpx<double>*, cpx<double>*,
                                             int64_t, int, hipStream_t);
 template hipError_t launch_crop_sq<double>(const double*, const double*, int, int, int, int, int,
-                                           int, const double*, int64_t, double*, hipStream_t);
+                                           int, int, const double*, int64_t, double*, hipStream_t);
 
 }  // namespace ccsc

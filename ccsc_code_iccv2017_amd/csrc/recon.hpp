@@ -15,6 +15,8 @@
 
 #include "kernels.hpp"
 
+#include <vector>
+
 namespace ccsc {
 
 // Row-pass geometry: G.X, G.Xh, G.RS (LDS row stride, units of T), G.px (plan of the
@@ -103,6 +105,12 @@ hipError_t launch_rows_pair(int code_mode, const RowArgs<T>& a, int64_t nz, cons
 template <typename T>
 hipError_t launch_cols(cpx<T>* S, int sign, int64_t nouter, const ColGeom& cg, const cpx<T>* tw,
                        hipStream_t st, cpx<T>* S2 = nullptr, int64_t nouter2 = 0);
+
+// Plans of the global 2D transforms of an X x Y grid (row pass over row pairs + y-line
+// column pass, solve.cpp), shared with the consensus learners' slices past one CU's LDS
+// (engine.cpp); false if a length has no line plan.
+bool gfft_plan(int X, int Y, RowGeom& rg, ColGeom& cy, std::vector<cpx<double>>& tw_rows,
+               std::vector<cpx<double>>& tw_cy);
 
 // Sherman-Morrison z-solve of SI / SP per (image, bin), in place:
 //   xi2 [n][K][F] -> zhat * invP, xi1 [n][F] -> sum_k dhat_k zhat_k (the next v1);

@@ -151,6 +151,21 @@ static bool plan_cols(int n, int Xh, ColGeom& cg) {
   return false;
 }
 
+bool gfft_plan(int X, int Y, RowGeom& rg, ColGeom& cy, std::vector<cpx<double>>& tw_rows,
+               std::vector<cpx<double>>& tw_cy) {
+  if (!plan_rows(X, Y, rg) || !plan_cols(Y, X / 2 + 1, cy)) return false;
+  const int Xh = X / 2 + 1;
+  cy.es = Xh;
+  cy.ninner = 1;
+  cy.sin = 0;
+  cy.sout = (int64_t)Xh * Y;
+  tw_rows.clear();
+  tw_cy.clear();
+  add_twiddles(rg.G.px, tw_rows);
+  add_twiddles(cy.p, tw_cy);
+  return true;
+}
+
 // ---------------------------------------------------------------------------
 // problem resolution
 // ---------------------------------------------------------------------------
