@@ -23,6 +23,8 @@
 // VALU phases (POTRF, TRSM) run beside the other's MFMA phases.
 #include "kernels.hpp"
 
+#include <utility>
+
 namespace ccsc {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
@@ -64,6 +66,62 @@ __device__ __forceinline__ void gc_tile(int t, int& I, int& J) {
   while ((I + 1) * (I + 2) / 2 <= t) ++I;
   while (I * (I + 1) / 2 > t) --I;
   J = t - I * (I + 1) / 2;
+}
+
+// the same map at compile time: the per-wave instantiations of the kernel body
+// (gram_chol_body<TM, HP, W>) see tile coordinates and LDS offsets as constants -- no
+// per-tile index arithmetic or branches in the MFMA loops (1.82 -> 1.70 ms per C2 block,
+// profiles/r05/gram_ct_ab.txt)
+constexpr int ct_I(int t) {
+  int I = 0;
+  while ((I + 1) * (I + 2) / 2 <= t) ++I;
+  return I;
+}
+constexpr int ct_J(int t) { return t - ct_I(t) * (ct_I(t) + 1) / 2; }
+
+// Gram MFMAs of tile S of wave W for one k-step (see gram_kstep)
+template <int TM, int W, int S>
+__device__ __forceinline__ void gram_tile_w(const cpx<double>* row, int Tn,
+                                            d4 (&t1)[GcShape<TM>::TW], d4 (&t2)[GcShape<TM>::TW],
+                                            d4 (&t3)[GcShape<TM>::Gauss ? GcShape<TM>::TW : 1]) {
+  constexpr int t = W + 4 * S;
+  if constexpr (t < GcShape<TM>::Tiles) {
+    constexpr int I = ct_I(t), J = ct_J(t);
+    if (I < Tn) {
+      const cpx<double> a = row[16 * I + (threadIdx.x & 15)];
+      const cpx<double> b = I == J ? a : row[16 * J + (threadIdx.x & 15)];
+      if constexpr (GcShape<TM>::Gauss) {
+        t1[S] = mfma(a.x, b.x, t1[S]);
+        t2[S] = mfma(a.y, b.y, t2[S]);
+        t3[S] = mfma(a.x - a.y, b.x + b.y, t3[S]);
+      } else {
+        t1[S] = mfma(a.x, b.x, t1[S]);
+        t1[S] = mfma(a.y, b.y, t1[S]);
+        t2[S] = mfma(a.x, b.y, t2[S]);
+        t2[S] = mfma(-a.y, b.x, t2[S]);
+      }
+    }
+  }
+  // one tile's operands at a time (hoisting the next tiles' LDS reads spills)
+  __builtin_amdgcn_sched_barrier(0);
+}
+template <int TM, int W, int... S>
+__device__ __forceinline__ void gram_kstep_seq(const cpx<double>* row, int Tn,
+                                               d4 (&t1)[GcShape<TM>::TW], d4 (&t2)[GcShape<TM>::TW],
+                                               d4 (&t3)[GcShape<TM>::Gauss ? GcShape<TM>::TW : 1],
+                                               std::integer_sequence<int, S...>) {
+  (gram_tile_w<TM, W, S>(row, Tn, t1, t2, t3), ...);
+}
+// the k-steps of one staged chunk (kvalid of kGcPC / 4), wave W
+template <int TM, int W>
+__device__ __forceinline__ void gram_chunk_w(const cpx<double>* row0, int kvalid, int Tn,
+                                             d4 (&t1)[GcShape<TM>::TW], d4 (&t2)[GcShape<TM>::TW],
+                                             d4 (&t3)[GcShape<TM>::Gauss ? GcShape<TM>::TW : 1]) {
+#pragma unroll
+  for (int kk = 0; kk < kGcPC / 4; ++kk)
+    if (kk < kvalid)
+      gram_kstep_seq<TM, W>(row0 + 4 * kk * GcShape<TM>::LD, Tn, t1, t2, t3,
+                            std::make_integer_sequence<int, GcShape<TM>::TW>{});
 }
 
 // Gram MFMAs of wave w for one k-step (4 patches: lane l takes patch l >> 4 of the
@@ -154,6 +212,32 @@ __device__ __forceinline__ void trail_step(const cpx<double>* P, cpx<double>* Pn
   }
 }
 
+// trail_step with wave W's tile coordinates as constants
+template <int TM, int W>
+__device__ __forceinline__ void trail_step_w(const cpx<double>* P, cpx<double>* Pn, int j, int Tn,
+                                             d4 (&gr)[GcShape<TM>::TW], d4 (&gi)[GcShape<TM>::TW]) {
+  const int lane = threadIdx.x & 63;
+  const int row = lane & 15, c4 = lane >> 4;
+#pragma unroll
+  for (int s = 0; s < GcShape<TM>::TW; ++s) {
+    const int t = W + 4 * s;
+    const int I = ct_I(t), J = ct_J(t);
+    if (t < GcShape<TM>::Tiles && I < Tn && J > j) {
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const int col = 4 * kk + c4;
+        const cpx<double> a = P[I * kGcTSZ + col * kGcTS + row];
+        const cpx<double> b = P[J * kGcTSZ + col * kGcTS + row];
+        gr[s] = mfma(-a.x, b.x, gr[s]);
+        gr[s] = mfma(-a.y, b.y, gr[s]);
+        gi[s] = mfma(-a.y, b.x, gi[s]);
+        gi[s] = mfma(a.x, b.y, gi[s]);
+      }
+      if (J == j + 1) tile_to_lds(Pn + I * kGcTSZ, gr[s], gi[s]);
+    }
+  }
+}
+
 template <int TM>
 __device__ __forceinline__ void first_panel(cpx<double>* P, int w, int Tn,
                                             const d4 (&gr)[GcShape<TM>::TW],
@@ -190,23 +274,21 @@ __device__ __forceinline__ void fix_diag(int w, int K, int Tn, double rho,
   }
 }
 
-// HP: right-hand-side entries of h per thread (1 when K NV <= kGcNT: the headline's one)
-template <int TM, int HP>
-__global__ __launch_bounds__(kGcNT, GcShape<TM>::WGS) void k_gram_chol_mf(const cpx<double>* __restrict__ Zh,
-                                                           const cpx<double>* __restrict__ Bh,
-                                                           cpx<double>* __restrict__ L,
-                                                           cpx<double>* __restrict__ h, int F,
-                                                           int K, int ni, double rho, int NV) {
-  const int per = gridDim.x >> 3;
-  const int f = (blockIdx.x & 7) * per + (blockIdx.x >> 3);   // XCD-aware: neighbours share L2
-  if (f >= F) return;
+// HP: right-hand-side entries of h per thread (1 when K NV <= kGcNT: the headline's one);
+// WV: the wave index as a template constant (0..3), or -1 for the run-time index (the
+// TM = 7, HP = 8 shape, whose per-wave instantiations spill)
+template <int TM, int HP, int WV>
+__device__ __forceinline__ void gram_chol_body(const cpx<double>* __restrict__ Zh,
+                                               const cpx<double>* __restrict__ Bh,
+                                               cpx<double>* __restrict__ L,
+                                               cpx<double>* __restrict__ h, int F, int K, int ni,
+                                               double rho, int NV, int f, char* smem) {
   using S = GcShape<TM>;
   constexpr int kGcTW = S::TW, kGcKP = S::KP, kGcLD = S::LD, kGcTM = TM;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
   cpx<double>* sA = reinterpret_cast<cpx<double>*>(smem);      // [2][kGcPC][kGcLD]
   cpx<double>* sB = sA + 2 * kGcPC * kGcLD;                    // [2][kGcPC][NV]
   const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wave = WV >= 0 ? WV : __builtin_amdgcn_readfirstlane(tid >> 6);
   int Tn = (K + 15) >> 4;
   const int KV = K * NV;
 
@@ -258,10 +340,14 @@ __global__ __launch_bounds__(kGcNT, GcShape<TM>::WGS) void k_gram_chol_mf(const 
     // k-steps past the last patch (the zero padding of a partial last chunk: ni = 100 is
     // 6.25 chunks) are skipped -- adding their zero products changes nothing
     const int kvalid = (ni - c * kGcPC + 3) >> 2;
+    if constexpr (WV >= 0) {
+      gram_chunk_w<TM, (WV >= 0 ? WV : 0)>(a + (lane >> 4) * kGcLD, kvalid, Tn, gr, gi, g3);
+    } else {
 #pragma unroll
-    for (int kk = 0; kk < kGcPC / 4; ++kk) {
-      const cpx<double>* row = a + (4 * kk + (lane >> 4)) * kGcLD;
-      if (kk < kvalid) gram_kstep<TM>(row, wave, Tn, gr, gi, g3);
+      for (int kk = 0; kk < kGcPC / 4; ++kk) {
+        const cpx<double>* row = a + (4 * kk + (lane >> 4)) * kGcLD;
+        if (kk < kvalid) gram_kstep<TM>(row, wave, Tn, gr, gi, g3);
+      }
     }
     const cpx<double>* b = sB + buf * kGcPC * NV;
 #pragma unroll
@@ -295,14 +381,17 @@ __global__ __launch_bounds__(kGcNT, GcShape<TM>::WGS) void k_gram_chol_mf(const 
     cpx<double>* Pn = Pbuf + ((j + 1) & 1) * kGcTM * kGcTSZ;
     __syncthreads();   // column j's tiles are in P
     // Panel j (POTRF of tile (j, j) + TRSM of the tiles below) in one sweep over its 16
-    // columns, every wave on its own: lanes 0..15 hold the rows of tile (j, j) (all four
-    // waves redundantly, so no wave waits for another), lanes 16..16 + RW - 1 up to
-    // RW = 4 (TM - 1) of the panel's other rows.  Column c of row r:
+    // columns, on as few waves as hold its rows: lanes 0..15 hold the rows of tile (j, j)
+    // (redundantly on each such wave, so none waits for another), lanes 16..63 RW = 48 of
+    // the panel's other rows -- waves 0 and 1 at K = 100 until j = 3, wave 0 alone after
+    // (the other waves go to the barrier and leave the SIMDs to the CU's other workgroup;
+    // every wave with 4 (TM - 1) rows: 1.89 ms per C2 block, this form 1.82).  Column c
+    // of row r:
     //   s = a[r][c] - sum_{k < c} L[r][k] conj(L[c][k]);  L[c][c] = sqrt(s of row c),
     //   L[r][c] = s / L[c][c]  (the POTRF and TRSM formulas coincide).
-    {
+    if (wave == 0 || wave * 48 < 16 * (Tn - 1 - j)) {
       const bool diag = lane < 16;
-      constexpr int RW = 4 * (TM - 1);   // panel rows below the diagonal tile per wave (<= 48)
+      constexpr int RW = 48;
       static_assert(16 + RW <= 64, "panel rows per wave");
       const int q = wave * RW + lane - 16;
       const int ti = diag ? j : j + 1 + (q >> 4);
@@ -347,7 +436,33 @@ __global__ __launch_bounds__(kGcNT, GcShape<TM>::WGS) void k_gram_chol_mf(const 
       }
     }
     __syncthreads();   // the panel L_.j is in P
-    if (j + 1 < Tn) trail_step<TM>(P, Pn, j, wave, Tn, gr, gi);
+    if (j + 1 < Tn) {
+      if constexpr (WV >= 0) trail_step_w<TM, (WV >= 0 ? WV : 0)>(P, Pn, j, Tn, gr, gi);
+      else trail_step<TM>(P, Pn, j, wave, Tn, gr, gi);
+    }
+  }
+}
+
+template <int TM, int HP>
+__global__ __launch_bounds__(kGcNT, GcShape<TM>::WGS) void k_gram_chol_mf(const cpx<double>* __restrict__ Zh,
+                                                           const cpx<double>* __restrict__ Bh,
+                                                           cpx<double>* __restrict__ L,
+                                                           cpx<double>* __restrict__ h, int F,
+                                                           int K, int ni, double rho, int NV) {
+  const int per = gridDim.x >> 3;
+  const int f = (blockIdx.x & 7) * per + (blockIdx.x >> 3);   // XCD-aware: neighbours share L2
+  if (f >= F) return;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  if constexpr (TM == 7 && HP > 1) {
+    gram_chol_body<TM, HP, -1>(Zh, Bh, L, h, F, K, ni, rho, NV, f, smem);
+  } else {
+    // every wave runs the same barriers in its own instantiation
+    switch (__builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6)) {
+      case 0: gram_chol_body<TM, HP, 0>(Zh, Bh, L, h, F, K, ni, rho, NV, f, smem); break;
+      case 1: gram_chol_body<TM, HP, 1>(Zh, Bh, L, h, F, K, ni, rho, NV, f, smem); break;
+      case 2: gram_chol_body<TM, HP, 2>(Zh, Bh, L, h, F, K, ni, rho, NV, f, smem); break;
+      default: gram_chol_body<TM, HP, 3>(Zh, Bh, L, h, F, K, ni, rho, NV, f, smem); break;
+    }
   }
 }
 
