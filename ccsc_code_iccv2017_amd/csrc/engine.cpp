@@ -321,9 +321,9 @@ static void check_supported(const ccsc_problem& p, Geom* Gout) {
   std::string why;
   const int X = (int)(p.sb[0] + 2 * r), Y = (int)(p.sb[1] + 2 * r);
   if (!make_grid2d(X, Y, g.G, why)) {
-    // the 2D consensus learners on any grid the reference accepts (dP:16,23-24): slices
-    // past one CU's LDS take the global line passes (the 4D / 3D / 2-3D learners do not)
-    const bool two_d = p.variant == CCSC_DPAR || p.variant == CCSC_DZPAR;
+    // the 2D and 4D consensus learners on any grid the reference accepts (dP:16,23-24):
+    // slices past one CU's LDS take the global line passes (the 3D / 2-3D learners do not)
+    const bool two_d = p.variant == CCSC_DPAR || p.variant == CCSC_DZPAR || p.variant == CCSC_L4D;
     RowGeom rg{};
     ColGeom cy{};
     std::vector<cpx<double>> t1, t2;
@@ -370,10 +370,10 @@ static bool zline_usable(const Grid2D& G) { return zline_grid(G); }
 // memory plan shared by ccsc_plan_bytes and the session
 struct Plan2D {
   int64_t np, nbl, b0;
-  size_t z, yz, cbuf, W, dhw, D, yD, Bhat, b, L, h, Ch, Dh, Zh, E, zl, big, misc, gr;
+  size_t z, yz, cbuf, W, dhw, D, yD, Bhat, b, L, h, Ch, Dh, Zh, E, zl, big, misc, gr, cg;
   size_t total() const {
     return z + yz + cbuf + W + dhw + D + yD + Bhat + b + L + h + Ch + Dh + Zh + E + zl + big + misc +
-           gr;
+           gr + cg;
   }
 };
 
@@ -422,6 +422,8 @@ static Plan2D plan2d(const ccsc_problem& p, const Geom& g, int rank, int nranks)
                                                      ttile_bins(g.Tn, G.Y, G.Xh, 2))
                          : 0;
   m.E = is4 || gp ? m.np * K * F * 16 : is3 ? m.np * K * std::max(F, F3t) * 16 : 0;
+  // 4D on global-pass slices: E keeps the view correlations, the z-step spectra go to cg
+  m.cg = is4 && gp ? m.np * K * F * 16 : 0;
   // register-line z-step (zline.hip, 110 grid): B^ and the two filter spectra in
   // bin-slot order, sden in bin-slot order
   m.zl = zline ? m.np * F * 16 + 2 * K * F * 16 + F * 8 : 0;
@@ -430,7 +432,7 @@ static Plan2D plan2d(const ccsc_problem& p, const Geom& g, int rank, int nranks)
   m.misc = (2 * K * NV * F) * 16 + F * 8 + (m.nbl + 2) * K * NV * SS * 8 * 2 +
            (4 * m.np * NV * g.Tn + 4 * K * NV * g.Tn + 64) * 8 + (size_t)(G.ntw + g.Gt.ntw) * 16 +
            (is3 ? F * 16 + P * 8 + (m.np + K) * F3t * 16 + F3t * 8 : 0) +
-           (gp ? F * 16 + P * 8 + 64 * 1024 : 0);   // objective scratch, line twiddles
+           (gp ? NV * (F * 16 + P * 8) + 64 * 1024 : 0);   // objective scratch, line twiddles
   return m;
 }
 
@@ -551,7 +553,7 @@ struct Session2D {
   bool gp = false;
   RowGeom grg{};
   ColGeom gcy{};
-  DevBuf gtwr, gtwc, gR;
+  DevBuf gtwr, gtwc, gR, Cg;
   int tsolve_tc = 0;       // 3D: x' columns per k_tsolve3 workgroup (0: three-kernel z-solve)
   Grid2D gt2{};            //     its t plan (K * tsolve_tc lines) and twiddles
   DevBuf twt2;
@@ -732,8 +734,9 @@ struct Session2D {
       HIPCHK(hipMemcpy(gtwr.p, t1.data(), gtwr.bytes, hipMemcpyHostToDevice));
       HIPCHK(hipMemcpy(gtwc.p, t2.data(), gtwc.bytes, hipMemcpyHostToDevice));
       gR.alloc(m.gr);
-      oacc.alloc((size_t)F * 16);
-      odz.alloc((size_t)P * 8);
+      oacc.alloc((size_t)NV * F * 16);
+      odz.alloc((size_t)NV * P * 8);
+      if (m.cg) Cg.alloc(m.cg);
     }
     const size_t KP = (size_t)K * P;
     bdev.alloc(m.b);
@@ -1010,7 +1013,7 @@ struct Session2D {
   // into this one's inverse, c_ready)
   ZTests zstep_iter(bool tol_on, bool write_z = true, bool more = false) {
     const auto* twc = tw.as<cpx<double>>();
-    if (is4) {
+    if (is4 && !gp) {
       HIPCHK(launch_zstep_diag<double>(z.as<double>(), yz.as<double>(), E.as<cpx<double>>(),
                                        sden.as<double>(), np * K, twc, G, theta, p.rho_z,
                                        znorm.as<double>(), tol_on, write_z || tol_on, st));
@@ -1040,12 +1043,17 @@ struct Session2D {
     } else if (gp) {
       // global-pass 2D slices: c = a - 2 clamp(a) -> R2C -> closed-form solve per bin
       // (k_zsolve3, the 1/P folded in) -> C2R -> a' = z' + clamp(a), z' when it is read
-      cpx<double>* C = E.as<cpx<double>>();
+      // (4D: the diagonal solve (E + rho c) sden against the view correlations, L4:327-347)
+      cpx<double>* C = is4 ? Cg.as<cpx<double>>() : E.as<cpx<double>>();
       HIPCHK(launch_gp_prolog<double>(3, nullptr, yz.as<double>(), nullptr, 0, 0, 0, theta, 1, r,
                                       gR.as<double>(), G.X, G.Y, np * K, st));
       g_r2c(gR.as<double>(), C, np * K);
-      HIPCHK(launch_zsolve3<double>(C, Bhat.as<cpx<double>>(), dhat.as<cpx<double>>(),
-                                    sden.as<double>(), F, np, K, 1.0 / (double)P, st));
+      if (is4)
+        HIPCHK(launch_gp_zdiag<double>(C, E.as<cpx<double>>(), sden.as<double>(), p.rho_z, (int)F,
+                                       np * K, st));
+      else
+        HIPCHK(launch_zsolve3<double>(C, Bhat.as<cpx<double>>(), dhat.as<cpx<double>>(),
+                                      sden.as<double>(), F, np, K, 1.0 / (double)P, st));
       g_c2r(C, gR.as<double>(), np * K);
       HIPCHK(launch_gp_epilog<double>(3, gR.as<double>(), z.as<double>(), nullptr, nullptr,
                                       tol_on ? znorm.as<double>() : nullptr, 0, 1.0, r, G.X, G.Y,
@@ -1201,10 +1209,27 @@ struct Session2D {
 
   // objective with filter spectrum `dsp` (valid on every rank); DZ optional.
   // global-pass 2D objective (dP:305-324), patch by patch through the z-step's spectra
+  // (4D, L4:349-369: every view of the patch from the same code spectra, DZ cropped per view)
   void objective_gp_parts(const cpx<double>* dsp, double* DZdev) {
-    cpx<double>* C = E.as<cpx<double>>();
+    cpx<double>* C = is4 ? Cg.as<cpx<double>>() : E.as<cpx<double>>();
     const int sbx = (int)p.sb[0], sby = (int)p.sb[1];
     HIPCHK(hipMemsetAsync(pair.p, 0, 2 * sizeof(double), st));
+    if (is4) {
+      const size_t vb = (size_t)sbx * sby;
+      for (int64_t q = 0; q < np; ++q) {
+        const double* zq = z.as<double>() + (size_t)q * K * P;
+        g_r2c(zq, C, K);
+        HIPCHK(launch_gp_views<double>(C, dsp, oacc.as<cpx<double>>(), (int)F, K, NV, st));
+        g_c2r(oacc.as<cpx<double>>(), gR.as<double>(), NV);
+        HIPCHK(launch_gp_crop<double>(gR.as<double>(), bdev.as<double>() + (size_t)q * NV * vb,
+                                      DZdev ? DZdev + (size_t)q * NV * vb : nullptr, sbx, sby, r,
+                                      G.X, G.Y, 1.0 / (double)P, pair.as<double>(), NV, st));
+        // sum |z| of the patch (no crop term: sx = sy = 0)
+        HIPCHK(launch_crop_sq<double>(gR.as<double>(), bdev.as<double>(), 0, 0, 1, r, 0, G.X, G.Y, zq,
+                                      (int64_t)K * P, pair.as<double>(), st));
+      }
+      return;
+    }
     for (int64_t q = 0; q < np; ++q) {
       const double* zq = z.as<double>() + (size_t)q * K * P;
       double* dzq = DZdev ? DZdev + (size_t)q * P : odz.as<double>();

@@ -200,6 +200,15 @@ hipError_t launch_crop_sq(const T* Dz, const T* b, int sx, int sy, int st, int r
 
 // ---- gslice.hip: elementwise stages of 2D slices past one CU's LDS (global-pass path) ----
 template <typename T>
+hipError_t launch_gp_zdiag(cpx<T>* C, const cpx<T>* E, const T* sden, T rho, int F, int64_t count,
+                           hipStream_t st);
+template <typename T>
+hipError_t launch_gp_views(const cpx<T>* Z, const cpx<T>* dhat, cpx<T>* out, int F, int K, int NV,
+                           hipStream_t st);
+template <typename T>
+hipError_t launch_gp_crop(const T* R, const T* b, T* DZ, int sbx, int sby, int r, int X, int Y,
+                          T scale, T* part, int count, hipStream_t st);
+template <typename T>
 hipError_t launch_gp_prolog(int mode, const T* a, T* b, const T* usup, int sx, int sy, int o,
                             T theta, int KG, int r, T* R, int X, int Y, int64_t count,
                             hipStream_t st);

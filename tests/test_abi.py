@@ -93,24 +93,25 @@ def test_supported_reports_reasons(L):
     eb = L.errbuf()
     p = _problem(L, 1)
     assert L.lib().ccsc_supported(C.byref(p), eb, len(eb)) == 0
-    # 4D views on a 160 x 160 grid: the LDS slice kernels cannot hold a 160^2 slice and the
-    # 4D learner has no global-pass fallback -> UNSUPPORTED with the planner's reason
-    p = _problem(L, 3, sb=(150, 150), n=4, K=3)
-    p.views[0] = p.views[1] = 2
+    # 3D clips on a 160 x 160 x 16 grid: the LDS plane kernels cannot hold a 160^2 plane and
+    # the 3D learner has no global-pass fallback -> UNSUPPORTED with the planner's reason
+    p = _problem(L, 2, sb=(150, 150, 6), n=4, K=3)
     p.ni = 2
     rc = L.lib().ccsc_supported(C.byref(p), eb, len(eb))
     assert rc == L.CCSC_E_UNSUPPORTED and b"radix plan" in eb.value
 
 
-@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("variant", [0, 1, 3])
 @pytest.mark.parametrize("sb", [(150, 150), (252, 150), (100, 124), (400, 400)])
 def test_2d_grids_past_lds_supported(L, variant, sb):
-    """2D learner grids whose slice does not fit one CU's LDS (VERDICT r04 missing item 1)
-    run on the global line passes: 160^2, 262 x 160 (a generic 131 pass), 110 x 134 (a
-    radix-67 line past the slice kernels' task budget) and 410^2, dP and dZ."""
+    """2D (and 4D view) grids whose slice does not fit one CU's LDS (VERDICT r04 missing
+    item 1) run on the global line passes: 160^2, 262 x 160 (a generic 131 pass), 110 x 134
+    (a radix-67 line past the slice kernels' task budget) and 410^2; dP, dZ and L4."""
     eb = L.errbuf()
-    p = _problem(L, variant, sb=sb, n=8, K=3)
+    p = _problem(L, variant, sb=sb, n=4, K=3)
     p.ni = 2
+    if variant == 3:
+        p.views[0] = p.views[1] = 2
     assert L.lib().ccsc_supported(C.byref(p), eb, len(eb)) == 0, eb.value
 
 
