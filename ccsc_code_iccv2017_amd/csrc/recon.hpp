@@ -40,9 +40,13 @@ struct ColGeom {
 };
 
 // Line kernels run 256-thread workgroups (several per CU: their LDS tiles are small) and
-// hold up to kLineGT generic-radix tasks per thread across a pass barrier.
+// hold up to kLineGT generic-radix tasks per thread across a pass barrier.  Two, not four:
+// the generic tasks' accumulators set the kernels' registers (~160 VGPRs at four, ~100 at
+// two), so two allow four workgroups per CU, as many as the 40 KB LDS tiles do -- same-box
+// solver bench: inpainting 0.587 -> 0.532, Poisson 2.40 -> 2.13, video 0.713 -> 0.643 ms per
+// iteration (profiles/r05/solver_gt_ab.txt)
 constexpr int kLineNT = 256;
-constexpr int kLineGT = 4;
+constexpr int kLineGT = 2;
 constexpr int kLineBS = 1;   // native-pass butterflies per thread: maxb_for_radix * BS
 
 constexpr int kRowParts = 5;   // partial sums per row workgroup (see RowArgs)
