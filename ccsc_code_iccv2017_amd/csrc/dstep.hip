@@ -1190,6 +1190,171 @@ __global__ __launch_bounds__(64 * kWbWG) __attribute__((amdgpu_waves_per_eu(KR <
   }
 }
 
+// k_dsolve_wbv with the views' right-hand sides staged through LDS (NV <= 32, two row
+// segments; C5: 0.809 -> 0.754 ms per launch, 19.8 -> 19.3 ms per outer iteration,
+// profiles/r05/c5_wbs_ab.txt): Ch and Dh are [blk][k][uv][F], so a lane's own (view, k) element is one
+// 16-B piece of a line F apart from its neighbour view's -- every load and store
+// instruction of k_dsolve_wbv touched ~50 lines (C5: the texture-address unit 76% busy,
+// 3.3 GB of L2 read requests for 1 GB of data).  Here the workgroup's 8 waves (8
+// consecutive f) move a chunk of kWbsCH rows per segment cooperatively: consecutive
+// threads take consecutive f of one (k, uv) row, 128 contiguous bytes, into an LDS tile
+// [row][f][uv] (uv padded to 33: each wave then reads its f's views conflict-free), and the
+// solutions leave the same way.  The next chunk's loads are in flight (registers) under the
+// current chunk's products.  Waves past F run along (clamped operands, nothing stored) so
+// every wave meets the barriers.
+constexpr int kWbsCH = 4;   // rows per segment and chunk (2: 20.07, 8: 19.91, 4: 19.33 ms per C5 iteration)
+constexpr int kWbsLD = 33;
+__host__ __device__ constexpr size_t wbs_stage_elems() { return (size_t)2 * kWbsCH * kWbWG * kWbsLD; }
+template <typename T, int KR>
+__global__ __launch_bounds__(64 * kWbWG) __attribute__((amdgpu_waves_per_eu(2))) void k_dsolve_wbs(
+    const cpx<T>* __restrict__ L, const cpx<T>* __restrict__ h, const cpx<T>* __restrict__ Ch,
+    cpx<T>* __restrict__ Dh, int F, int K, T rho, int fgroups, int ntot, int NV, int ni, int Kp) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int g = xcd_group(ntot);
+  if (g < 0) return;   // the whole workgroup
+  const int blk = g / fgroups;
+  const int fb = (g - blk * fgroups) * kWbWG;
+  const int f = min(fb + wave, F - 1);   // waves past F: clamped, results not stored
+  const int sz = ni * K + ni * ni;
+  cpx<T>* sA = reinterpret_cast<cpx<T>*>(smem) + wave * (sz + kWbvPad);
+  cpx<T>* SB = reinterpret_cast<cpx<T>*>(smem) + kWbWG * (sz + kWbvPad);
+  const cpx<T>* slot = L + ((int64_t)blk * F + f) * Kp;
+  for (int i = lane; i < sz + kWbvPad; i += 64) sA[i] = i < sz ? slot[i] : cpx<T>{(T)0, (T)0};
+  const cpx<T> zero = {(T)0, (T)0};
+  const int v = lane & 31, hh = lane >> 5;
+  const int KH = (K + 1) / 2, k0 = hh * KH;
+  const int lv = min(v, NV - 1);
+  const int64_t cs = (int64_t)NV * F;   // k stride of Ch / Dh
+  const cpx<T>* hf = h + ((int64_t)blk * F + f) * NV * K + lv * K;   // [blk][f][uv][k]
+  const cpx<T>* Cblk = Ch + (int64_t)blk * K * cs;
+  cpx<T>* Dblk = Dh + (int64_t)blk * K * cs;
+  constexpr int NCH = (KR + kWbsCH - 1) / kWbsCH;
+  constexpr int EPT = (int)(2 * kWbsCH * 32 * kWbWG / (64 * kWbWG));   // staged elements per thread
+  // element e of a chunk: f offset fl = e & 7, view uv = (e >> 3) & 31, tile row kk = e >> 8
+  // (segment kk / kWbsCH, row c kWbsCH + kk % kWbsCH of it)
+  auto rowk = [&](int c, int kk) {
+    const int i = c * kWbsCH + (kk % kWbsCH);
+    return i < KH ? (kk / kWbsCH) * KH + i : K;   // K: past the segment
+  };
+  auto sbi = [](int kk, int fl, int uv) { return (kk * kWbWG + fl) * kWbsLD + uv; };
+  cpx<T> pre[EPT];
+  auto gload = [&](int c) {
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {
+      const int e = tid + j * 64 * kWbWG;
+      const int fl = e & 7, uv = (e >> 3) & 31, kk = e >> 8;
+      const int k = rowk(c, kk), ff = fb + fl;
+      pre[j] = ldc_if(k < K && uv < NV && ff < F, Cblk + (int64_t)k * cs + (int64_t)uv * F + ff);
+    }
+  };
+  auto sput = [&]() {
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {
+      const int e = tid + j * 64 * kWbWG;
+      SB[sbi(e >> 8, e & 7, (e >> 3) & 31)] = pre[j];
+    }
+  };
+  cpx<T> r[KR];   // rows past KR >= KH are zero: skipped at compile time
+  cpx<T> t[kWbMaxNi];
+#pragma unroll
+  for (int p = 0; p < kWbMaxNi; ++p) t[p] = zero;
+  int ar[kWbMaxNi];
+#pragma unroll
+  for (int p = 0; p < kWbMaxNi; ++p) ar[p] = min(p, ni - 1) * K + k0;
+  gload(0);
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    __syncthreads();   // the previous chunk's tile reads are done (and sA is written)
+    sput();
+    __syncthreads();
+    if (c + 1 < NCH) gload(c + 1);
+#pragma unroll
+    for (int i = 0; i < kWbsCH; ++i) {
+      const int ii = c * kWbsCH + i;
+      if (ii >= KR) break;
+      const bool ok = ii < KH && k0 + ii < K;
+      const cpx<T> cv = SB[sbi(hh * kWbsCH + i, wave, v)];
+      const cpx<T> hv = hf[min(k0 + ii, K - 1)];
+      r[ii] = {ok ? fma(rho, cv.x, hv.x) : (T)0, ok ? fma(rho, cv.y, hv.y) : (T)0};
+      asm volatile("" : "+v"(r[ii].x), "+v"(r[ii].y));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int p = 0; p < kWbMaxNi; ++p) {
+#pragma unroll
+      for (int i = 0; i < kWbsCH; ++i) {
+        const int ii = c * kWbsCH + i;
+        if (ii >= KR) break;
+        const cpx<T> a = sA[ar[p] + ii];
+        t[p].x = fma(a.x, r[ii].x, fma(-a.y, r[ii].y, t[p].x));
+        t[p].y = fma(a.x, r[ii].y, fma(a.y, r[ii].x, t[p].y));
+      }
+      asm volatile("" : "+v"(t[p].x), "+v"(t[p].y));
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+#pragma unroll
+  for (int p = 0; p < kWbMaxNi; ++p) t[p] = {half_swap_sum(t[p].x), half_swap_sum(t[p].y)};
+  // M s = t (as k_dsolve_wbv)
+  const cpx<T>* lm = sA + ni * K;
+  T dinv[kWbMaxNi];
+#pragma unroll
+  for (int j = 0; j < kWbMaxNi; ++j) dinv[j] = (T)1 / lm[min(j, ni - 1) * (ni + 1)].x;
+#pragma unroll
+  for (int j = 0; j < kWbMaxNi; ++j) {
+    if (j < ni) {
+      t[j] = cscale(t[j], dinv[j]);
+#pragma unroll
+      for (int q = j + 1; q < kWbMaxNi; ++q)
+        if (q < ni) t[q] = cmsub(t[q], lm[q * ni + j], t[j]);
+    }
+  }
+#pragma unroll
+  for (int j = kWbMaxNi - 1; j >= 0; --j) {
+    if (j < ni) {
+      t[j] = cscale(t[j], dinv[j]);
+#pragma unroll
+      for (int q = 0; q < j; ++q) t[q] = cmsubc(t[q], lm[j * ni + q], t[j]);
+    }
+  }
+#pragma unroll
+  for (int p = 0; p < kWbMaxNi; ++p)
+    if (p >= ni) t[p] = zero;
+  // x = (r - A^H s) / rho, staged out chunk by chunk
+  int xo = wave * (sz + kWbvPad);
+  asm volatile("" : "+s"(xo));
+  const cpx<T>* sA2 = reinterpret_cast<const cpx<T>*>(smem) + xo;
+  const T irho = (T)1 / rho;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    __syncthreads();   // the tile is free
+#pragma unroll
+    for (int i = 0; i < kWbsCH; ++i) {
+      const int ii = c * kWbsCH + i;
+      if (ii >= KR) break;
+      cpx<T> x = r[ii];
+#pragma unroll
+      for (int p = 0; p < kWbMaxNi; ++p) {   // x -= conj(A[p][k]) s_p
+        const cpx<T> a = sA2[ar[p] + ii];
+        x.x = fma(-a.x, t[p].x, fma(-a.y, t[p].y, x.x));
+        x.y = fma(-a.x, t[p].y, fma(a.y, t[p].x, x.y));
+      }
+      SB[sbi(hh * kWbsCH + i, wave, v)] = cscale(x, irho);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {
+      const int e = tid + j * 64 * kWbWG;
+      const int fl = e & 7, uv = (e >> 3) & 31, kk = e >> 8;
+      const int k = rowk(c, kk), ff = fb + fl;
+      if (k < K && uv < NV && ff < F) Dblk[(int64_t)k * cs + (int64_t)uv * F + ff] = SB[sbi(kk, fl, uv)];
+    }
+  }
+}
+
 template <typename T>
 hipError_t launch_gram_wb(const cpx<T>* Zh, const cpx<T>* Bh, cpx<T>* L, cpx<T>* h, int F, int K,
                           int ni, T rho, int NV, hipStream_t st) {
@@ -1229,7 +1394,20 @@ hipError_t launch_dsolve_wb(const cpx<T>* L, const cpx<T>* h, const cpx<T>* Ch, 
       hipLaunchKernelGGL(kern, dim3(grid.x), dim3(64 * kWbWG), smem, st, L, h, Ch, Dh, F, K, rho,
                          fgroups, n, NV, ni, K * (K + 1) / 2);
     };
-    if (NV <= 32) {   // two row segments of KH = ceil(K / 2) <= 32
+    const char* es = std::getenv("CCSC_WB_STAGE");   // A/B: CCSC_WB_STAGE=0 keeps k_dsolve_wbv
+    if (NV <= 32 && !(es && es[0] == '0')) {   // staged views (k_dsolve_wbs)
+      const int kh = (K + 1) / 2;
+      const size_t smem2 = smem + wbs_stage_elems() * sizeof(cpx<T>);
+      auto go2 = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(grid.x), dim3(64 * kWbWG), smem2, st, L, h, Ch, Dh, F, K, rho,
+                           fgroups, n, NV, ni, K * (K + 1) / 2);
+      };
+      if (kh <= 8) go2(k_dsolve_wbs<T, 8>);
+      else if (kh <= 16) go2(k_dsolve_wbs<T, 16>);
+      else if (kh <= 24) go2(k_dsolve_wbs<T, 24>);
+      else if (kh <= 28) go2(k_dsolve_wbs<T, 28>);
+      else go2(k_dsolve_wbs<T, 32>);
+    } else if (NV <= 32) {   // two row segments of KH = ceil(K / 2) <= 32
       const int kh = (K + 1) / 2;
       if (kh <= 8) go(k_dsolve_wbv<T, 8, 2>);
       else if (kh <= 16) go(k_dsolve_wbv<T, 16, 2>);
