@@ -613,13 +613,17 @@ __device__ __forceinline__ void wave_sync_lds() {
   __builtin_amdgcn_wave_barrier();
 }
 
-bool dsolve_tile_ok(int K, int NV) { return NV == 1 && K > 64 && K <= 16 * kDtT; }
+// NV right-hand sides per (block, f) -- the 4D views, L23's W wavelengths -- are solved one
+// after the other against the factor tiles the workgroup loaded once (k_dsolve streams the
+// factor twice per group of up to 8 right-hand sides); layouts [blk][k][uv][F] (Ch, Dh) and
+// [blk][f][uv][k] (h)
+bool dsolve_tile_ok(int K, int NV) { return NV >= 1 && NV <= 64 && K > 64 && K <= 16 * kDtT; }
 
 __global__ __launch_bounds__(256) void k_dsolve_tile(const cpx<double>* __restrict__ L,
                                                      const cpx<double>* __restrict__ h,
                                                      const cpx<double>* __restrict__ Ch,
                                                      cpx<double>* __restrict__ Dh, int F, int K,
-                                                     double rho) {
+                                                     double rho, int NV) {
   __shared__ cpx<double> sr[16 * kDtT], sy[16 * kDtT], sx[16 * kDtT], sp[2][kDtT][16];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -649,16 +653,21 @@ __global__ __launch_bounds__(256) void k_dsolve_tile(const cpx<double>* __restri
       Lt[s][q] = ldc_if(tI[s] >= 0 && R < K && C <= R, Lf + C * K - (C * (C - 1)) / 2 + R - C);
     }
   }
-  if (tid < 16 * Tn) {
+  // right-hand side uv: r = h + rho C (thread tid < K holds row tid), prefetched one ahead
+  auto rhs = [&](int uv) {
     cpx<double> v = zero;
-    if (tid < K) {
-      const cpx<double> c = Ch[((int64_t)blk * K + tid) * F + f];
-      const cpx<double> hh = h[((int64_t)blk * F + f) * K + tid];
+    if (tid < K && uv < NV) {
+      const cpx<double> c = Ch[(((int64_t)blk * K + tid) * NV + uv) * F + f];
+      const cpx<double> hh = h[(((int64_t)blk * F + f) * NV + uv) * K + tid];
       v = {hh.x + rho * c.x, hh.y + rho * c.y};
     }
-    sr[tid] = v;
-  }
+    return v;
+  };
+  cpx<double> vn = rhs(0);
+  for (int uv = 0; uv < NV; ++uv) {
+  if (tid < 16 * Tn) sr[tid] = vn;
   __syncthreads();
+  vn = rhs(uv + 1);
   // y = M v for the diagonal tile in slot s, v[i] in vbuf (LDS, this wave's own writes)
   auto diag_fwd = [&](const cpx<double> (&Mt)[4], const cpx<double>* vbuf, cpx<double>* ybuf) {
     cpx<double> v = zero;
@@ -722,16 +731,17 @@ __global__ __launch_bounds__(256) void k_dsolve_tile(const cpx<double>* __restri
     __syncthreads();
   }
   __syncthreads();
-  if (tid < K) Dh[((int64_t)blk * K + tid) * F + f] = sx[tid];
+  if (tid < K) Dh[(((int64_t)blk * K + tid) * NV + uv) * F + f] = sx[tid];
+  }
 }
 
 hipError_t launch_dsolve_tile(const cpx<double>* L, const cpx<double>* h, const cpx<double>* Ch,
-                              cpx<double>* Dh, int nblocks, int F, int K, double rho,
+                              cpx<double>* Dh, int nblocks, int F, int K, double rho, int NV,
                               hipStream_t st) {
   if (nblocks <= 0) return hipSuccess;
-  if (!dsolve_tile_ok(K, 1)) return hipErrorInvalidValue;
+  if (!dsolve_tile_ok(K, NV)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_dsolve_tile, dim3((unsigned)(nblocks * 8 * ((F + 7) / 8))), dim3(256), 0,
-                     st, L, h, Ch, Dh, F, K, rho);
+                     st, L, h, Ch, Dh, F, K, rho, NV);
   return hipGetLastError();
 }
 

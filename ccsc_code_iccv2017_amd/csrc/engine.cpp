@@ -1358,7 +1358,7 @@ struct Session2D {
         else if (dtile)
           HIPCHK(launch_dsolve_tile(L.as<cpx<double>>(), h.as<cpx<double>>(),
                                     Ch.as<cpx<double>>(), Dh.as<cpx<double>>(), (int)nbl, F, K,
-                                    p.rho_d, st));
+                                    p.rho_d, NV, st));
         else
           HIPCHK(launch_dsolve<double>(L.as<cpx<double>>(), h.as<cpx<double>>(),
                                        Ch.as<cpx<double>>(), Dh.as<cpx<double>>(), (int)nbl, F, K,
@@ -1656,6 +1656,9 @@ struct SessionHS {
 
   int outer_done = 0;
   bool finished = false;
+  // 64 < K <= 112: the tile d-solve over the W wavelengths on a factor with inverted
+  // diagonal tiles (dstep.hip; CCSC_DS_TILE=0 keeps the two-sweep k_dsolve)
+  bool hs_dtile = false;
   double obj = std::numeric_limits<double>::quiet_NaN();
   double obj_filter = obj, obj_z = obj;
   std::vector<double> v_obj_d, v_obj_z, v_tim, tr_od, tr_oz, tr_dd, tr_zd;
@@ -1670,6 +1673,10 @@ struct SessionHS {
     if (ctx->nranks != 1)
       throw Err(CCSC_E_UNSUPPORTED, "the 2-3D learner runs on one rank (its d-solve sums over "
                                     "every image per frequency; SURVEY.md 8e: replicas only)");
+    {
+      const char* et = std::getenv("CCSC_DS_TILE");
+      hs_dtile = dsolve_tile_ok(p.K, p.views[0]) && !(et && et[0] == '0');
+    }
     if (!b || !smooth_init) throw Err(CCSC_E_INVALID, "b and smooth_init must not be NULL");
     G = g.G;
     m = plan_hs(p, g);
@@ -1831,6 +1838,8 @@ struct SessionHS {
     // on the matrix cores (gramchol.hip, K <= 192; no right-hand side here: NV = 0)
     HIPCHK(launch_gram_chol_mf(Zh.as<cpx<double>>(), Zh.as<cpx<double>>(), L.as<cpx<double>>(),
                                h.as<cpx<double>>(), F, K, n, p.rho_d, 0, st));
+    // 64 < K <= 112: the tile d-solve over the W wavelengths (factor read once per solve)
+    if (hs_dtile) HIPCHK(launch_invert_diag(L.as<cpx<double>>(), F, K, st));
     for (int id = 0; id < p.max_it_d; ++id) {                                    // L23:102
       // c = 1: masked data split (L23:112, 117, 120-121)
       HIPCHK(launch_hs_data_r2c<double>(v.as<double>(), eD.as<double>(), bdev.as<double>(),
@@ -1842,8 +1851,12 @@ struct SessionHS {
       // d_hat = opt (Z' xi1 + rho xi2) per (bin, wavelength)  (L23:125, 289-295)
       HIPCHK(launch_hs_corr<double>(Zh.as<cpx<double>>(), Xi.as<cpx<double>>(),
                                     h.as<cpx<double>>(), F, W, K, n, st));
-      HIPCHK(launch_dsolve<double>(L.as<cpx<double>>(), h.as<cpx<double>>(), Ch.as<cpx<double>>(),
-                                   Dh.as<cpx<double>>(), 1, F, K, p.rho_d, W, st));
+      if (hs_dtile)
+        HIPCHK(launch_dsolve_tile(L.as<cpx<double>>(), h.as<cpx<double>>(), Ch.as<cpx<double>>(),
+                                  Dh.as<cpx<double>>(), 1, F, K, p.rho_d, W, st));
+      else
+        HIPCHK(launch_dsolve<double>(L.as<cpx<double>>(), h.as<cpx<double>>(), Ch.as<cpx<double>>(),
+                                     Dh.as<cpx<double>>(), 1, F, K, p.rho_d, W, st));
       // d = real(ifft2(d_hat)) (L23:126); support of d - d_D{2} -> u_D{2} of the next d-iteration
       HIPCHK(launch_c2r_dout<double>(Dh.as<cpx<double>>(), D.as<double>(), yD.as<double>(),
                                      supp.as<double>(), dnorm.as<double>(), 0, KG, twc, G, r, st));

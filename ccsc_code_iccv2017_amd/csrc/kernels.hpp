@@ -130,7 +130,7 @@ hipError_t launch_dsolve(const cpx<T>* L, const cpx<T>* h, const cpx<T>* Ch, cpx
 bool dsolve_tile_ok(int K, int NV);
 hipError_t launch_invert_diag(cpx<double>* L, int F, int K, hipStream_t st);
 hipError_t launch_dsolve_tile(const cpx<double>* L, const cpx<double>* h, const cpx<double>* Ch,
-                              cpx<double>* Dh, int nblocks, int F, int K, double rho,
+                              cpx<double>* Dh, int nblocks, int F, int K, double rho, int NV,
                               hipStream_t st);
 // Woodbury form for blocks of few patches (woodbury_fits): per f the slot of
 // Kp = K(K+1)/2 complex holds A (ni x K, row-major) and the Cholesky factor of

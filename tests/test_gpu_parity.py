@@ -166,6 +166,38 @@ def test_learn_2d_grids_past_lds_match_oracle(gpu_ctx, variant, sb, verbose, tol
         np.testing.assert_allclose(it_e["trace"]["obj_z"], np.array(tr_o["obj_z"]), rtol=1e-9)
 
 
+def test_learn_4d_tile_dsolve_many_views_matches_oracle(gpu_ctx):
+    """The tile d-solve over several right-hand sides (dstep.hip k_dsolve_tile, NV = 4 views,
+    K = 72 on the Cholesky factor with inverted diagonal tiles) against the oracle and
+    against the two-sweep k_dsolve (CCSC_DS_TILE=0)."""
+    import os
+    from ccsc_code_iccv2017_amd import learners as E
+    rng = np.random.default_rng(13)
+    sb, UV, psf, K, n = (10, 9), 2, 5, 72, 4
+    r = psf // 2
+    X, Y = sb[0] + 2 * r, sb[1] + 2 * r
+    b = rng.standard_normal((sb[0], sb[1], UV, UV, n))
+    init = {"d": rng.standard_normal((psf, psf, UV, UV, K)),
+            "z": rng.standard_normal((X, Y, 1, 1, K, n))}
+    ks = [psf, psf, UV, UV, K]
+    d_o, z_o, DZ_o, obj_o, it_o, tr_o = O.learn_4d(b, ks, 1.0, 1.0, 2, 0.0, "all", init,
+                                                   trace_objective=True)
+    outs = {}
+    for tile in ("1", "0"):
+        os.environ["CCSC_DS_TILE"] = tile
+        try:
+            outs[tile] = E.admm_learn_conv4D_lightfield(b, ks, 1.0, 1.0, 2, 0.0, "all", init,
+                                                        trace_objective=True, ctx=gpu_ctx,
+                                                        dfactor="cholesky")
+        finally:
+            del os.environ["CCSC_DS_TILE"]
+    for e in outs.values():
+        assert _rel(e[0], d_o) < 1e-7
+        assert _rel(e[1].real, z_o.real) < 1e-7
+        np.testing.assert_allclose(e[4]["trace"]["obj_z"], np.array(tr_o["obj_z"]), rtol=1e-9)
+    assert _rel(outs["1"][0], outs["0"][0]) < 1e-9
+
+
 def test_learn_4d_cholesky_many_views_matches_oracle(gpu_ctx):
     """The K x K D-factor with many right-hand sides per frequency (4D, 16 views, K = 20,
     CCSC_DFACTOR_CHOLESKY): K NV = 320 > 256 takes gramchol.hip's eight h slots per thread
