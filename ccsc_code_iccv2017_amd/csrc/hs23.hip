@@ -369,10 +369,11 @@ __global__ __launch_bounds__(256) void k_max_parts(const T* __restrict__ a, int6
 // ---------------------------------------------------------------------------
 // Host launchers
 // ---------------------------------------------------------------------------
-template <typename T, bool CONJA>
-static hipError_t bin_gemm(BinGemm<T> g, hipStream_t st) {
-  constexpr int TM = 4, TN = 4;
-  if (g.M <= 0 || g.N <= 0 || g.F <= 0) return hipSuccess;
+// register tile TM x TN per thread: 4 x 8 where N allows (C3: 4 x 4 0.0977, 8 x 4 0.0930,
+// 4 x 8 0.0919 s per outer iteration, profiles/r05/bin_gemm_tile_ab.txt), 4 x 4 for the
+// solvers' one-image GEMMs (N < 8)
+template <typename T, bool CONJA, int TM, int TN>
+static hipError_t bin_gemm_t(BinGemm<T> g, hipStream_t st) {
   g.mtiles = (g.M + TM - 1) / TM;
   g.ntiles = (g.N + TN - 1) / TN;
   const int64_t nwg = (int64_t)((g.F + kBgNT - 1) / kBgNT) * g.mtiles * g.ntiles;
@@ -380,6 +381,11 @@ static hipError_t bin_gemm(BinGemm<T> g, hipStream_t st) {
   const dim3 grid((unsigned)nwg);
   hipLaunchKernelGGL((k_bin_gemm<T, TM, TN, CONJA>), grid, dim3(kBgNT), 0, st, g);
   return hipGetLastError();
+}
+template <typename T, bool CONJA>
+static hipError_t bin_gemm(BinGemm<T> g, hipStream_t st) {
+  if (g.M <= 0 || g.N <= 0 || g.F <= 0) return hipSuccess;
+  return g.N >= 8 ? bin_gemm_t<T, CONJA, 4, 8>(g, st) : bin_gemm_t<T, CONJA, 4, 4>(g, st);
 }
 
 // Yv [n][W][F] = sum_k dhat [K][W][F] * zhat [n][K][F]
