@@ -850,7 +850,9 @@ __device__ __forceinline__ int xcd_group(int ntot) {
   return g < ntot ? g : -1;
 }
 
-template <typename T, int RPL>
+// HT: h in the [k][uv][F] layout of Ch (block-local), which k_dsolve_wbs stages through LDS
+// with the right-hand sides; else [f][uv][k]
+template <typename T, int RPL, bool HT = false>
 __global__ __launch_bounds__(64 * kWbWG) void k_gram_wb(const cpx<T>* __restrict__ Zh,
                                                         const cpx<T>* __restrict__ Bh,
                                                         cpx<T>* __restrict__ L,
@@ -941,7 +943,7 @@ __global__ __launch_bounds__(64 * kWbWG) void k_gram_wb(const cpx<T>* __restrict
 #pragma unroll
     for (int u = 0; u < RPL; ++u) {
       const int i = lane + 64 * u;
-      if (i < K) h[((int64_t)f * NV + uv) * K + i] = acc[u];
+      if (i < K) h[HT ? ((int64_t)i * NV + uv) * F + f : ((int64_t)f * NV + uv) * K + i] = acc[u];
     }
   }
 }
@@ -1232,7 +1234,7 @@ __global__ __launch_bounds__(64 * kWbWG) __attribute__((amdgpu_waves_per_eu(KR <
   }
 }
 
-// k_dsolve_wbv with the views' right-hand sides staged through LDS (NV <= 32, two row
+// k_dsolve_wbv with the views' right-hand sides r = h + rho C staged through LDS (NV <= 32, two row
 // segments; C5: 0.809 -> 0.754 ms per launch, 19.8 -> 19.3 ms per outer iteration,
 // profiles/r05/c5_wbs_ab.txt): Ch and Dh are [blk][k][uv][F], so a lane's own (view, k) element is one
 // 16-B piece of a line F apart from its neighbour view's -- every load and store
@@ -1269,7 +1271,7 @@ __global__ __launch_bounds__(64 * kWbWG) __attribute__((amdgpu_waves_per_eu(2)))
   const int KH = (K + 1) / 2, k0 = hh * KH;
   const int lv = min(v, NV - 1);
   const int64_t cs = (int64_t)NV * F;   // k stride of Ch / Dh
-  const cpx<T>* hf = h + ((int64_t)blk * F + f) * NV * K + lv * K;   // [blk][f][uv][k]
+  const cpx<T>* Hblk = h + (int64_t)blk * K * cs;   // [blk][k][uv][F] (k_gram_wb<HT>)
   const cpx<T>* Cblk = Ch + (int64_t)blk * K * cs;
   cpx<T>* Dblk = Dh + (int64_t)blk * K * cs;
   constexpr int NCH = (KR + kWbsCH - 1) / kWbsCH;
@@ -1288,7 +1290,10 @@ __global__ __launch_bounds__(64 * kWbWG) __attribute__((amdgpu_waves_per_eu(2)))
       const int e = tid + j * 64 * kWbWG;
       const int fl = e & 7, uv = (e >> 3) & 31, kk = e >> 8;
       const int k = rowk(c, kk), ff = fb + fl;
-      pre[j] = ldc_if(k < K && uv < NV && ff < F, Cblk + (int64_t)k * cs + (int64_t)uv * F + ff);
+      const bool ok = k < K && uv < NV && ff < F;
+      const int64_t o = (int64_t)k * cs + (int64_t)uv * F + ff;
+      const cpx<T> cv = ldc_if(ok, Cblk + o), hv = ldc_if(ok, Hblk + o);
+      pre[j] = {fma(rho, cv.x, hv.x), fma(rho, cv.y, hv.y)};   // r = h + rho c
     }
   };
   auto sput = [&]() {
@@ -1317,9 +1322,8 @@ __global__ __launch_bounds__(64 * kWbWG) __attribute__((amdgpu_waves_per_eu(2)))
       const int ii = c * kWbsCH + i;
       if (ii >= KR) break;
       const bool ok = ii < KH && k0 + ii < K;
-      const cpx<T> cv = SB[sbi(hh * kWbsCH + i, wave, v)];
-      const cpx<T> hv = hf[min(k0 + ii, K - 1)];
-      r[ii] = {ok ? fma(rho, cv.x, hv.x) : (T)0, ok ? fma(rho, cv.y, hv.y) : (T)0};
+      const cpx<T> rv = SB[sbi(hh * kWbsCH + i, wave, v)];
+      r[ii] = {ok ? rv.x : (T)0, ok ? rv.y : (T)0};
       asm volatile("" : "+v"(r[ii].x), "+v"(r[ii].y));
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -1397,13 +1401,23 @@ __global__ __launch_bounds__(64 * kWbWG) __attribute__((amdgpu_waves_per_eu(2)))
   }
 }
 
+// the many-view d-solve runs staged (k_dsolve_wbs) and then reads h in Ch's layout
+static bool wb_staged(int K, int NV, int F) {
+  const char* es = std::getenv("CCSC_WB_STAGE");   // A/B: CCSC_WB_STAGE=0 keeps k_dsolve_wbv
+  return NV > 1 && NV <= 32 && K <= 64 && !(es && es[0] == '0') &&
+         (int64_t)K * NV * F * (int64_t)sizeof(cpx<double>) < ((int64_t)1 << 32);
+}
+
 template <typename T>
 hipError_t launch_gram_wb(const cpx<T>* Zh, const cpx<T>* Bh, cpx<T>* L, cpx<T>* h, int F, int K,
                           int ni, T rho, int NV, hipStream_t st) {
   if (!woodbury_ok(K, ni)) return hipErrorInvalidValue;
   const int Kp = K * (K + 1) / 2;
   const dim3 grid((unsigned)((((F + kWbWG - 1) / kWbWG + 7) / 8) * 8));   // whole XCD rounds
-  if (K <= 64)
+  if (wb_staged(K, NV, F))
+    hipLaunchKernelGGL((k_gram_wb<T, 1, true>), grid, dim3(64 * kWbWG), 0, st, Zh, Bh, L, h, F, K,
+                       ni, rho, NV, Kp);
+  else if (K <= 64)
     hipLaunchKernelGGL((k_gram_wb<T, 1>), grid, dim3(64 * kWbWG), 0, st, Zh, Bh, L, h, F, K, ni,
                        rho, NV, Kp);
   else
@@ -1436,8 +1450,7 @@ hipError_t launch_dsolve_wb(const cpx<T>* L, const cpx<T>* h, const cpx<T>* Ch, 
       hipLaunchKernelGGL(kern, dim3(grid.x), dim3(64 * kWbWG), smem, st, L, h, Ch, Dh, F, K, rho,
                          fgroups, n, NV, ni, K * (K + 1) / 2);
     };
-    const char* es = std::getenv("CCSC_WB_STAGE");   // A/B: CCSC_WB_STAGE=0 keeps k_dsolve_wbv
-    if (NV <= 32 && !(es && es[0] == '0')) {   // staged views (k_dsolve_wbs)
+    if (wb_staged(K, NV, F)) {   // staged views (k_dsolve_wbs; h in Ch's layout, k_gram_wb)
       const int kh = (K + 1) / 2;
       const size_t smem2 = smem + wbs_stage_elems() * sizeof(cpx<T>);
       auto go2 = [&](auto kern) {
