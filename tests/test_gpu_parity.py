@@ -198,6 +198,38 @@ def test_learn_4d_tile_dsolve_many_views_matches_oracle(gpu_ctx):
     assert _rel(outs["1"][0], outs["0"][0]) < 1e-9
 
 
+def test_woodbury_staged_matches_per_lane(gpu_ctx):
+    """The LDS-staged many-view Woodbury d-solve (k_dsolve_wbs, h in Ch's layout) against the
+    per-lane form (CCSC_WB_STAGE=0: k_dsolve_wbv) and the oracle: 4D, 3 x 3 views, K = 24,
+    ni = 4 (Woodbury), two blocks."""
+    import os
+    from ccsc_code_iccv2017_amd import learners as E
+    rng = np.random.default_rng(31)
+    sb, UV, psf, K, n = (10, 9), 3, 5, 24, 16
+    r = psf // 2
+    X, Y = sb[0] + 2 * r, sb[1] + 2 * r
+    b = rng.standard_normal((sb[0], sb[1], UV, UV, n))
+    init = {"d": rng.standard_normal((psf, psf, UV, UV, K)),
+            "z": rng.standard_normal((X, Y, 1, 1, K, n))}
+    ks = [psf, psf, UV, UV, K]
+    d_o, z_o, DZ_o, obj_o, it_o, tr_o = O.learn_4d(b, ks, 1.0, 1.0, 2, 0.0, "all", init,
+                                                   trace_objective=True)
+    outs = {}
+    for stage in ("1", "0"):
+        os.environ["CCSC_WB_STAGE"] = stage
+        try:
+            outs[stage] = E.admm_learn_conv4D_lightfield(b, ks, 1.0, 1.0, 2, 0.0, "all", init,
+                                                         trace_objective=True, ctx=gpu_ctx,
+                                                         dfactor="woodbury")
+        finally:
+            del os.environ["CCSC_WB_STAGE"]
+    for e in outs.values():
+        assert _rel(e[0], d_o) < 1e-7
+        assert _rel(e[1].real, z_o.real) < 1e-7
+        np.testing.assert_allclose(e[4]["trace"]["obj_z"], np.array(tr_o["obj_z"]), rtol=1e-9)
+    assert _rel(outs["1"][0], outs["0"][0]) < 1e-10
+
+
 def test_learn_4d_cholesky_many_views_matches_oracle(gpu_ctx):
     """The K x K D-factor with many right-hand sides per frequency (4D, 16 views, K = 20,
     CCSC_DFACTOR_CHOLESKY): K NV = 320 > 256 takes gramchol.hip's eight h slots per thread
