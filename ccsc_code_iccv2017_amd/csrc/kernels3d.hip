@@ -29,6 +29,17 @@ __device__ __forceinline__ int64_t ttile_idx(int t, int f2, int Tn, int Xh, int 
   return ((int64_t)(y * ntile + tile) * Tn + t) * tc + c;
 }
 
+// XCD-aware plane order: logical plane L = (b mod 8) per + b / 8 (per = gridDim / 8), so the
+// workgroups of one XCD take consecutive planes (t) of a slice -- the t-minor spectra of
+// neighbouring planes share 128-B lines (k_tsolve3's order), which one L2 then fetches and
+// writes whole instead of every XCD a 32-B piece of each
+__device__ __forceinline__ int64_t plane_of_block(int64_t nplanes) {
+  const int64_t per = gridDim.x >> 3;
+  const int64_t L = (int64_t)(blockIdx.x & 7) * per + (blockIdx.x >> 3);
+  return L < nplanes ? L : -1;
+}
+__host__ inline unsigned plane_grid(int64_t nplanes) { return (unsigned)(((nplanes + 7) / 8) * 8); }
+
 template <typename T, int RM>
 __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(slice_waves<RM>())))
 void k_plane_fwd(int mode, const T* __restrict__ a,
@@ -36,14 +47,16 @@ void k_plane_fwd(int mode, const T* __restrict__ a,
                                                    int sx, int sy, int st, int o, T theta,
                                                    int KG, int r, cpx<T>* __restrict__ dst,
                                                    int Tn, const cpx<T>* __restrict__ twg,
-                                                   Grid2D G, int tc) {
+                                                   Grid2D G, int tc, int64_t nplanes) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int64_t pl = plane_of_block(nplanes);
+  if (pl < 0) return;   // the whole workgroup
   Smem<T> S = carve<T>(smem, G);
   using Q = SG<RM>;
   const int GX = Q::X(G), GY = Q::Y(G), RS = Q::RS(G), GF = Q::F(G), GXh = Q::Xh(G);
   if constexpr (!Q::fixed) load_twiddles(S.tw, twg, G.ntw);
-  const int64_t slice = blockIdx.x / Tn;
-  const int t = blockIdx.x - (int)(slice * Tn);
+  const int64_t slice = pl / Tn;
+  const int t = (int)(pl - slice * Tn);
   const int P = GX * GY;
   const int s = 2 * r + 1;
   if (mode == 0) {
@@ -158,14 +171,16 @@ void k_plane_inv(int mode, const cpx<T>* src,
                                                    int64_t nfirst, T scale, int r, int Tn,
                                                    const cpx<T>* __restrict__ twg, Grid2D G,
                                                    int tc, T* __restrict__ state, T theta, int wz,
-                                                   cpx<T>* nxt) {
+                                                   cpx<T>* nxt, int64_t nplanes) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int64_t pl = plane_of_block(nplanes);
+  if (pl < 0) return;   // the whole workgroup
   Smem<T> S = carve<T>(smem, G);
   using Q = SG<RM>;
   const int GX = Q::X(G), GY = Q::Y(G), GF = Q::F(G), GXh = Q::Xh(G);
   if constexpr (!Q::fixed) load_twiddles(S.tw, twg, G.ntw);
-  const int64_t slice = blockIdx.x / Tn;
-  const int t = blockIdx.x - (int)(slice * Tn);
+  const int64_t slice = pl / Tn;
+  const int t = (int)(pl - slice * Tn);
   if (tc > 0) {   // t-minor tiles (k_tsolve3's order)
     const int ntile = (GXh + tc - 1) / tc;
     const cpx<T>* in = src + slice * ((int64_t)GY * ntile * Tn * tc);
@@ -495,9 +510,9 @@ hipError_t launch_plane_fwd(int mode, const T* a, T* b, const T* usup, int sx, i
                             const cpx<T>* tw, const Grid2D& G, hipStream_t stream, int tc) {
   if (nslices <= 0) return hipSuccess;
   auto go = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3((unsigned)(nslices * Tn)), dim3(kNT),
+    hipLaunchKernelGGL(kern, dim3(plane_grid(nslices * Tn)), dim3(kNT),
                        slice_smem_bytes(G, sizeof(T)), stream, mode, a, b, usup, sx, sy, st, o,
-                       theta, KG, r, dst, Tn, tw, G, tc);
+                       theta, KG, r, dst, Tn, tw, G, tc, nslices * Tn);
   };
   if (grid_is74(G)) go(k_plane_fwd<T, kRm74F>);
   else if (slice_fits(kRm74, G)) go(k_plane_fwd<T, kRm74>);
@@ -615,9 +630,10 @@ hipError_t launch_plane_inv(int mode, const cpx<T>* src, T* dst, const T* yv, T*
   if (mode == 3 && (!state || (norms && !wz))) return hipErrorInvalidValue;
   if (nxt && (mode != 3 || nxt != src)) return hipErrorInvalidValue;
   auto go = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3((unsigned)(nslices * Tn)), dim3(kNT),
+    hipLaunchKernelGGL(kern, dim3(plane_grid(nslices * Tn)), dim3(kNT),
                        slice_smem_bytes(G, sizeof(T)), stream, mode, src, dst, yv, supp, norms,
-                       nfirst, scale, r, Tn, tw, G, tc, state, theta, wz ? 1 : 0, nxt);
+                       nfirst, scale, r, Tn, tw, G, tc, state, theta, wz ? 1 : 0, nxt,
+                       nslices * Tn);
   };
   if (grid_is74(G)) go(k_plane_inv<T, kRm74F>);
   else if (slice_fits(kRm74, G)) go(k_plane_inv<T, kRm74>);
