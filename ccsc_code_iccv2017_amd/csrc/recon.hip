@@ -222,15 +222,21 @@ __global__ __launch_bounds__(kLineNT) void k_rows_pair(RowArgs<T> a, RowArgs<T> 
 template <typename T, int SIGN>
 __global__ __launch_bounds__(kLineNT) void k_cols(cpx<T>* __restrict__ S, cpx<T>* __restrict__ S2,
                                               int64_t n1, ColGeom cg,
-                                              const cpx<T>* __restrict__ tw) {
+                                              const cpx<T>* __restrict__ tw, int64_t ntot) {
   extern __shared__ __align__(16) unsigned char smem_raw[];
   T* lds = reinterpret_cast<T*>(smem_raw);
-  int64_t o = blockIdx.x;
+  // XCD-aware order, tiles of one line set consecutive: logical id L = (b mod 8) per + b / 8,
+  // so the neighbouring column tiles of a line set -- which share the 128-B lines their
+  // TC-column row segments cut -- run on one XCD at about the same time
+  const int64_t per = gridDim.x >> 3;
+  const int64_t L = (int64_t)(blockIdx.x & 7) * per + (blockIdx.x >> 3);
+  if (L >= ntot) return;   // the whole workgroup
+  int64_t o = L / cg.xtiles;
+  const int tile = (int)(L - o * cg.xtiles);
   if (o >= n1) {   // workgroups past the first set's n1 line sets run the second set
     S = S2;
     o -= n1;
   }
-  const int tile = blockIdx.y;
   const int TC = cg.TC, n = cg.n;
   const int c0 = tile * TC;
   const int nc = min(TC, cg.Xh - c0);
@@ -425,12 +431,14 @@ template <typename T>
 hipError_t launch_cols(cpx<T>* S, int sign, int64_t nouter, const ColGeom& cg, const cpx<T>* tw,
                        hipStream_t st, cpx<T>* S2, int64_t nouter2) {
   if (nouter + nouter2 <= 0) return hipSuccess;
-  const dim3 grid((unsigned)(nouter + nouter2), (unsigned)cg.xtiles);
+  const int64_t ntot = (nouter + nouter2) * (int64_t)cg.xtiles;
+  if (ntot >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
+  const dim3 grid((unsigned)(((ntot + 7) / 8) * 8));
   const size_t sm = cols_smem_bytes(cg, sizeof(T));
   if (sign < 0)
-    hipLaunchKernelGGL((k_cols<T, -1>), grid, dim3(kLineNT), sm, st, S, S2, nouter, cg, tw);
+    hipLaunchKernelGGL((k_cols<T, -1>), grid, dim3(kLineNT), sm, st, S, S2, nouter, cg, tw, ntot);
   else
-    hipLaunchKernelGGL((k_cols<T, +1>), grid, dim3(kLineNT), sm, st, S, S2, nouter, cg, tw);
+    hipLaunchKernelGGL((k_cols<T, +1>), grid, dim3(kLineNT), sm, st, S, S2, nouter, cg, tw, ntot);
   return hipGetLastError();
 }
 
