@@ -1269,7 +1269,6 @@ __global__ __launch_bounds__(64 * kWbWG) __attribute__((amdgpu_waves_per_eu(2)))
   const cpx<T> zero = {(T)0, (T)0};
   const int v = lane & 31, hh = lane >> 5;
   const int KH = (K + 1) / 2, k0 = hh * KH;
-  const int lv = min(v, NV - 1);
   const int64_t cs = (int64_t)NV * F;   // k stride of Ch / Dh
   const cpx<T>* Hblk = h + (int64_t)blk * K * cs;   // [blk][k][uv][F] (k_gram_wb<HT>)
   const cpx<T>* Cblk = Ch + (int64_t)blk * K * cs;
