@@ -768,12 +768,13 @@ hipError_t launch_dsolve_tile(const cpx<double>* L, const cpx<double>* h, const 
   if (nblocks <= 0) return hipSuccess;
   if (!dsolve_tile_ok(K, NV)) return hipErrorInvalidValue;
   const dim3 grid((unsigned)(nblocks * 8 * ((F + 7) / 8)));
-  // two right-hand sides per barrier phase (C3: 0.1211 -> 0.1165 s per outer iteration; four:
-  // 169 VGPRs, two waves per SIMD, 0.1217 s)
+  // three right-hand sides per barrier phase (C3: one 0.1211, two 0.1165 -> three (163 VGPRs)
+  // 0.0910 -> 0.0896 s per outer iteration after the GEMM changes; four: 169 VGPRs, two waves
+  // per SIMD, 0.1217 s)
   if (NV == 1)
     hipLaunchKernelGGL(k_dsolve_tile<1>, grid, dim3(256), 0, st, L, h, Ch, Dh, F, K, rho, NV);
   else
-    hipLaunchKernelGGL(k_dsolve_tile<2>, grid, dim3(256), 0, st, L, h, Ch, Dh, F, K, rho, NV);
+    hipLaunchKernelGGL(k_dsolve_tile<3>, grid, dim3(256), 0, st, L, h, Ch, Dh, F, K, rho, NV);
   return hipGetLastError();
 }
 
