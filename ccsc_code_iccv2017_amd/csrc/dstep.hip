@@ -1249,9 +1249,13 @@ __global__ __launch_bounds__(64 * kWbWG) __attribute__((amdgpu_waves_per_eu(KR <
 // every wave meets the barriers.
 constexpr int kWbsCH = 4;   // rows per segment and chunk (2: 20.07, 8: 19.91, 4: 19.33 ms per C5 iteration)
 constexpr int kWbsLD = 33;
-__host__ __device__ constexpr size_t wbs_stage_elems() { return (size_t)2 * kWbsCH * kWbWG * kWbsLD; }
+// waves (consecutive f) per workgroup: 4, so two workgroups share a CU (two waves per SIMD at
+// these registers either way) and one's chunk barriers overlap the other's work (C5: 8 per
+// workgroup 17.1, 4 per workgroup 16.5 ms per outer iteration, profiles/r05/c5_wbs_wg_ab.txt)
+constexpr int kWbsWG = 4;
+__host__ __device__ constexpr size_t wbs_stage_elems() { return (size_t)2 * kWbsCH * kWbsWG * kWbsLD; }
 template <typename T, int KR>
-__global__ __launch_bounds__(64 * kWbWG) __attribute__((amdgpu_waves_per_eu(2))) void k_dsolve_wbs(
+__global__ __launch_bounds__(64 * kWbsWG) __attribute__((amdgpu_waves_per_eu(2))) void k_dsolve_wbs(
     const cpx<T>* __restrict__ L, const cpx<T>* __restrict__ h, const cpx<T>* __restrict__ Ch,
     cpx<T>* __restrict__ Dh, int F, int K, T rho, int fgroups, int ntot, int NV, int ni, int Kp) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1260,11 +1264,11 @@ __global__ __launch_bounds__(64 * kWbWG) __attribute__((amdgpu_waves_per_eu(2)))
   const int g = xcd_group(ntot);
   if (g < 0) return;   // the whole workgroup
   const int blk = g / fgroups;
-  const int fb = (g - blk * fgroups) * kWbWG;
+  const int fb = (g - blk * fgroups) * kWbsWG;
   const int f = min(fb + wave, F - 1);   // waves past F: clamped, results not stored
   const int sz = ni * K + ni * ni;
   cpx<T>* sA = reinterpret_cast<cpx<T>*>(smem) + wave * (sz + kWbvPad);
-  cpx<T>* SB = reinterpret_cast<cpx<T>*>(smem) + kWbWG * (sz + kWbvPad);
+  cpx<T>* SB = reinterpret_cast<cpx<T>*>(smem) + kWbsWG * (sz + kWbvPad);
   const cpx<T>* slot = L + ((int64_t)blk * F + f) * Kp;
   for (int i = lane; i < sz + kWbvPad; i += 64) sA[i] = i < sz ? slot[i] : cpx<T>{(T)0, (T)0};
   const cpx<T> zero = {(T)0, (T)0};
@@ -1275,20 +1279,21 @@ __global__ __launch_bounds__(64 * kWbWG) __attribute__((amdgpu_waves_per_eu(2)))
   const cpx<T>* Cblk = Ch + (int64_t)blk * K * cs;
   cpx<T>* Dblk = Dh + (int64_t)blk * K * cs;
   constexpr int NCH = (KR + kWbsCH - 1) / kWbsCH;
-  constexpr int EPT = (int)(2 * kWbsCH * 32 * kWbWG / (64 * kWbWG));   // staged elements per thread
-  // element e of a chunk: f offset fl = e & 7, view uv = (e >> 3) & 31, tile row kk = e >> 8
+  constexpr int EPT = (int)(2 * kWbsCH * 32 * kWbsWG / (64 * kWbsWG));   // staged elements per thread
+  constexpr int FB = kWbsWG == 8 ? 3 : kWbsWG == 4 ? 2 : 1;   // log2(kWbsWG)
+  // element e of a chunk: f offset fl = e mod kWbsWG, view uv = (e / kWbsWG) mod 32, tile row kk
   // (segment kk / kWbsCH, row c kWbsCH + kk % kWbsCH of it)
   auto rowk = [&](int c, int kk) {
     const int i = c * kWbsCH + (kk % kWbsCH);
     return i < KH ? (kk / kWbsCH) * KH + i : K;   // K: past the segment
   };
-  auto sbi = [](int kk, int fl, int uv) { return (kk * kWbWG + fl) * kWbsLD + uv; };
+  auto sbi = [](int kk, int fl, int uv) { return (kk * kWbsWG + fl) * kWbsLD + uv; };
   cpx<T> pre[EPT];
   auto gload = [&](int c) {
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
-      const int e = tid + j * 64 * kWbWG;
-      const int fl = e & 7, uv = (e >> 3) & 31, kk = e >> 8;
+      const int e = tid + j * 64 * kWbsWG;
+      const int fl = e & (kWbsWG - 1), uv = (e >> FB) & 31, kk = e >> (FB + 5);
       const int k = rowk(c, kk), ff = fb + fl;
       const bool ok = k < K && uv < NV && ff < F;
       const int64_t o = (int64_t)k * cs + (int64_t)uv * F + ff;
@@ -1299,8 +1304,8 @@ __global__ __launch_bounds__(64 * kWbWG) __attribute__((amdgpu_waves_per_eu(2)))
   auto sput = [&]() {
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
-      const int e = tid + j * 64 * kWbWG;
-      SB[sbi(e >> 8, e & 7, (e >> 3) & 31)] = pre[j];
+      const int e = tid + j * 64 * kWbsWG;
+      SB[sbi(e >> (FB + 5), e & (kWbsWG - 1), (e >> FB) & 31)] = pre[j];
     }
   };
   cpx<T> r[KR];   // rows past KR >= KH are zero: skipped at compile time
@@ -1393,8 +1398,8 @@ __global__ __launch_bounds__(64 * kWbWG) __attribute__((amdgpu_waves_per_eu(2)))
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
-      const int e = tid + j * 64 * kWbWG;
-      const int fl = e & 7, uv = (e >> 3) & 31, kk = e >> 8;
+      const int e = tid + j * 64 * kWbsWG;
+      const int fl = e & (kWbsWG - 1), uv = (e >> FB) & 31, kk = e >> (FB + 5);
       const int k = rowk(c, kk), ff = fb + fl;
       if (k < K && uv < NV && ff < F) Dblk[(int64_t)k * cs + (int64_t)uv * F + ff] = SB[sbi(kk, fl, uv)];
     }
@@ -1452,10 +1457,12 @@ hipError_t launch_dsolve_wb(const cpx<T>* L, const cpx<T>* h, const cpx<T>* Ch, 
     };
     if (wb_staged(K, NV, F)) {   // staged views (k_dsolve_wbs; h in Ch's layout, k_gram_wb)
       const int kh = (K + 1) / 2;
-      const size_t smem2 = smem + wbs_stage_elems() * sizeof(cpx<T>);
+      const size_t smem2 = (size_t)kWbsWG * (ni * K + ni * ni + kWbvPad) * sizeof(cpx<T>) +
+                           wbs_stage_elems() * sizeof(cpx<T>);
+      const int fg2 = (F + kWbsWG - 1) / kWbsWG, n2 = nblocks * fg2;
       auto go2 = [&](auto kern) {
-        hipLaunchKernelGGL(kern, dim3(grid.x), dim3(64 * kWbWG), smem2, st, L, h, Ch, Dh, F, K, rho,
-                           fgroups, n, NV, ni, K * (K + 1) / 2);
+        hipLaunchKernelGGL(kern, dim3((unsigned)(((n2 + 7) / 8) * 8)), dim3(64 * kWbsWG), smem2, st,
+                           L, h, Ch, Dh, F, K, rho, fg2, n2, NV, ni, K * (K + 1) / 2);
       };
       if (kh <= 8) go2(k_dsolve_wbs<T, 8>);
       else if (kh <= 16) go2(k_dsolve_wbs<T, 16>);
