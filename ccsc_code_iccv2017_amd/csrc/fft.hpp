@@ -479,7 +479,15 @@ __host__ __device__ constexpr int pfa_slots(int nlines, int M, int QP) {
 
 // gi: where the radix-2 pass left the inputs (the fixed 74-point x pass stores them
 // line-minor so the 37 reads per task are lane-contiguous; g otherwise); g: the output.
-template <typename T, int M, int SIGN, int QP, int NT>
+// PRE: the radix-2 pass before (fft_fixed.hpp fpass2_pairs) stored the symmetric input
+// pairs already formed -- element k1 holds u_0, element 2 + 4 (r - 1) + 2 k1 holds
+// u_r + u_{M-r} and the next one u_r - u_{M-r} -- so each task reads them instead of
+// forming them (the same two adds per pair, once per line instead of once per output group)
+template <int M>
+__host__ __device__ constexpr int pfa_pre_slot(int r, int k1, int dif) {
+  return r == 0 ? k1 : 2 + 4 * (r - 1) + 2 * k1 + dif;
+}
+template <typename T, int M, int SIGN, int QP, int NT, bool PRE = false>
 __device__ __forceinline__ void fft_pass_pfa(T* lds, const LineGeom& g, const LineGeom& gi) {
   constexpr int H = (M - 1) / 2;
   constexpr int NG = (H + QP - 1) / QP;
@@ -506,8 +514,11 @@ __device__ __forceinline__ void fft_pass_pfa(T* lds, const LineGeom& g, const Li
   };
   auto body = [&](auto gc, auto k1c) {
     constexpr int gg = decltype(gc)::value;
+    constexpr int kk = decltype(k1c)::value;
     {
-      const cpx<T> u0 = in(std::integral_constant<int, 0>{}, k1c);
+      cpx<T> u0;
+      if constexpr (PRE) u0 = lds_cpx(ibase + pfa_pre_slot<M>(0, kk, 0) * gi.estride, gi.imoff);
+      else u0 = in(std::integral_constant<int, 0>{}, k1c);
       if constexpr (gg == 0) dc = u0;
 #pragma unroll
       for (int i = 0; i < QP; ++i) A[i] = u0;
@@ -516,9 +527,16 @@ __device__ __forceinline__ void fft_pass_pfa(T* lds, const LineGeom& g, const Li
     // (4 H VGPRs of complex) to the top: 8 waves per SIMD cover the LDS latency
     sfor<H>([&](auto ri) {
       constexpr int r = decltype(ri)::value + 1;
-      const cpx<T> a = in(std::integral_constant<int, r>{}, k1c);
-      const cpx<T> b = in(std::integral_constant<int, M - r>{}, k1c);
-      const cpx<T> sr = cadd(a, b), dr = csub(a, b);
+      cpx<T> sr, dr;
+      if constexpr (PRE) {
+        sr = lds_cpx(ibase + pfa_pre_slot<M>(r, kk, 0) * gi.estride, gi.imoff);
+        dr = lds_cpx(ibase + pfa_pre_slot<M>(r, kk, 1) * gi.estride, gi.imoff);
+      } else {
+        const cpx<T> a = in(std::integral_constant<int, r>{}, k1c);
+        const cpx<T> b = in(std::integral_constant<int, M - r>{}, k1c);
+        sr = cadd(a, b);
+        dr = csub(a, b);
+      }
       if constexpr (gg == 0) dc = cadd(dc, sr);
       sfor<QP>([&](auto ii) {
         constexpr int q = gg * QP + decltype(ii)::value + 1;

@@ -166,6 +166,79 @@ __device__ __forceinline__ void fpass(T* lds, const cpx<T>* __restrict__ tw, int
   lds_sync();
 }
 
+// The radix-2 Stockham pass (NS = 1) of a length N = 2 M line ahead of fft_pass_pfa<PRE>:
+// one task per line and input pair r of the M-point pass -- the butterflies j = 2 r and
+// M - 2 r (r = 0: butterfly 0 alone) -- storing the pairs the prime pass sums over,
+//   k1 = 0: out[4r] +- out[2(M-2r)],  k1 = 1: out[4r+1] -+ out[2(M-2r)+1]
+// (out[2j] = x_j + x_{j+M}, out[2j+1] = x_j - x_{j+M}; the k1 = 1 partner enters the prime
+// pass negated, fft_pass_pfa) at elements pfa_pre_slot: the same adds, formed once per line
+// here instead of once per output group there, and H + 1 tasks per line instead of M.
+// Loads as fpass (MODE, kLmIn); stores line-minor for x passes (kLmOut required),
+// interleaved columns for y passes.
+template <typename T, class FG, int NT, bool XD, int MODE, int LM = 0>
+__device__ __forceinline__ void fpass2_pairs(T* lds, int tid) {
+  constexpr int N = XD ? FG::X : FG::Y;
+  constexpr int M = N / 2;
+  constexpr int H = (M - 1) / 2;
+  constexpr int NL = XD ? FG::Yp / 2 : FG::Xh;
+  constexpr int NP = H + 1;
+  constexpr int TOTAL = NL * NP;
+  constexpr int MAXB = (TOTAL + NT - 1) / NT;
+  constexpr bool IPERM = (LM & kLmIn) != 0, OPERM = (LM & kLmOut) != 0;
+  static_assert(N == 2 * M && (M & 1), "a 2 x odd line");
+  static_assert(!XD || OPERM, "x passes store line-minor");
+  constexpr int OESTR = XD ? 2 * NL : FG::RS;
+  asm volatile("" : "+v"(tid));
+  cpx<T> v[MAXB][4];
+  int ob[MAXB], rr[MAXB];
+#pragma unroll
+  for (int b = 0; b < MAXB; ++b) {
+    const int bf = tid + b * NT;
+    ob[b] = -1;
+    rr[b] = 0;
+    if (bf < TOTAL) {
+      int line, r;
+      if constexpr (XD && !IPERM) {   // lanes over a line's pairs (the HermPair x pass)
+        line = bf / NP;
+        r = bf - line * NP;
+      } else {                        // lanes over the lines
+        r = bf / NL;
+        line = bf - r * NL;
+      }
+      ob[b] = 2 * line;
+      rr[b] = r;
+      const int j = 2 * r;
+      v[b][0] = fload<T, FG, XD, MODE, IPERM>(lds, line, j);
+      v[b][1] = fload<T, FG, XD, MODE, IPERM>(lds, line, j + M);
+      if (r > 0) {
+        v[b][2] = fload<T, FG, XD, MODE, IPERM>(lds, line, M - j);
+        v[b][3] = fload<T, FG, XD, MODE, IPERM>(lds, line, N - j);
+      }
+    }
+  }
+  lds_sync();
+#pragma unroll
+  for (int b = 0; b < MAXB; ++b) {
+    if (ob[b] >= 0) {
+      T* base = lds + ob[b];
+      const cpx<T> e0 = cadd(v[b][0], v[b][1]), o0 = csub(v[b][0], v[b][1]);
+      const int r = rr[b];
+      if (r == 0) {
+        lds_cpx_store(base + pfa_pre_slot<M>(0, 0, 0) * OESTR, 1, e0);
+        lds_cpx_store(base + pfa_pre_slot<M>(0, 1, 0) * OESTR, 1, o0);
+      } else {
+        const cpx<T> e1 = cadd(v[b][2], v[b][3]), o1 = csub(v[b][2], v[b][3]);
+        T* p = base + pfa_pre_slot<M>(r, 0, 0) * OESTR;
+        lds_cpx_store(p, 1, cadd(e0, e1));
+        lds_cpx_store(p + OESTR, 1, csub(e0, e1));
+        lds_cpx_store(p + 2 * OESTR, 1, csub(o0, o1));
+        lds_cpx_store(p + 3 * OESTR, 1, cadd(o0, o1));
+      }
+    }
+  }
+  lds_sync();
+}
+
 // Forward 2D R2C (MATLAB fft2) of the real slice in LDS rows [y*RS, y*RS+X);
 // result: interleaved half spectrum, bin (x', y) at lds[y*RS + 2x'].
 // (A wave-local variant -- each 110-point line owned by 11 lanes of one wave,

@@ -101,13 +101,28 @@ struct SG {
 // the x passes read and write the line-minor layout (fpass LM): the forward one for the
 // split-to-half y pass, the inverse one, the last pass of the C2R, for the kernels' real
 // planes (SG<kRm74F>::px)
+// kPfaPre: the radix-2 passes store the prime pass's symmetric input pairs already formed
+// (fpass2_pairs, fft_pass_pfa<PRE>); 0 keeps the plain radix-2 pass (A/B builds)
+#ifndef CCSC_PFA_PRE
+#define CCSC_PFA_PRE 1
+#endif
+constexpr bool kPfaPre = CCSC_PFA_PRE != 0;
+#ifndef CCSC_PFA74_QP
+#define CCSC_PFA74_QP kPfaQP
+#endif
 template <typename T, int SIGN>
 __device__ __forceinline__ void pfa74(T* lds, bool xdir) {
   using FG = Grid74;
   constexpr LineGeom gy = {FG::Xh, 2, FG::RS, 1};
   constexpr LineGeom gxi = {FG::Yp / 2, 2, FG::Yp, 1};   // line-minor
-  if (xdir) fft_pass_pfa<T, kPfaM, SIGN, kPfaQP, kNT>(lds, gxi, gxi);
-  else fft_pass_pfa<T, kPfaM, SIGN, kPfaQP, kNT>(lds, gy);
+  if (xdir) fft_pass_pfa<T, kPfaM, SIGN, CCSC_PFA74_QP, kNT, kPfaPre>(lds, gxi, gxi);
+  else fft_pass_pfa<T, kPfaM, SIGN, CCSC_PFA74_QP, kNT, kPfaPre>(lds, gy, gy);
+}
+// the radix-2 pass of a 74-point direction ahead of pfa74
+template <typename T, bool XD, int SIGN, int MODE, int LM>
+__device__ __forceinline__ void rad2_74(T* lds, const cpx<T>* tw, int tid) {
+  if constexpr (kPfaPre) fpass2_pairs<T, Grid74, kNT, XD, MODE, LM>(lds, tid);
+  else fpass<T, Grid74, kNT, XD, 2, 1, SIGN, MODE, LM>(lds, tw, tid);
 }
 
 // slice_r2c / slice_c2r of instantiation RM (fft.hpp), the fixed passes on kRm74F
@@ -116,9 +131,9 @@ __device__ __forceinline__ void slice_r2c_rm(T* lds, const Grid2D& G, const cpx<
   if constexpr (RM == kRm74F) {
     lds_sync();
     const int tid = threadIdx.x;
-    fpass<T, Grid74, kNT, true, 2, 1, -1, kModePlain, kLmIn | kLmOut>(lds, tw, tid);
+    rad2_74<T, true, -1, kModePlain, kLmIn | kLmOut>(lds, tw, tid);
     pfa74<T, -1>(lds, true);
-    fpass<T, Grid74, kNT, false, 2, 1, -1, kModeSplitToHalf, kLmIn>(lds, tw, tid);
+    rad2_74<T, false, -1, kModeSplitToHalf, kLmIn>(lds, tw, tid);
     pfa74<T, -1>(lds, false);
   } else {
     slice_r2c<T, kMaxB, RM>(lds, G, tw);
@@ -129,9 +144,9 @@ __device__ __forceinline__ void slice_c2r_rm(T* lds, const Grid2D& G, const cpx<
   if constexpr (RM == kRm74F) {
     lds_sync();
     const int tid = threadIdx.x;
-    fpass<T, Grid74, kNT, false, 2, 1, +1, kModePlain>(lds, tw, tid);
+    rad2_74<T, false, +1, kModePlain, 0>(lds, tw, tid);
     pfa74<T, +1>(lds, false);
-    fpass<T, Grid74, kNT, true, 2, 1, +1, kModeHermPair, kLmOut>(lds, tw, tid);
+    rad2_74<T, true, +1, kModeHermPair, kLmOut>(lds, tw, tid);
     pfa74<T, +1>(lds, true);
   } else {
     slice_c2r<T, kMaxB, RM>(lds, G, tw);
