@@ -589,6 +589,127 @@ __device__ __forceinline__ void fft_pass_pfa(T* lds, const LineGeom& g, const Li
   lds_sync();
 }
 
+// fft_pass_pfa<PRE> with dense lanes, for NL = 32 .. 49 lines: the plain form runs one task
+// per (output group, k1, line) with lanes over the lines, 37 or 38 of a wave's 64.  Here wave
+// g < NG takes output group g of lines 0..31 for both k1 (lane = 32 k1 + line; k1 only moves
+// the input slot and the output index by M); the waves after them take lines 32..NL-1, one
+// task per (line, k1, conjugate output pair q), their roots read from the LDS table `roots`
+// (roots[m] = exp(2 pi i m / M), lane-varying m = r q mod M).  Same products, same order.
+template <typename T, int M, int SIGN, int QP, int NT, int NL>
+__device__ __forceinline__ void fft_pass_pfa_packed(T* lds, const LineGeom& g, const LineGeom& gi,
+                                                    const cpx<T>* roots) {
+  constexpr int H = (M - 1) / 2;
+  constexpr int NG = (H + QP - 1) / QP;
+  constexpr int N = 2 * M;
+  constexpr int NLO = NL - 32;                     // lines past the main waves
+  constexpr int NLEFT = NLO * 2 * H;               // their (line, k1, q) tasks
+  static_assert(NL >= 32 && NG * 64 + NLEFT <= NT, "dense prime pass: 32..49 lines");
+  int o = (int)threadIdx.x;
+  asm volatile("" : "+v"(o));
+  const int wave = __builtin_amdgcn_readfirstlane(o >> 6);
+  const int lane = o & 63;
+  const int ies = gi.estride, iim = gi.imoff, es = g.estride, im = g.imoff;
+  auto slot = [&](int r, int d) { return (2 + 4 * (r - 1) + d) * ies; };   // pfa_pre_slot, k1 = 0
+  cpx<T> A[QP], S[QP], dc = {(T)0, (T)0};
+#pragma unroll
+  for (int i = 0; i < QP; ++i) A[i] = S[i] = {(T)0, (T)0};
+  int kk = 0, line = 0, q = 0;
+  bool on = false;
+  if (wave < NG) {
+    kk = lane >> 5;
+    line = lane & 31;
+    on = true;
+    const T* ib = lds + line * gi.lstride;
+    const T* ip = ib + 2 * kk * ies;
+    sfor<NG>([&](auto gc) {
+      constexpr int gg = decltype(gc)::value;
+      if (wave == gg) {
+        const cpx<T> u0 = lds_cpx(ib + kk * ies, iim);
+        if constexpr (gg == 0) dc = u0;
+#pragma unroll
+        for (int i = 0; i < QP; ++i) A[i] = u0;
+        sfor<H>([&](auto ri) {
+          constexpr int r = decltype(ri)::value + 1;
+          const cpx<T> sr = lds_cpx(ip + slot(r, 0), iim);
+          const cpx<T> dr = lds_cpx(ip + slot(r, 1), iim);
+          if constexpr (gg == 0) dc = cadd(dc, sr);
+          sfor<QP>([&](auto ii) {
+            constexpr int qq = gg * QP + decltype(ii)::value + 1;
+            if constexpr (qq <= H) {
+              constexpr int m = (r * qq) % M;
+              constexpr T c = (T)TC<M, m>::c;
+              constexpr T sn = (T)TC<M, m>::s;
+              A[ii].x += sr.x * c;
+              A[ii].y += sr.y * c;
+              S[ii].x += dr.x * sn;
+              S[ii].y += dr.y * sn;
+            }
+          });
+          __builtin_amdgcn_sched_barrier(0);
+        });
+      }
+    });
+  } else {
+    const int t = (wave - NG) * 64 + lane;
+    if (t < NLEFT) {
+      const int qi = t / (2 * NLO), rem = t - qi * (2 * NLO);
+      kk = rem / NLO;
+      line = 32 + rem - kk * NLO;
+      q = qi + 1;
+      on = true;
+      const T* ib = lds + line * gi.lstride;
+      const T* ip = ib + 2 * kk * ies;
+      const cpx<T> u0 = lds_cpx(ib + kk * ies, iim);
+      dc = u0;
+      A[0] = u0;
+      int m = 0;
+      sfor<H>([&](auto ri) {
+        constexpr int r = decltype(ri)::value + 1;
+        const cpx<T> sr = lds_cpx(ip + slot(r, 0), iim);
+        const cpx<T> dr = lds_cpx(ip + slot(r, 1), iim);
+        dc = cadd(dc, sr);
+        m += q;
+        m = m >= M ? m - M : m;
+        const cpx<T> w = lds_cpx(reinterpret_cast<const T*>(roots + m), 1);
+        A[0].x += sr.x * w.x;
+        A[0].y += sr.y * w.x;
+        S[0].x += dr.x * w.y;
+        S[0].y += dr.y * w.y;
+        __builtin_amdgcn_sched_barrier(0);
+      });
+    }
+  }
+  lds_sync();
+  if (on) {
+    T* base = lds + line * g.lstride;
+    const int kd = kk * M * es;   // k1 = 1 moves every output index by M (mod N)
+    if (wave < NG) {
+      sfor<NG>([&](auto gc) {
+        constexpr int gg = decltype(gc)::value;
+        if (wave == gg) {
+          if constexpr (gg == 0) lds_cpx_store(base + kd, im, dc);
+          sfor<QP>([&](auto ii) {
+            constexpr int qq = gg * QP + decltype(ii)::value + 1;
+            if constexpr (qq <= H) {
+              const cpx<T> iS = {-(T)SIGN * S[ii].y, (T)SIGN * S[ii].x};
+              constexpr int kq0 = ((M + 1) * qq) % N, kr0 = ((M + 1) * (M - qq)) % N;
+              lds_cpx_store(base + kq0 * es + (kq0 < M ? kd : -kd), im, cadd(A[ii], iS));
+              lds_cpx_store(base + kr0 * es + (kr0 < M ? kd : -kd), im, csub(A[ii], iS));
+            }
+          });
+        }
+      });
+    } else {
+      if (q == 1) lds_cpx_store(base + kd, im, dc);
+      const cpx<T> iS = {-(T)SIGN * S[0].y, (T)SIGN * S[0].x};
+      const int kq = (M * kk + (M + 1) * q) % N, kr = (M * kk + (M + 1) * (M - q)) % N;
+      lds_cpx_store(base + kq * es, im, cadd(A[0], iS));
+      lds_cpx_store(base + kr * es, im, csub(A[0], iS));
+    }
+  }
+  lds_sync();
+}
+
 template <typename T, int M, int SIGN, int QP, int NT>
 __device__ __forceinline__ void fft_pass_pfa(T* lds, const LineGeom& g) {
   fft_pass_pfa<T, M, SIGN, QP, NT>(lds, g, g);

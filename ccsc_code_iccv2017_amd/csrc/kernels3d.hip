@@ -91,7 +91,7 @@ void k_plane_fwd(int mode, const T* __restrict__ a,
     }
     zero_pad_row(S.slice, G);
   }
-  slice_r2c_rm<T, RM>(S.slice, G, S.tw);
+  slice_r2c_rm<T, RM, true>(S.slice, G, S.tw);
   if (tc > 0) {   // t-minor tiles (k_tsolve3's order)
     const int ntile = (GXh + tc - 1) / tc;
     cpx<T>* out = dst + slice * ((int64_t)GY * ntile * Tn * tc);
@@ -190,7 +190,7 @@ void k_plane_inv(int mode, const cpx<T>* src,
     const cpx<T>* in = src + (slice * Tn + t) * GF;
     for (int f = threadIdx.x; f < GF; f += kNT) lds_cpx_store(S.slice + Q::bin(f, G), 1, in[f]);
   }
-  slice_c2r_rm<T, RM>(S.slice, G, S.tw);
+  slice_c2r_rm<T, RM, true>(S.slice, G, S.tw);
   const int P = GX * GY;
   const int64_t off = (slice * Tn + t) * P;
   const bool nrm = (mode == 3 && norms) || (mode == 2 && slice < nfirst);
@@ -235,7 +235,7 @@ void k_plane_inv(int mode, const cpx<T>* src,
   }
   if (mode == 3 && nxt) {   // the next iteration's forward plane transform (k_plane_fwd mode 3)
     zero_pad_row(S.slice, G);
-    slice_r2c_rm<T, RM>(S.slice, G, S.tw);
+    slice_r2c_rm<T, RM, true>(S.slice, G, S.tw);
     if (tc > 0) {
       const int ntile = (GXh + tc - 1) / tc;
       cpx<T>* out = nxt + slice * ((int64_t)GY * ntile * Tn * tc);

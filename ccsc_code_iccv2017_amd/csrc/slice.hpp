@@ -110,13 +110,50 @@ constexpr bool kPfaPre = CCSC_PFA_PRE != 0;
 #ifndef CCSC_PFA74_QP
 #define CCSC_PFA74_QP kPfaQP
 #endif
-template <typename T, int SIGN>
+// PK: the prime pass with dense lanes (fft_pass_pfa_packed; needs kPfaPre) -- the 3D plane
+// kernels (C4 0.1884 -> 0.1836 s per outer iteration); the 4D kernels keep the plain form
+// (C5 0.0157 -> 0.0159 with it, profiles/r05/pfa_pack_ab.txt).  CCSC_PFA_PACK=0 turns it off.
+#ifndef CCSC_PFA_PACK
+#define CCSC_PFA_PACK 1
+#endif
+constexpr bool kPfaPack = kPfaPre && CCSC_PFA_PACK != 0;
+// the 37 roots of the packed pass's lane-varying tasks, one LDS copy per workgroup
+template <typename T>
+__device__ __forceinline__ cpx<T>* pfa74_roots() {
+  __shared__ __attribute__((aligned(16))) cpx<T> roots[kPfaM];
+  return roots;
+}
+template <typename T, bool PK>
+__device__ __forceinline__ void pfa74_fill_roots(int tid) {
+  if constexpr (PK) {
+    static constexpr double tab[kPfaM][2] = {
+#define CCSC_R(m) {TC<kPfaM, m>::c, TC<kPfaM, m>::s}
+        CCSC_R(0),  CCSC_R(1),  CCSC_R(2),  CCSC_R(3),  CCSC_R(4),  CCSC_R(5),  CCSC_R(6),
+        CCSC_R(7),  CCSC_R(8),  CCSC_R(9),  CCSC_R(10), CCSC_R(11), CCSC_R(12), CCSC_R(13),
+        CCSC_R(14), CCSC_R(15), CCSC_R(16), CCSC_R(17), CCSC_R(18), CCSC_R(19), CCSC_R(20),
+        CCSC_R(21), CCSC_R(22), CCSC_R(23), CCSC_R(24), CCSC_R(25), CCSC_R(26), CCSC_R(27),
+        CCSC_R(28), CCSC_R(29), CCSC_R(30), CCSC_R(31), CCSC_R(32), CCSC_R(33), CCSC_R(34),
+        CCSC_R(35), CCSC_R(36)};
+#undef CCSC_R
+    if (tid < kPfaM) pfa74_roots<T>()[tid] = {(T)tab[tid][0], (T)tab[tid][1]};
+  }
+}
+template <typename T, int SIGN, bool PK>
 __device__ __forceinline__ void pfa74(T* lds, bool xdir) {
   using FG = Grid74;
   constexpr LineGeom gy = {FG::Xh, 2, FG::RS, 1};
   constexpr LineGeom gxi = {FG::Yp / 2, 2, FG::Yp, 1};   // line-minor
-  if (xdir) fft_pass_pfa<T, kPfaM, SIGN, CCSC_PFA74_QP, kNT, kPfaPre>(lds, gxi, gxi);
-  else fft_pass_pfa<T, kPfaM, SIGN, CCSC_PFA74_QP, kNT, kPfaPre>(lds, gy, gy);
+  if constexpr (PK) {
+    if (xdir)
+      fft_pass_pfa_packed<T, kPfaM, SIGN, CCSC_PFA74_QP, kNT, FG::Yp / 2>(lds, gxi, gxi,
+                                                                          pfa74_roots<T>());
+    else
+      fft_pass_pfa_packed<T, kPfaM, SIGN, CCSC_PFA74_QP, kNT, FG::Xh>(lds, gy, gy,
+                                                                      pfa74_roots<T>());
+  } else {
+    if (xdir) fft_pass_pfa<T, kPfaM, SIGN, CCSC_PFA74_QP, kNT, kPfaPre>(lds, gxi, gxi);
+    else fft_pass_pfa<T, kPfaM, SIGN, CCSC_PFA74_QP, kNT, kPfaPre>(lds, gy, gy);
+  }
 }
 // the radix-2 pass of a 74-point direction ahead of pfa74
 template <typename T, bool XD, int SIGN, int MODE, int LM>
@@ -126,28 +163,32 @@ __device__ __forceinline__ void rad2_74(T* lds, const cpx<T>* tw, int tid) {
 }
 
 // slice_r2c / slice_c2r of instantiation RM (fft.hpp), the fixed passes on kRm74F
-template <typename T, int RM>
+template <typename T, int RM, bool PACK = false>
 __device__ __forceinline__ void slice_r2c_rm(T* lds, const Grid2D& G, const cpx<T>* tw) {
+  constexpr bool PK = PACK && kPfaPack;
   if constexpr (RM == kRm74F) {
-    lds_sync();
     const int tid = threadIdx.x;
+    pfa74_fill_roots<T, PK>(tid);
+    lds_sync();
     rad2_74<T, true, -1, kModePlain, kLmIn | kLmOut>(lds, tw, tid);
-    pfa74<T, -1>(lds, true);
+    pfa74<T, -1, PK>(lds, true);
     rad2_74<T, false, -1, kModeSplitToHalf, kLmIn>(lds, tw, tid);
-    pfa74<T, -1>(lds, false);
+    pfa74<T, -1, PK>(lds, false);
   } else {
     slice_r2c<T, kMaxB, RM>(lds, G, tw);
   }
 }
-template <typename T, int RM>
+template <typename T, int RM, bool PACK = false>
 __device__ __forceinline__ void slice_c2r_rm(T* lds, const Grid2D& G, const cpx<T>* tw) {
+  constexpr bool PK = PACK && kPfaPack;
   if constexpr (RM == kRm74F) {
-    lds_sync();
     const int tid = threadIdx.x;
+    pfa74_fill_roots<T, PK>(tid);
+    lds_sync();
     rad2_74<T, false, +1, kModePlain, 0>(lds, tw, tid);
-    pfa74<T, +1>(lds, false);
+    pfa74<T, +1, PK>(lds, false);
     rad2_74<T, true, +1, kModeHermPair, kLmOut>(lds, tw, tid);
-    pfa74<T, +1>(lds, true);
+    pfa74<T, +1, PK>(lds, true);
   } else {
     slice_c2r<T, kMaxB, RM>(lds, G, tw);
   }
