@@ -713,7 +713,10 @@ struct Session2D {
       // cannot hold
       {
         std::string why2;
-        for (int tc : {2, 4, 1}) {
+        // (C4 itself runs TC = 1 on narrow workgroups when kernels3d.hip builds that form:
+        // two workgroups per CU, tsolve3_nt)
+        const bool narrow = tsolve3_nt(Tn, K, 1) != kNT;
+        for (int tc : narrow ? std::initializer_list<int>{1, 2, 4} : std::initializer_list<int>{2, 4, 1}) {
           Grid2D Gt2{};
           if (!tsolve3_ok(Tn, K, tc) || !make_gridt(Tn, K * tc, Gt2, why2)) continue;
           if (tsolve3_smem_bytes(Gt2, K, tc, sizeof(double)) > 160 * 1024) continue;

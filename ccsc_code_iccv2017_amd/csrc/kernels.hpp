@@ -183,6 +183,7 @@ hipError_t launch_plane_inv(int mode, const cpx<T>* src, T* dst, const T* yv, T*
 // t-minor tile order of tile width TC; ppw patches per workgroup (the filter-spectrum
 // columns of a block stay in L2 across them)
 bool tsolve3_ok(int Tn, int K, int TC);
+int tsolve3_nt(int Tn, int K, int TC);   // threads per k_tsolve3 workgroup
 size_t tsolve3_smem_bytes(const Grid2D& Gt2, int K, int TC, size_t tsize, bool dl = false);
 template <typename T>
 hipError_t launch_tsolve3(cpx<T>* C, const cpx<T>* Bhat, const cpx<T>* dhat, const T* sden,

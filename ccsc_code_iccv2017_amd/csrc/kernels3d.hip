@@ -118,13 +118,13 @@ __host__ inline bool tline42_ok(const Grid2D& Gt, int nl) {
          p.rad[0] == 7 && p.rad[1] == 3 && p.rad[2] == 2 && p.twoff[0] == 0 && p.twoff[1] == 6 &&
          p.twoff[2] == 20;
 }
-template <typename T, int NL, int SIGN>
+template <typename T, int NL, int SIGN, int NT = kNT>
 __device__ __forceinline__ void tfft42(T* lds, const cpx<T>* tw) {
   using FG = TLines42<NL>;
   const int tid = threadIdx.x;
-  fpass<T, FG, kNT, false, 7, 1, SIGN, kModePlain>(lds, tw, tid);
-  fpass<T, FG, kNT, false, 3, 7, SIGN, kModePlain>(lds, tw + 6, tid);
-  fpass<T, FG, kNT, false, 2, 21, SIGN, kModePlain>(lds, tw + 20, tid);
+  fpass<T, FG, NT, false, 7, 1, SIGN, kModePlain>(lds, tw, tid);
+  fpass<T, FG, NT, false, 3, 7, SIGN, kModePlain>(lds, tw + 6, tid);
+  fpass<T, FG, NT, false, 2, 21, SIGN, kModePlain>(lds, tw + 20, tid);
 }
 
 // ---- t-direction complex FFT (src may equal dst); one workgroup per (slice, y)
@@ -285,9 +285,10 @@ __global__ void k_zsolve3(cpx<T>* __restrict__ C, const cpx<T>* __restrict__ Bha
 // workgroup -- the solve of every patch reads them there instead of from L2 (two exposed
 // global round trips per patch otherwise) -- and each patch's B^ values are loaded before
 // its forward t-FFT, consumed after it.
-// FNL > 0: the t transforms on the compile-time 42-point plan over FNL = K TC lines (C4)
-template <typename T, int RM, int LD, int KMAX, bool DL, int FNL>
-__global__ __launch_bounds__(kNT) void k_tsolve3(cpx<T>* __restrict__ C,
+// FNL > 0: the t transforms on the compile-time 42-point plan over FNL = K TC lines (C4),
+// TC = TCF; NT threads per workgroup (NT, or 512 for C4's TC = 1 form: two workgroups per CU)
+template <typename T, int RM, int LD, int KMAX, bool DL, int FNL, int NT = kNT, int TCF = 2>
+__global__ __launch_bounds__(NT) void k_tsolve3(cpx<T>* __restrict__ C,
                                                  const cpx<T>* __restrict__ Bhat,
                                                  const cpx<T>* __restrict__ dhat,
                                                  const T* __restrict__ sden, int K, int Yn,
@@ -297,10 +298,10 @@ __global__ __launch_bounds__(kNT) void k_tsolve3(cpx<T>* __restrict__ C,
   extern __shared__ __attribute__((aligned(16))) char smem[];
   cpx<T>* s_tw = reinterpret_cast<cpx<T>*>(smem);
   T* lds = reinterpret_cast<T*>(s_tw + Gt.ntw);
-  for (int i = threadIdx.x; i < Gt.ntw; i += kNT) s_tw[i] = twg[i];
-  if constexpr (FNL > 0) {   // C4: TC = 2, T = 42, K = FNL / 2 -- the index math compile-time
-    TC = 2;
-    K = FNL / 2;
+  for (int i = threadIdx.x; i < Gt.ntw; i += NT) s_tw[i] = twg[i];
+  if constexpr (FNL > 0) {   // C4: TC = TCF, T = 42, K = FNL / TCF -- the index math compile-time
+    TC = TCF;
+    K = FNL / TCF;
   }
   const int tile = blockIdx.x % xtiles;
   const int64_t rest = blockIdx.x / xtiles;
@@ -315,31 +316,31 @@ __global__ __launch_bounds__(kNT) void k_tsolve3(cpx<T>* __restrict__ C,
   const int64_t F3t = (int64_t)Yn * xtiles * TT;
   const int64_t blk = (int64_t)(y * xtiles + tile) * TT;
   const LineGeom g = {NL, 2, 2 * NL, 1};
-  // load slot j of this thread: i = threadIdx.x + j * kNT < K * TT -> global offset
+  // load slot j of this thread: i = threadIdx.x + j * NT < K * TT -> global offset
   // (K F3t < 2^31: checked by the host) and LDS offset; recomputed where used from a
   // laundered thread index, so the patch loop does not keep them (and every FFT pass's
   // per-thread index math) live in registers across its iterations
   auto slot = [&](int tid, int j, int& src, int& dst) {
-    const int i = tid + j * kNT;
+    const int i = tid + j * NT;
     const int k = i / TT, rem = i - k * TT;
     const int t = rem / TC, c = rem - t * TC;
     src = (i < KT && c < nc) ? k * (int)F3t + rem : -1;
     dst = i < KT ? 2 * (t * NL + k * TC + c) : -1;
   };
   cpx<T> pre[LD];
-  // solve-phase geometry: G = kNT / (T TC) threads per bin split the k range
+  // solve-phase geometry: G = NT / (T TC) threads per bin split the k range
   const int nb = TT;
-  const int G = max(1, kNT / nb);
+  const int G = max(1, NT / nb);
   const int kg = (K + G - 1) / G;
   cpx<T>* part = reinterpret_cast<cpx<T>*>(lds + 2 * (size_t)Tn * NL);   // [G][nb]
   cpx<T>* sD = part + (size_t)G * nb;                                    // DL: [K][nb]
   T* sS = reinterpret_cast<T*>(sD + (size_t)K * nb);                     // DL: [nb]
   if constexpr (DL) {   // visible after the patch loop's first barrier
-    for (int i = threadIdx.x; i < K * nb; i += kNT) {
+    for (int i = threadIdx.x; i < K * nb; i += NT) {
       const int k = i / nb, bb = i - k * nb;
       sD[i] = dhat[(int64_t)k * F3t + blk + bb];
     }
-    for (int i = threadIdx.x; i < nb; i += kNT) sS[i] = sden[blk + i];
+    for (int i = threadIdx.x; i < nb; i += NT) sS[i] = sden[blk + i];
   }
   {
     const cpx<T>* Cp = C + p0 * K * F3t + blk;
@@ -375,8 +376,8 @@ __global__ __launch_bounds__(kNT) void k_tsolve3(cpx<T>* __restrict__ C,
       const int b = tid % nb, grp = tid / nb;
       if (grp < G && b - (b / TC) * TC < nc) bh = Bhat[p * F3t + blk + b];
     }
-    if constexpr (FNL > 0) tfft42<T, FNL, -1>(lds, s_tw);
-    else fft_dir<T, kMaxB, -1, kMaxPass, kNT, 1, 1, RM>(lds, kModePlain, g, g, Gt, Gt.py, s_tw);
+    if constexpr (FNL > 0) tfft42<T, FNL, -1, NT>(lds, s_tw);
+    else fft_dir<T, kMaxB, -1, kMaxPass, NT, 1, 1, RM>(lds, kModePlain, g, g, Gt, Gt.py, s_tw);
     // per bin (t, c): w = (B - sum_k d_k C_k) sden, C_k <- C_k / P3 + conj(d_k) w; the
     // d_k of a thread's k range stay in registers between the two sweeps, partial sums
     // meet in LDS past the spectra
@@ -422,8 +423,8 @@ __global__ __launch_bounds__(kNT) void k_tsolve3(cpx<T>* __restrict__ C,
       }
     }
     lds_sync();
-    if constexpr (FNL > 0) tfft42<T, FNL, +1>(lds, s_tw);
-    else fft_dir<T, kMaxB, +1, kMaxPass, kNT, 1, 1, RM>(lds, kModePlain, g, g, Gt, Gt.py, s_tw);
+    if constexpr (FNL > 0) tfft42<T, FNL, +1, NT>(lds, s_tw);
+    else fft_dir<T, kMaxB, +1, kMaxPass, NT, 1, 1, RM>(lds, kModePlain, g, g, Gt, Gt.py, s_tw);
     tid = (int)threadIdx.x;
     asm volatile("" : "+v"(tid));
 #pragma unroll
@@ -565,22 +566,34 @@ hipError_t launch_tfft(const cpx<T>* src, cpx<T>* dst, int64_t nslices, int Yn, 
   return hipGetLastError();
 }
 
+// C4's narrow form: TC = 1 on 512-thread workgroups (74 KB of LDS with the filter block
+// staged, two workgroups per CU: one's barriers and exposed loads overlap the other's work)
+#ifndef CCSC_TSOLVE_NARROW
+#define CCSC_TSOLVE_NARROW 0
+#endif
+constexpr int kTsNarrowNT = 512;
+int tsolve3_nt(int Tn, int K, int TC) {
+  return (CCSC_TSOLVE_NARROW != 0 && Tn == 42 && K == 49 && TC == 1) ? kTsNarrowNT : kNT;
+}
 // per-thread k range of the solve phase (<= 16 k values) and block load slots (<= 8)
 static int tsolve3_kg(int Tn, int K, int TC) {
-  const int G = std::max(1, kNT / (Tn * TC));
+  const int G = std::max(1, tsolve3_nt(Tn, K, TC) / (Tn * TC));
   return (K + G - 1) / G;
 }
-static int tsolve3_ld(int Tn, int K, int TC) { return (K * Tn * TC + kNT - 1) / kNT; }
+static int tsolve3_ld(int Tn, int K, int TC) {
+  const int nt = tsolve3_nt(Tn, K, TC);
+  return (K * Tn * TC + nt - 1) / nt;
+}
 
 bool tsolve3_ok(int Tn, int K, int TC) {
   const int nb = Tn * TC;
-  if (nb > kNT) return false;
+  if (nb > tsolve3_nt(Tn, K, TC)) return false;
   return tsolve3_kg(Tn, K, TC) <= 16 && tsolve3_ld(Tn, K, TC) <= 8;
 }
 
 size_t tsolve3_smem_bytes(const Grid2D& Gt2, int K, int TC, size_t tsize, bool dl) {
   const int nb = Gt2.Y * TC;
-  const int G = std::max(1, kNT / nb);
+  const int G = std::max(1, tsolve3_nt(Gt2.Y, K, TC) / nb);
   return (size_t)Gt2.ntw * 2 * tsize + (size_t)Gt2.Y * K * TC * 2 * tsize +
          (size_t)G * nb * 2 * tsize +                        // + the solve's partial sums
          (dl ? (size_t)K * nb * 2 * tsize + (size_t)nb * tsize : 0);   // + dhat, sden (DL)
@@ -604,13 +617,17 @@ hipError_t launch_tsolve3(cpx<T>* C, const cpx<T>* Bhat, const cpx<T>* dhat, con
   const dim3 grid((unsigned)(pgroups * Yn * xtiles));
   const bool dl = tsolve3_dl(Gt2, K, TC, sizeof(T));
   const size_t smem = tsolve3_smem_bytes(Gt2, K, TC, sizeof(T), dl);
+  const int nt = tsolve3_nt(Gt2.Y, K, TC);
   auto go = [&](auto kern) {
-    hipLaunchKernelGGL(kern, grid, dim3(kNT), smem, stream, C, Bhat, dhat, sden, K, Yn, Xh, TC,
+    hipLaunchKernelGGL(kern, grid, dim3(nt), smem, stream, C, Bhat, dhat, sden, K, Yn, Xh, TC,
                        xtiles, invP3, tw, Gt2, npatch, ppw);
   };
   const bool r42 = rm_fits(kRm42, Gt2.py, Gt2.Xh);
   const bool small = tsolve3_ld(Gt2.Y, K, TC) <= 5 && tsolve3_kg(Gt2.Y, K, TC) <= 8;
-  if (r42 && small && dl && TC == 2 && tline42_ok(Gt2, 98)) go(k_tsolve3<T, kRm42, 5, 8, true, 98>);   // C4
+  if (nt != kNT) {   // C4's narrow form, nothing else
+    if (!(r42 && small && dl && TC == 1 && tline42_ok(Gt2, 49))) return hipErrorInvalidValue;
+    go(k_tsolve3<T, kRm42, 5, 8, true, 49, kTsNarrowNT, 1>);
+  } else if (r42 && small && dl && TC == 2 && tline42_ok(Gt2, 98)) go(k_tsolve3<T, kRm42, 5, 8, true, 98>);   // C4
   else if (r42 && small && dl) go(k_tsolve3<T, kRm42, 5, 8, true, 0>);
   else if (r42 && small) go(k_tsolve3<T, kRm42, 5, 8, false, 0>);
   else if (r42) go(k_tsolve3<T, kRm42, 8, 16, false, 0>);
