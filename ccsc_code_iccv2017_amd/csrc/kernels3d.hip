@@ -567,7 +567,8 @@ hipError_t launch_tfft(const cpx<T>* src, cpx<T>* dst, int64_t nslices, int Yn, 
 }
 
 // C4's narrow form: TC = 1 on 512-thread workgroups (74 KB of LDS with the filter block
-// staged, two workgroups per CU: one's barriers and exposed loads overlap the other's work)
+// staged, two workgroups per CU).  Measured slower than TC = 2 on 1024 threads (C4 0.1843 ->
+// 0.1954 s per outer iteration, profiles/r05/tsolve_narrow_ab.txt): off unless built with 1.
 #ifndef CCSC_TSOLVE_NARROW
 #define CCSC_TSOLVE_NARROW 0
 #endif
