@@ -13,6 +13,12 @@
 // t-solve reads and writes T * TC contiguous values per filter instead of TC-complex
 // segments at the plane stride, and the filter spectrum, B^ and sden it reads are
 // kept in the same order (k_to_ttiles).
+// the plane kernels' dense-lane 37-point pass (slice.hpp PK) with two output pairs per task:
+// 9 main waves + 3-4, 0-4 spilled VGPRs instead of 16-36 at three; C4 0.1845 -> 0.1823 s per
+// outer iteration, same box (profiles/r05/pfa_pack_q2_ab.txt)
+#ifndef CCSC_PFA74_QP
+#define CCSC_PFA74_QP 2
+#endif
 #include "slice.hpp"
 
 namespace ccsc {
