@@ -320,15 +320,22 @@ static void check_supported(const ccsc_problem& p, Geom* Gout) {
   Geom g;
   std::string why;
   const int X = (int)(p.sb[0] + 2 * r), Y = (int)(p.sb[1] + 2 * r);
-  if (!make_grid2d(X, Y, g.G, why)) {
-    // the 2D and 4D consensus learners on any grid the reference accepts (dP:16,23-24):
-    // slices past one CU's LDS take the global line passes (the 3D / 2-3D learners do not)
-    const bool two_d = p.variant == CCSC_DPAR || p.variant == CCSC_DZPAR || p.variant == CCSC_L4D;
+  const bool is3 = p.variant == CCSC_L3D;
+  const int Tn = is3 ? (int)(p.sb[2] + 2 * r) : 1;
+  bool fits = make_grid2d(X, Y, g.G, why);
+  // 3D: the plane kernels also need a t-tile plan (k_tfft / k_tsolve3 hold whole t-columns)
+  if (fits && is3 && !make_gridt(Tn, g.G.Xh, g.Gt, why)) fits = false;
+  if (!fits) {
+    // the 2D, 4D and 3D consensus learners on any grid the reference accepts (dP:16,23-24;
+    // L3:16,23-26): slices past one CU's LDS (or 3D t-columns past the t-tile kernels) take
+    // the global line passes (the 2-3D learner does not)
+    const bool gp_ok = p.variant == CCSC_DPAR || p.variant == CCSC_DZPAR ||
+                       p.variant == CCSC_L4D || is3;
     RowGeom rg{};
-    ColGeom cy{};
-    std::vector<cpx<double>> t1, t2;
-    if (!two_d) throw Err(CCSC_E_UNSUPPORTED, why);
-    if (!gfft_plan(X, Y, rg, cy, t1, t2))
+    ColGeom cy{}, ct{};
+    std::vector<cpx<double>> t1, t2, t3;
+    if (!gp_ok) throw Err(CCSC_E_UNSUPPORTED, why);
+    if (is3 ? !gfft_plan3(X, Y, Tn, rg, cy, ct, t1, t2, t3) : !gfft_plan(X, Y, rg, cy, t1, t2))
       throw Err(CCSC_E_UNSUPPORTED, why + "; no global line plan either");
     g.gp = true;
     g.G = Grid2D{};
@@ -338,12 +345,13 @@ static void check_supported(const ccsc_problem& p, Geom* Gout) {
     g.G.Yp = Y + (Y & 1);
     g.G.F = g.G.Xh * Y;
     g.G.ntw = 1;   // (the slice twiddle table is unused)
+    g.Gt = Grid2D{};
     if ((int64_t)g.G.F * 16 > INT32_MAX / 2) throw Err(CCSC_E_UNSUPPORTED, "2D half spectrum too large");
   }
-  if (p.variant == CCSC_L3D) {
-    g.Tn = (int)(p.sb[2] + 2 * r);
-    if (!make_gridt(g.Tn, g.G.Xh, g.Gt, why)) throw Err(CCSC_E_UNSUPPORTED, why);
-    if (g.F() > INT32_MAX / 2) throw Err(CCSC_E_UNSUPPORTED, "3D half spectrum too large");
+  if (is3) {
+    g.Tn = Tn;
+    if (g.F() > INT32_MAX / 2 || g.P() > INT32_MAX / 2)
+      throw Err(CCSC_E_UNSUPPORTED, "3D half spectrum too large");
   }
   if (Gout) *Gout = g;
 }
@@ -418,7 +426,7 @@ static Plan2D plan2d(const ccsc_problem& p, const Geom& g, int rank, int nranks)
   // 4D: view correlations E; 3D: spectra of the z-step's plane/t transforms, in the
   // t-minor tile order when k_tsolve3 runs (padded to whole tiles: sized for TC = 4),
   // with B^, the filter spectrum and sden in that order (misc)
-  const size_t F3t = is3 ? (size_t)std::max<int64_t>(ttile_bins(g.Tn, G.Y, G.Xh, 4),
+  const size_t F3t = is3 && !gp ? (size_t)std::max<int64_t>(ttile_bins(g.Tn, G.Y, G.Xh, 4),
                                                      ttile_bins(g.Tn, G.Y, G.Xh, 2))
                          : 0;
   m.E = is4 || gp ? m.np * K * F * 16 : is3 ? m.np * K * std::max(F, F3t) * 16 : 0;
@@ -552,8 +560,8 @@ struct Session2D {
   // twiddles, and the real scratch the elementwise stages (gslice.hip) read and write
   bool gp = false;
   RowGeom grg{};
-  ColGeom gcy{};
-  DevBuf gtwr, gtwc, gR, Cg;
+  ColGeom gcy{}, gct{};   // gct: the 3D learner's t-lines
+  DevBuf gtwr, gtwc, gtwt, gR, Cg;
   int tsolve_tc = 0;       // 3D: x' columns per k_tsolve3 workgroup (0: three-kernel z-solve)
   Grid2D gt2{};            //     its t plan (K * tsolve_tc lines) and twiddles
   DevBuf twt2;
@@ -701,7 +709,7 @@ struct Session2D {
     auto tws = make_twiddles(G);
     tw.alloc(tws.size() * sizeof(cpx<double>));
     HIPCHK(hipMemcpy(tw.p, tws.data(), tw.bytes, hipMemcpyHostToDevice));
-    if (is3) {
+    if (is3 && !gp) {
       auto twts = make_twiddles(g.Gt);
       twt.alloc(twts.size() * sizeof(cpx<double>));
       HIPCHK(hipMemcpy(twt.p, twts.data(), twt.bytes, hipMemcpyHostToDevice));
@@ -730,12 +738,18 @@ struct Session2D {
       }
     }
     if (gp) {
-      std::vector<cpx<double>> t1, t2;
-      if (!gfft_plan(G.X, G.Y, grg, gcy, t1, t2)) throw Err(CCSC_E_UNSUPPORTED, "no global line plan");
+      std::vector<cpx<double>> t1, t2, t3;
+      if (is3 ? !gfft_plan3(G.X, G.Y, Tn, grg, gcy, gct, t1, t2, t3)
+              : !gfft_plan(G.X, G.Y, grg, gcy, t1, t2))
+        throw Err(CCSC_E_UNSUPPORTED, "no global line plan");
       gtwr.alloc(t1.size() * sizeof(cpx<double>));
       gtwc.alloc(t2.size() * sizeof(cpx<double>));
       HIPCHK(hipMemcpy(gtwr.p, t1.data(), gtwr.bytes, hipMemcpyHostToDevice));
       HIPCHK(hipMemcpy(gtwc.p, t2.data(), gtwc.bytes, hipMemcpyHostToDevice));
+      if (is3) {
+        gtwt.alloc(std::max<size_t>(t3.size(), 1) * sizeof(cpx<double>));
+        HIPCHK(hipMemcpy(gtwt.p, t3.data(), t3.size() * sizeof(cpx<double>), hipMemcpyHostToDevice));
+      }
       gR.alloc(m.gr);
       oacc.alloc((size_t)NV * F * 16);
       odz.alloc((size_t)NV * P * 8);
@@ -894,16 +908,20 @@ struct Session2D {
   // ---- transforms ------------------------------------------------------------
   // global-pass 2D slices: real [count][Y][X] -> half spectra [count][Y][Xh], and back
   // (unnormalised; src is overwritten by the inverse column pass)
+  // (3D: slices of Tn planes, [count][t][y][x] -> [count][t][y][x']; y-lines per plane,
+  // then t-lines over the Y rows of each slice)
   void g_r2c(const double* src, cpx<double>* dst, int64_t count) {
     RowArgs<double> a{};
     a.S = dst;
     a.src = src;
     a.per_img = 1;
     HIPCHK(launch_rows<double>(kRowFwd, a, count, grg, gtwr.as<cpx<double>>(), st));
-    HIPCHK(launch_cols<double>(dst, -1, count, gcy, gtwc.as<cpx<double>>(), st));
+    HIPCHK(launch_cols<double>(dst, -1, count * Tn, gcy, gtwc.as<cpx<double>>(), st));
+    if (Tn > 1) HIPCHK(launch_cols<double>(dst, -1, count * G.Y, gct, gtwt.as<cpx<double>>(), st));
   }
   void g_c2r(cpx<double>* src, double* dst, int64_t count) {
-    HIPCHK(launch_cols<double>(src, +1, count, gcy, gtwc.as<cpx<double>>(), st));
+    if (Tn > 1) HIPCHK(launch_cols<double>(src, +1, count * G.Y, gct, gtwt.as<cpx<double>>(), st));
+    HIPCHK(launch_cols<double>(src, +1, count * Tn, gcy, gtwc.as<cpx<double>>(), st));
     RowArgs<double> a{};
     a.S = src;
     a.Z = dst;
@@ -916,12 +934,13 @@ struct Session2D {
                  int64_t count) {
     const auto* twc = tw.as<cpx<double>>();
     if (gp) {
-      if (sx == G.X && sy == G.Y && o == 0) {
+      if (sx == G.X && sy == G.Y && stt == Tn && o == 0) {
         g_r2c(src, dst, count);
         return;
       }
       HIPCHK(launch_gp_prolog<double>(0, src, nullptr, nullptr, sx, sy, o, 0.0, 1, r,
-                                      gR.as<double>(), G.X, G.Y, count, st));
+                                      gR.as<double>(), G.X, G.Y, count, st, Tn, stt,
+                                      Tn > 1 ? o : 0));
       g_r2c(gR.as<double>(), dst, count);
       return;
     }
@@ -939,7 +958,7 @@ struct Session2D {
     const auto* twc = tw.as<cpx<double>>();
     if (gp) {
       HIPCHK(launch_gp_prolog<double>(2, D.as<double>(), yD.as<double>(), Usup.as<double>(), 0, 0,
-                                      0, 0.0, KG, r, gR.as<double>(), G.X, G.Y, nbl * KG, st));
+                                      0, 0.0, KG, r, gR.as<double>(), G.X, G.Y, nbl * KG, st, Tn));
       g_r2c(gR.as<double>(), Ch.as<cpx<double>>(), nbl * KG);
       return;
     }
@@ -961,7 +980,7 @@ struct Session2D {
       g_c2r(Ch.as<cpx<double>>(), gR.as<double>(), nbl * KG);
       HIPCHK(launch_gp_epilog<double>(2, gR.as<double>(), D.as<double>(), yD.as<double>(),
                                       supp.as<double>(), dnorm.as<double>(), owner0 ? KG : 0,
-                                      1.0 / (double)P, r, G.X, G.Y, nbl * KG, nullptr, 0.0, 0, st));
+                                      1.0 / (double)P, r, G.X, G.Y, nbl * KG, nullptr, 0.0, 0, st, Tn));
       return;
     }
     if (!is3) {
@@ -1020,7 +1039,7 @@ struct Session2D {
       HIPCHK(launch_zstep_diag<double>(z.as<double>(), yz.as<double>(), E.as<cpx<double>>(),
                                        sden.as<double>(), np * K, twc, G, theta, p.rho_z,
                                        znorm.as<double>(), tol_on, write_z || tol_on, st));
-    } else if (is3) {
+    } else if (is3 && !gp) {
       cpx<double>* C = E.as<cpx<double>>();
       const auto* twtc = twt.as<cpx<double>>();
       // the state a = z + y lives in `yz` (modes 3, kernels3d.hip)
@@ -1049,7 +1068,7 @@ struct Session2D {
       // (4D: the diagonal solve (E + rho c) sden against the view correlations, L4:327-347)
       cpx<double>* C = is4 ? Cg.as<cpx<double>>() : E.as<cpx<double>>();
       HIPCHK(launch_gp_prolog<double>(3, nullptr, yz.as<double>(), nullptr, 0, 0, 0, theta, 1, r,
-                                      gR.as<double>(), G.X, G.Y, np * K, st));
+                                      gR.as<double>(), G.X, G.Y, np * K, st, Tn));
       g_r2c(gR.as<double>(), C, np * K);
       if (is4)
         HIPCHK(launch_gp_zdiag<double>(C, E.as<cpx<double>>(), sden.as<double>(), p.rho_z, (int)F,
@@ -1060,7 +1079,7 @@ struct Session2D {
       g_c2r(C, gR.as<double>(), np * K);
       HIPCHK(launch_gp_epilog<double>(3, gR.as<double>(), z.as<double>(), nullptr, nullptr,
                                       tol_on ? znorm.as<double>() : nullptr, 0, 1.0, r, G.X, G.Y,
-                                      np * K, yz.as<double>(), theta, write_z || tol_on, st));
+                                      np * K, yz.as<double>(), theta, write_z || tol_on, st, Tn));
     } else if (zl_on) {
       // register-line z-step (zline.hip): mode 0 reads (z, y) and leaves a in state order.
       // tol > 0: a launch whose starting w was solved with the current filters measures
@@ -1240,9 +1259,12 @@ struct Session2D {
       HIPCHK(launch_corr_sum<double>(C, dsp, oacc.as<cpx<double>>(), F, K, st));
       g_c2r(oacc.as<cpx<double>>(), gR.as<double>(), 1);
       HIPCHK(launch_gp_epilog<double>(0, gR.as<double>(), dzq, nullptr, nullptr, nullptr, 0,
-                                      1.0 / (double)P, r, G.X, G.Y, 1, nullptr, 0.0, 0, st));
-      HIPCHK(launch_crop_sq<double>(dzq, bdev.as<double>() + (size_t)q * sbx * sby, sbx, sby, 1, r,
-                                    0, G.X, G.Y, zq, (int64_t)K * P, pair.as<double>(), st));
+                                      1.0 / (double)P, r, G.X, G.Y, 1, nullptr, 0.0, 0, st, Tn));
+      // (3D: the crop of L3:351 in t as well)
+      const int sbt = Tn > 1 ? (int)p.sb[2] : 1;
+      HIPCHK(launch_crop_sq<double>(dzq, bdev.as<double>() + (size_t)q * sbx * sby * sbt, sbx, sby,
+                                    sbt, r, Tn > 1 ? r : 0, G.X, G.Y, zq, (int64_t)K * P,
+                                    pair.as<double>(), st));
     }
   }
 
@@ -1379,7 +1401,8 @@ struct Session2D {
       double dd = std::numeric_limits<double>::quiet_NaN();
       if (tol_on) {
         if (owner0)
-          HIPCHK(launch_sum_pairs<double>(dnorm.as<double>(), KG * Tn, pair.as<double>(), st));
+          // (the plane kernels leave one pair per (slice, t); the global-pass epilogue per slice)
+          HIPCHK(launch_sum_pairs<double>(dnorm.as<double>(), gp ? KG : KG * Tn, pair.as<double>(), st));
         else HIPCHK(hipMemsetAsync(pair.p, 0, 2 * sizeof(double), st));
         allreduce(pair.as<double>(), 2);
         double h2[2];
@@ -1470,7 +1493,7 @@ struct Session2D {
       } else if (zt_done.form) {
         zd = z_test(iz, fpart(), np);
       } else if (tol_on && !zl_tol) {
-        zd = z_test(iz, znorm.as<double>(), np * K * Tn);
+        zd = z_test(iz, znorm.as<double>(), gp ? np * K : np * K * Tn);
       }
       if (want_oz) {
         zsplit_join();

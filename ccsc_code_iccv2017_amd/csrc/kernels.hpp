@@ -212,11 +212,11 @@ hipError_t launch_gp_crop(const T* R, const T* b, T* DZ, int sbx, int sby, int r
 template <typename T>
 hipError_t launch_gp_prolog(int mode, const T* a, T* b, const T* usup, int sx, int sy, int o,
                             T theta, int KG, int r, T* R, int X, int Y, int64_t count,
-                            hipStream_t st);
+                            hipStream_t st, int Tn = 1, int sst = 1, int ot = 0);
 template <typename T>
 hipError_t launch_gp_epilog(int mode, const T* R, T* dst, const T* yv, T* supp, T* norms,
                             int64_t nfirst, T scale, int r, int X, int Y, int64_t count,
-                            T* state, T theta, int wz, hipStream_t st);
+                            T* state, T theta, int wz, hipStream_t st, int Tn = 1);
 
 // ---- hs23.hip: the 2-3D hyperspectral learner (L23) ----------------------------
 // Spectra slice-major [slice][F]: dhat [K][W], zhat [n][K], Xi1 / Yv [n][W]; h [F][W][K].

@@ -115,6 +115,10 @@ hipError_t launch_cols(cpx<T>* S, int sign, int64_t nouter, const ColGeom& cg, c
 // (engine.cpp); false if a length has no line plan.
 bool gfft_plan(int X, int Y, RowGeom& rg, ColGeom& cy, std::vector<cpx<double>>& tw_rows,
                std::vector<cpx<double>>& tw_cy);
+// X x Y x T grids: + the t-line pass (ct) over the Y rows of each slice
+bool gfft_plan3(int X, int Y, int Tn, RowGeom& rg, ColGeom& cy, ColGeom& ct,
+                std::vector<cpx<double>>& tw_rows, std::vector<cpx<double>>& tw_cy,
+                std::vector<cpx<double>>& tw_ct);
 
 // Sherman-Morrison z-solve of SI / SP per (image, bin), in place:
 //   xi2 [n][K][F] -> zhat * invP, xi1 [n][F] -> sum_k dhat_k zhat_k (the next v1);

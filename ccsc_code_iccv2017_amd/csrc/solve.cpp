@@ -166,6 +166,32 @@ bool gfft_plan(int X, int Y, RowGeom& rg, ColGeom& cy, std::vector<cpx<double>>&
   return true;
 }
 
+// 3D grids X x Y x T (the 3D learner's slices past one CU's LDS or past the t-tile
+// kernels): rows over the Y T rows of a slice, y-lines per plane, t-lines over the Y rows
+// of a slice (the video solver's passes, resolve_solve)
+bool gfft_plan3(int X, int Y, int Tn, RowGeom& rg, ColGeom& cy, ColGeom& ct,
+                std::vector<cpx<double>>& tw_rows, std::vector<cpx<double>>& tw_cy,
+                std::vector<cpx<double>>& tw_ct) {
+  if (!plan_rows(X, Y * Tn, rg) || !plan_cols(Y, X / 2 + 1, cy) || !plan_cols(Tn, X / 2 + 1, ct))
+    return false;
+  const int Xh = X / 2 + 1;
+  cy.es = Xh;
+  cy.ninner = 1;
+  cy.sin = 0;
+  cy.sout = (int64_t)Xh * Y;
+  ct.es = (int64_t)Xh * Y;
+  ct.ninner = Y;
+  ct.sin = Xh;
+  ct.sout = (int64_t)Xh * Y * Tn;
+  tw_rows.clear();
+  tw_cy.clear();
+  tw_ct.clear();
+  add_twiddles(rg.G.px, tw_rows);
+  add_twiddles(cy.p, tw_cy);
+  add_twiddles(ct.p, tw_ct);
+  return true;
+}
+
 // ---------------------------------------------------------------------------
 // problem resolution
 // ---------------------------------------------------------------------------

@@ -379,6 +379,40 @@ def test_learn_3d_production_path_matches_oracle(gpu_ctx, sb, psf, K, n):
     assert _rel(DZ_e, DZ_o) < 1e-7
 
 
+@pytest.mark.parametrize("sb,psf,K,n,tol,verbose", [
+    ((120, 120, 32), 11, 2, 1, 0.0, "all"),    # 130^2 planes: past one CU's LDS
+    ((64, 64, 242), 11, 2, 1, 0.0, "none"),    # T = 252 = 4 * 63: past the t-tile kernels
+    ((150, 150, 4), 3, 2, 4, 5e-2, "all"),     # 152^2 x 6, two blocks, tol breaks (n_z 10, 4)
+])
+def test_learn_3d_grids_past_lds_match_oracle(gpu_ctx, sb, psf, K, n, tol, verbose):
+    """3D clips the LDS plane / t-tile kernels cannot hold (VERDICT r05 missing item 1: the
+    reference crops any clip, L3:16,23-26, learn_kernels_3D.m:31-44) run on the global line
+    passes (x rows, y lines per plane, t lines; gslice.hip's 3D prologue / epilogue): d, z and
+    DZ at 1e-7, the objective trace at 1e-9, the tol path's inner-iteration counts exact."""
+    from ccsc_code_iccv2017_amd import learners as E
+    rng = np.random.default_rng(29)
+    r = psf // 2
+    g = tuple(s + 2 * r for s in sb)
+    b = rng.standard_normal(sb + (n,))
+    init = {"d": rng.standard_normal((psf, psf, psf, K)), "z": rng.standard_normal(g + (K, n))}
+    ks = [psf, psf, psf, K]
+    trace = verbose != "none"
+    d_o, z_o, DZ_o, obj_o, it_o, tr_o = O.learn_3d(b, ks, 1.0, 0.1, 2, tol, verbose, init,
+                                                   trace_objective=trace)
+    d_e, z_e, DZ_e, obj_e, it_e = E.admm_learn_conv3D_large(b, ks, 1.0, 0.1, 2, tol, verbose, init,
+                                                            trace_objective=trace, ctx=gpu_ctx)
+    assert _rel(d_e, d_o) < 1e-7
+    assert _rel(z_e, z_o) < 1e-7
+    assert _rel(DZ_e, DZ_o) < 1e-7
+    assert abs(obj_e - obj_o) <= 1e-9 * abs(obj_o)
+    if trace:
+        tr = it_e["trace"]
+        np.testing.assert_array_equal(tr["n_z"], np.array(tr_o["n_z"]))
+        np.testing.assert_array_equal(tr["n_d"], np.array(tr_o["n_d"]))
+        for i, oz in enumerate(tr_o["obj_z"]):
+            np.testing.assert_allclose(tr["obj_z"][i, :len(oz)], oz, rtol=1e-9)
+
+
 @pytest.mark.parametrize("sb,UV,psf,K,n", [((10, 9), 2, 5, 3, 4),
                                            ((64, 64), 5, 11, 4, 4),    # C5 grid 74x74, 25 views
                                            ((8, 8), 6, 3, 40, 4)])     # Woodbury over the views
