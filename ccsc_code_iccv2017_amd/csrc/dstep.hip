@@ -1406,20 +1406,21 @@ __global__ __launch_bounds__(64 * kWbsWG) __attribute__((amdgpu_waves_per_eu(2))
   }
 }
 
-// the many-view d-solve runs staged (k_dsolve_wbs) and then reads h in Ch's layout
-static bool wb_staged(int K, int NV, int F) {
-  const char* es = std::getenv("CCSC_WB_STAGE");   // A/B: CCSC_WB_STAGE=0 keeps k_dsolve_wbv
-  return NV > 1 && NV <= 32 && K <= 64 && !(es && es[0] == '0') &&
+// the many-view d-solve runs staged (k_dsolve_wbs) and then reads h in Ch's layout.
+// `allow` is the session's choice (CCSC_WB_STAGE, read once at session creation), passed to
+// both launchers so the Gram's h layout and the solve's reads cannot disagree
+static bool wb_staged(int K, int NV, int F, bool allow) {
+  return allow && NV > 1 && NV <= 32 && K <= 64 &&
          (int64_t)K * NV * F * (int64_t)sizeof(cpx<double>) < ((int64_t)1 << 32);
 }
 
 template <typename T>
 hipError_t launch_gram_wb(const cpx<T>* Zh, const cpx<T>* Bh, cpx<T>* L, cpx<T>* h, int F, int K,
-                          int ni, T rho, int NV, hipStream_t st) {
+                          int ni, T rho, int NV, bool staged, hipStream_t st) {
   if (!woodbury_ok(K, ni)) return hipErrorInvalidValue;
   const int Kp = K * (K + 1) / 2;
   const dim3 grid((unsigned)((((F + kWbWG - 1) / kWbWG + 7) / 8) * 8));   // whole XCD rounds
-  if (wb_staged(K, NV, F))
+  if (wb_staged(K, NV, F, staged))
     hipLaunchKernelGGL((k_gram_wb<T, 1, true>), grid, dim3(64 * kWbWG), 0, st, Zh, Bh, L, h, F, K,
                        ni, rho, NV, Kp);
   else if (K <= 64)
@@ -1442,7 +1443,8 @@ static void dsolve_wb_go(dim3 grid, hipStream_t st, const cpx<T>* L, const cpx<T
 
 template <typename T>
 hipError_t launch_dsolve_wb(const cpx<T>* L, const cpx<T>* h, const cpx<T>* Ch, cpx<T>* Dh,
-                            int nblocks, int F, int K, int ni, T rho, int NV, hipStream_t st) {
+                            int nblocks, int F, int K, int ni, T rho, int NV, bool staged,
+                            hipStream_t st) {
   if (nblocks <= 0) return hipSuccess;
   if (!woodbury_ok(K, ni)) return hipErrorInvalidValue;
   const int fgroups = (F + kWbWG - 1) / kWbWG;
@@ -1455,7 +1457,7 @@ hipError_t launch_dsolve_wb(const cpx<T>* L, const cpx<T>* h, const cpx<T>* Ch, 
       hipLaunchKernelGGL(kern, dim3(grid.x), dim3(64 * kWbWG), smem, st, L, h, Ch, Dh, F, K, rho,
                          fgroups, n, NV, ni, K * (K + 1) / 2);
     };
-    if (wb_staged(K, NV, F)) {   // staged views (k_dsolve_wbs; h in Ch's layout, k_gram_wb)
+    if (wb_staged(K, NV, F, staged)) {   // staged views (k_dsolve_wbs; h in Ch's layout, k_gram_wb)
       const int kh = (K + 1) / 2;
       const size_t smem2 = (size_t)kWbsWG * (ni * K + ni * ni + kWbvPad) * sizeof(cpx<T>) +
                            wbs_stage_elems() * sizeof(cpx<T>);
@@ -1496,10 +1498,11 @@ hipError_t launch_dsolve_wb(const cpx<T>* L, const cpx<T>* h, const cpx<T>* Ch, 
 }
 
 template hipError_t launch_gram_wb<double>(const cpx<double>*, const cpx<double>*, cpx<double>*,
-                                           cpx<double>*, int, int, int, double, int, hipStream_t);
+                                           cpx<double>*, int, int, int, double, int, bool,
+                                           hipStream_t);
 template hipError_t launch_dsolve_wb<double>(const cpx<double>*, const cpx<double>*,
                                              const cpx<double>*, cpx<double>*, int, int, int, int,
-                                             double, int, hipStream_t);
+                                             double, int, bool, hipStream_t);
 template hipError_t launch_gram_chol<double>(const cpx<double>*, const cpx<double>*,
                                              cpx<double>*, cpx<double>*, int, int, int, double,
                                              int, hipStream_t);

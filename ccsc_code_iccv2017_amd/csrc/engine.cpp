@@ -305,9 +305,10 @@ struct Geom {
 // engine capability check (separate from validity: valid reference inputs we
 // do not run yet return CCSC_E_UNSUPPORTED)
 static void check_supported(const ccsc_problem& p, Geom* Gout) {
-  // (the 2-3D learner forms its right-hand sides with the per-bin GEMM, not in the gram kernel)
-  if (p.variant != CCSC_HS23 && (int64_t)p.K * p.views[0] * p.views[1] > 2048)
-    throw Err(CCSC_E_UNSUPPORTED, "K * views > 2048 exceeds the gram kernel's RHS budget");
+  // (right-hand sides past the Gram kernels' budget, K * views > 2048 or views > 16, are
+  // formed by the per-bin GEMM of hs23.hip instead, Session2D::h_sep)
+  if ((int64_t)p.K * p.views[0] * p.views[1] > (int64_t)1 << 20)
+    throw Err(CCSC_E_UNSUPPORTED, "K * views > 2^20 filter slices");
   // K <= 192: the register-resident MFMA factor (gramchol.hip); 192 < K <= 400: the
   // HBM-resident Gram + left-looking Cholesky of gramchol_big.hip (consensus learners)
   if (p.K > 400) throw Err(CCSC_E_UNSUPPORTED, "K > 400 exceeds the d-solve's rows per lane");
@@ -326,11 +327,11 @@ static void check_supported(const ccsc_problem& p, Geom* Gout) {
   // 3D: the plane kernels also need a t-tile plan (k_tfft / k_tsolve3 hold whole t-columns)
   if (fits && is3 && !make_gridt(Tn, g.G.Xh, g.Gt, why)) fits = false;
   if (!fits) {
-    // the 2D, 4D and 3D consensus learners on any grid the reference accepts (dP:16,23-24;
-    // L3:16,23-26): slices past one CU's LDS (or 3D t-columns past the t-tile kernels) take
-    // the global line passes (the 2-3D learner does not)
+    // every learner on any grid the reference accepts (dP:16,23-24; L3:16,23-26;
+    // L23:12-26): slices past one CU's LDS (or 3D t-columns past the t-tile kernels) take
+    // the global line passes
     const bool gp_ok = p.variant == CCSC_DPAR || p.variant == CCSC_DZPAR ||
-                       p.variant == CCSC_L4D || is3;
+                       p.variant == CCSC_L4D || is3 || p.variant == CCSC_HS23;
     RowGeom rg{};
     ColGeom cy{}, ct{};
     std::vector<cpx<double>> t1, t2, t3;
@@ -513,6 +514,11 @@ struct Session2D {
   bool gram_mf;    // Gram + Cholesky on the matrix cores (gramchol.hip; else the VALU form)
   bool dtile = false;   // tile d-solve on a factor with inverted diagonal tiles (dstep.hip)
   bool gram_big = false;   // K > 192: HBM-resident Gram + Cholesky (gramchol_big.hip), X its workspace
+  // right-hand sides h = A^H b past what the Gram kernels hold (K NV > 2048 or NV > 16 for
+  // gramchol.hip, K NV > 8192 for gramchol_big.hip): the Gram runs with NV = 0 and the
+  // per-bin GEMM of hs23.hip forms h (its Zh^H Xi, L23:289-295), same [F][NV][K] layout
+  bool h_sep = false;
+  bool wb_stage = true;    // CCSC_WB_STAGE (A/B: 0 keeps k_dsolve_wbv), read once per session
   DevBuf Xbig;
   // the diagonal-tile inversion of block j runs on st2 beside block j+1's precompute R2C
   hipStream_t st2 = nullptr;
@@ -677,8 +683,12 @@ struct Session2D {
     NV = p.views[0] * p.views[1];
     KG = K * NV;
     {
-      gram_mf = gram_chol_mf_ok(K, NV);
-      gram_big = !woodbury && K > 192 && gram_big_ok(K, NV);
+      const char* ew = std::getenv("CCSC_WB_STAGE");
+      wb_stage = !(ew && ew[0] == '0');
+      h_sep = !woodbury && (K > 192 ? !gram_big_ok(K, NV) : !gram_chol_mf_ok(K, NV));
+      const int NVg = h_sep ? 0 : NV;
+      gram_mf = gram_chol_mf_ok(K, NVg);
+      gram_big = !woodbury && K > 192 && gram_big_ok(K, NVg);
       // tile d-solve (one read of the factor per solve) on the MFMA factor with inverted
       // diagonal tiles; CCSC_DS_TILE=0 keeps the two-sweep k_dsolve
       const char* et = std::getenv("CCSC_DS_TILE");
@@ -1348,12 +1358,15 @@ struct Session2D {
         const cpx<double>* Bj = Bhat.as<cpx<double>>() + (size_t)jl * ni * NV * F;
         cpx<double>* Lj = L.as<cpx<double>>() + (size_t)jl * F * Kp;
         cpx<double>* hj = h.as<cpx<double>>() + (size_t)jl * F * NV * K;
+        const int NVg = h_sep ? 0 : NV;
+        if (h_sep)
+          HIPCHK(launch_hs_corr<double>(Zc, Bj, hj, F, NV, K, ni, st));
         if (woodbury)
-          HIPCHK(launch_gram_wb<double>(Zc, Bj, Lj, hj, F, K, ni, p.rho_d, NV, st));
+          HIPCHK(launch_gram_wb<double>(Zc, Bj, Lj, hj, F, K, ni, p.rho_d, NV, wb_stage, st));
         else if (gram_big)
-          HIPCHK(launch_gram_big(Zc, Bj, Xbig.as<cpx<double>>(), Lj, hj, F, K, ni, p.rho_d, NV, st));
+          HIPCHK(launch_gram_big(Zc, Bj, Xbig.as<cpx<double>>(), Lj, hj, F, K, ni, p.rho_d, NVg, st));
         else if (gram_mf) {
-          HIPCHK(launch_gram_chol_mf(Zc, Bj, Lj, hj, F, K, ni, p.rho_d, NV, st));
+          HIPCHK(launch_gram_chol_mf(Zc, Bj, Lj, hj, F, K, ni, p.rho_d, NVg, st));
           if (dtile) {
             HIPCHK(hipEventRecord(ev_g, st));
             HIPCHK(hipStreamWaitEvent(st2, ev_g, 0));
@@ -1361,7 +1374,7 @@ struct Session2D {
           }
         }
         else
-          HIPCHK(launch_gram_chol<double>(Zc, Bj, Lj, hj, F, K, ni, p.rho_d, NV, st));
+          HIPCHK(launch_gram_chol<double>(Zc, Bj, Lj, hj, F, K, ni, p.rho_d, NVg, st));
       });
       if (ovz) HIPCHK(hipEventRecord(ev_gz[jl & 1], st));
     }
@@ -1379,7 +1392,7 @@ struct Session2D {
         if (woodbury)
           HIPCHK(launch_dsolve_wb<double>(L.as<cpx<double>>(), h.as<cpx<double>>(),
                                           Ch.as<cpx<double>>(), Dh.as<cpx<double>>(), (int)nbl, F,
-                                          K, ni, p.rho_d, NV, st));
+                                          K, ni, p.rho_d, NV, wb_stage, st));
         else if (dtile)
           HIPCHK(launch_dsolve_tile(L.as<cpx<double>>(), h.as<cpx<double>>(),
                                     Ch.as<cpx<double>>(), Dh.as<cpx<double>>(), (int)nbl, F, K,
@@ -1642,8 +1655,10 @@ struct Session2D {
 //            Ch [K][W][F] (xi_D{2}), Dh, Dhold [K][W][F] (d_hat), h [F][W][K],
 //            L [F][K(K+1)/2] (Cholesky of Z'Z + rho I per bin)
 struct PlanHS {
-  size_t b, vwn, dwk, zkn, Zh, Xi, dspec, L, h, misc;
-  size_t total() const { return b + 4 * vwn + 3 * dwk + 3 * zkn + Zh + Xi + 3 * dspec + L + h + misc; }
+  size_t b, vwn, dwk, zkn, Zh, Xi, dspec, L, h, misc, gr;
+  size_t total() const {
+    return b + 4 * vwn + 3 * dwk + 3 * zkn + Zh + Xi + 3 * dspec + L + h + misc + gr;
+  }
 };
 
 static PlanHS plan_hs(const ccsc_problem& p, const Geom& g) {
@@ -1662,7 +1677,9 @@ static PlanHS plan_hs(const ccsc_problem& p, const Geom& g) {
   // smooth_init staging, sden, support/projection, d0 staging, reduction scratch, twiddles
   m.misc = m.b + F * 8 + 2 * W * K * SS * 8 + 2 * W * K * 8 + (SS * K + SS * W * K) * 8 +
            (2 * std::max<size_t>(std::max(W * n, K * n), kNormParts) + 8) * 8 +
-           (size_t)g.G.ntw * 16;
+           (size_t)g.G.ntw * 16 + (g.gp ? 64 * 1024 : 0);
+  // global-pass slices: the real scratch of the largest transform batch
+  m.gr = g.gp ? std::max({W * n, K * n, W * K}) * P * 8 : 0;
   return m;
 }
 
@@ -1679,6 +1696,12 @@ struct SessionHS {
 
   DevBuf tw, bdev, smp, v, eD, eZ, D, yD, Dold, z, eZ2, zold, Zh, Xi, Ch, Dh, Dhold, L, h, sden,
       Usup, supp, dnorm, part, pair;
+  // slices past one CU's LDS (Geom::gp): the global line passes of recon.hip with the
+  // elementwise halves of the fused slice kernels in gslice.hip over the real scratch gR
+  bool gp = false;
+  RowGeom grg{};
+  ColGeom gcy{};
+  DevBuf gtwr, gtwc, gR;
 
   int outer_done = 0;
   bool finished = false;
@@ -1705,6 +1728,7 @@ struct SessionHS {
     }
     if (!b || !smooth_init) throw Err(CCSC_E_INVALID, "b and smooth_init must not be NULL");
     G = g.G;
+    gp = g.gp;
     m = plan_hs(p, g);
     r = p.psf / 2;
     s = p.psf;
@@ -1728,6 +1752,15 @@ struct SessionHS {
     auto tws = make_twiddles(G);
     tw.alloc(tws.size() * sizeof(cpx<double>));
     HIPCHK(hipMemcpy(tw.p, tws.data(), tw.bytes, hipMemcpyHostToDevice));
+    if (gp) {
+      std::vector<cpx<double>> t1, t2;
+      if (!gfft_plan(G.X, G.Y, grg, gcy, t1, t2)) throw Err(CCSC_E_UNSUPPORTED, "no global line plan");
+      gtwr.alloc(t1.size() * sizeof(cpx<double>));
+      gtwc.alloc(t2.size() * sizeof(cpx<double>));
+      HIPCHK(hipMemcpy(gtwr.p, t1.data(), gtwr.bytes, hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(gtwc.p, t2.data(), gtwc.bytes, hipMemcpyHostToDevice));
+      gR.alloc(m.gr);
+    }
     const size_t vwn = (size_t)P * W * n, dwk = (size_t)P * KG, zkn = (size_t)P * K * n;
     bdev.alloc(m.b);
     smp.alloc(vwn * 8);
@@ -1798,8 +1831,7 @@ struct SessionHS {
     if (z0) HIPCHK(hipMemcpy(z.p, z0, z.bytes, hipMemcpyHostToDevice));
     else HIPCHK(launch_randn<double>(z.as<double>(), (int64_t)zkn, p.seed, 0, st));
     // d_hat = fft2(d) (L23:57); u_D{2} of the first d-iteration = Pi(d - 0) (L23:113)
-    HIPCHK(launch_r2c_embed<double>(D.as<double>(), P, G.X, G.Y, 0, 0, Dh.as<cpx<double>>(), F, KG,
-                                    tw.as<cpx<double>>(), G, st));
+    r2c_full(D.as<double>(), Dh.as<cpx<double>>(), KG);
     HIPCHK(launch_gather_support<double>(D.as<double>(), yD.as<double>(), supp.as<double>(), KG, r,
                                          G.X, G.Y, st));
     HIPCHK(launch_project<double>(supp.as<double>(), Usup.as<double>(), KG, SS, 1.0, st));
@@ -1810,12 +1842,129 @@ struct SessionHS {
     v_tim.push_back(0.0);
   }
 
+  // ---- slice transforms: the fused LDS slice kernels, or on global-pass slices the line
+  // passes of recon.hip around gslice.hip's elementwise halves.  On global passes the
+  // inverse consumes its input spectrum (the column pass runs in place): Xi and Zh are dead
+  // after their C2R here; Dh is copied to Ch (free between its d-solve and the next dual).
+  void g_r2c(const double* src, cpx<double>* dst, int64_t count) {
+    RowArgs<double> a{};
+    a.S = dst;
+    a.src = src;
+    a.per_img = 1;
+    HIPCHK(launch_rows<double>(kRowFwd, a, count, grg, gtwr.as<cpx<double>>(), st));
+    HIPCHK(launch_cols<double>(dst, -1, count, gcy, gtwc.as<cpx<double>>(), st));
+  }
+  void g_c2r(cpx<double>* src, double* dst, int64_t count) {
+    HIPCHK(launch_cols<double>(src, +1, count, gcy, gtwc.as<cpx<double>>(), st));
+    RowArgs<double> a{};
+    a.S = src;
+    a.Z = dst;
+    a.per_img = 1;
+    HIPCHK(launch_rows<double>(kRowFinalZ, a, count, grg, gtwr.as<cpx<double>>(), st));
+  }
+  // fft2 of whole real slices (L23:57,100,158,234)
+  void r2c_full(const double* src, cpx<double>* dst, int64_t count) {
+    if (gp) g_r2c(src, dst, count);
+    else
+      HIPCHK(launch_r2c_embed<double>(src, P, G.X, G.Y, 0, 0, dst, F, count, tw.as<cpx<double>>(),
+                                      G, st));
+  }
+  // v = real(ifft2(Xi)), DZ (nullable), the objective's data parts (k_hs_c2r_v)
+  void c2r_v(double* DZ) {
+    const int64_t cnt = (int64_t)W * n;
+    if (!gp) {
+      HIPCHK(launch_hs_c2r_v<double>(Xi.as<cpx<double>>(), v.as<double>(), bdev.as<double>(),
+                                     smp.as<double>(), DZ, part.as<double>(), cnt,
+                                     tw.as<cpx<double>>(), G, r, sbx, sby, st));
+      return;
+    }
+    g_c2r(Xi.as<cpx<double>>(), gR.as<double>(), cnt);
+    HIPCHK(launch_gp_hs_epilog<double>(kHsV, gR.as<double>(), v.as<double>(), bdev.as<double>(),
+                                       smp.as<double>(), DZ, part.as<double>(), G.X, G.Y, r, sbx,
+                                       sby, 1.0 / (double)P, cnt, st));
+  }
+  // masked-data split with dual e, into Xi (k_hs_data_r2c)
+  void data_r2c(DevBuf& e, double theta) {
+    const int64_t cnt = (int64_t)W * n;
+    if (!gp) {
+      HIPCHK(launch_hs_data_r2c<double>(v.as<double>(), e.as<double>(), bdev.as<double>(),
+                                        smp.as<double>(), Xi.as<cpx<double>>(), cnt,
+                                        tw.as<cpx<double>>(), G, r, sbx, sby, theta, st));
+      return;
+    }
+    HIPCHK(launch_gp_hs_prolog<double>(kHsData, v.as<double>(), e.as<double>(), bdev.as<double>(),
+                                       smp.as<double>(), gR.as<double>(), G.X, G.Y, r, sbx, sby,
+                                       theta, cnt, st));
+    g_r2c(gR.as<double>(), Xi.as<cpx<double>>(), cnt);
+  }
+  // kernel-constraint split of the D-phase, into Ch (k_dual_r2c)
+  void dual_r2c() {
+    if (!gp) {
+      HIPCHK(launch_dual_r2c<double>(D.as<double>(), yD.as<double>(), Usup.as<double>(),
+                                     Ch.as<cpx<double>>(), KG, tw.as<cpx<double>>(), G, KG, r, st));
+      return;
+    }
+    HIPCHK(launch_gp_prolog<double>(2, D.as<double>(), yD.as<double>(), Usup.as<double>(), 0, 0, 0,
+                                    0.0, KG, r, gR.as<double>(), G.X, G.Y, KG, st));
+    g_r2c(gR.as<double>(), Ch.as<cpx<double>>(), KG);
+  }
+  // d = real(ifft2(d_hat)), the support of d + y (k_c2r_dout); Dh stays intact
+  void c2r_dout() {
+    if (!gp) {
+      HIPCHK(launch_c2r_dout<double>(Dh.as<cpx<double>>(), D.as<double>(), yD.as<double>(),
+                                     supp.as<double>(), dnorm.as<double>(), 0, KG,
+                                     tw.as<cpx<double>>(), G, r, st));
+      return;
+    }
+    HIPCHK(hipMemcpyAsync(Ch.p, Dh.p, Dh.bytes, hipMemcpyDeviceToDevice, st));
+    g_c2r(Ch.as<cpx<double>>(), gR.as<double>(), KG);
+    HIPCHK(launch_gp_epilog<double>(2, gR.as<double>(), D.as<double>(), yD.as<double>(),
+                                    supp.as<double>(), dnorm.as<double>(), 0, 1.0 / (double)P, r,
+                                    G.X, G.Y, KG, nullptr, 0.0, 0, st));
+  }
+  // sparsity split of the Z-phase with dual eZ2, into Zh (k_hs_z_r2c)
+  void z_r2c() {
+    const int64_t cnt = (int64_t)K * n;
+    if (!gp) {
+      HIPCHK(launch_hs_z_r2c<double>(z.as<double>(), eZ2.as<double>(), Zh.as<cpx<double>>(), cnt,
+                                     tw.as<cpx<double>>(), G, th_Z2, st));
+      return;
+    }
+    HIPCHK(launch_gp_hs_prolog<double>(kHsSparse, z.as<double>(), eZ2.as<double>(),
+                                       bdev.as<double>(), smp.as<double>(), gR.as<double>(), G.X,
+                                       G.Y, r, sbx, sby, th_Z2, cnt, st));
+    g_r2c(gR.as<double>(), Zh.as<cpx<double>>(), cnt);
+  }
+  // z = real(ifft2(zhat)), sum |z| per slice (k_hs_c2r_z)
+  void c2r_z() {
+    const int64_t cnt = (int64_t)K * n;
+    if (!gp) {
+      HIPCHK(launch_hs_c2r_z<double>(Zh.as<cpx<double>>(), z.as<double>(), part.as<double>(), cnt,
+                                     tw.as<cpx<double>>(), G, st));
+      return;
+    }
+    g_c2r(Zh.as<cpx<double>>(), gR.as<double>(), cnt);
+    HIPCHK(launch_gp_hs_epilog<double>(kHsZ, gR.as<double>(), z.as<double>(), bdev.as<double>(),
+                                       smp.as<double>(), nullptr, part.as<double>(), G.X, G.Y, r,
+                                       sbx, sby, 1.0 / (double)P, cnt, st));
+  }
+  // D = real(ifft2(Dh)) (the rollback); Dh stays intact
+  void c2r_plain_D() {
+    if (!gp) {
+      HIPCHK(launch_c2r_plain<double>(Dh.as<cpx<double>>(), F, D.as<double>(), P, KG,
+                                      tw.as<cpx<double>>(), G, 1.0 / (double)P, st));
+      return;
+    }
+    HIPCHK(hipMemcpyAsync(Ch.p, Dh.p, Dh.bytes, hipMemcpyDeviceToDevice, st));
+    g_c2r(Ch.as<cpx<double>>(), gR.as<double>(), KG);
+    HIPCHK(launch_gp_epilog<double>(0, gR.as<double>(), D.as<double>(), nullptr, nullptr, nullptr,
+                                    0, 1.0 / (double)P, r, G.X, G.Y, KG, nullptr, 0.0, 0, st));
+  }
+
   // v = real(ifft2(H zhat)) from Xi (= H zhat) and the objective of (z, d_hat)
   // (objectiveFunction, L23:326-343); pair[2] must hold sum |z|.
   double finish_objective() {
-    HIPCHK(launch_hs_c2r_v<double>(Xi.as<cpx<double>>(), v.as<double>(), bdev.as<double>(),
-                                   smp.as<double>(), nullptr, part.as<double>(), (int64_t)W * n,
-                                   tw.as<cpx<double>>(), G, r, sbx, sby, st));
+    c2r_v(nullptr);
     HIPCHK(launch_sum_pairs<double>(part.as<double>(), W * n, pair.as<double>(), st));
     double h4[4];
     HIPCHK(hipMemcpyAsync(h4, pair.p, sizeof h4, hipMemcpyDeviceToHost, st));
@@ -1824,8 +1973,7 @@ struct SessionHS {
   }
   // zhat = fft2(z) (L23:100,158,234), sum |z|, v = H z and the objective
   double objective_fresh() {
-    HIPCHK(launch_r2c_embed<double>(z.as<double>(), P, G.X, G.Y, 0, 0, Zh.as<cpx<double>>(), F,
-                                    (int64_t)K * n, tw.as<cpx<double>>(), G, st));
+    r2c_full(z.as<double>(), Zh.as<cpx<double>>(), (int64_t)K * n);
     HIPCHK(launch_norms<double>(z.as<double>(), nullptr, (int64_t)z.bytes / 8, part.as<double>(),
                                 pair.as<double>() + 2, st));
     HIPCHK(launch_hs_synth<double>(Dh.as<cpx<double>>(), Zh.as<cpx<double>>(),
@@ -1854,7 +2002,6 @@ struct SessionHS {
   void outer_iteration() {
     const int it = outer_done;
     const auto t0 = std::chrono::steady_clock::now();
-    const auto* twc = tw.as<cpx<double>>();
     const double obj_min = std::min(obj_filter, obj_z);   // L23:94
     HIPCHK(hipMemcpyAsync(Dold.p, D.p, D.bytes, hipMemcpyDeviceToDevice, st));    // d_old (L23:95)
     HIPCHK(hipMemcpyAsync(Dhold.p, Dh.p, Dh.bytes, hipMemcpyDeviceToDevice, st)); // d_hat_old
@@ -1868,12 +2015,9 @@ struct SessionHS {
     if (hs_dtile) HIPCHK(launch_invert_diag(L.as<cpx<double>>(), F, K, st));
     for (int id = 0; id < p.max_it_d; ++id) {                                    // L23:102
       // c = 1: masked data split (L23:112, 117, 120-121)
-      HIPCHK(launch_hs_data_r2c<double>(v.as<double>(), eD.as<double>(), bdev.as<double>(),
-                                        smp.as<double>(), Xi.as<cpx<double>>(), (int64_t)W * n,
-                                        twc, G, r, sbx, sby, th_D1, st));
+      data_r2c(eD, th_D1);
       // c = 2: kernel constraint split, y = -d_D{2} (L23:113, 117, 120-121)
-      HIPCHK(launch_dual_r2c<double>(D.as<double>(), yD.as<double>(), Usup.as<double>(),
-                                     Ch.as<cpx<double>>(), KG, twc, G, KG, r, st));
+      dual_r2c();
       // d_hat = opt (Z' xi1 + rho xi2) per (bin, wavelength)  (L23:125, 289-295)
       HIPCHK(launch_hs_corr<double>(Zh.as<cpx<double>>(), Xi.as<cpx<double>>(),
                                     h.as<cpx<double>>(), F, W, K, n, st));
@@ -1884,8 +2028,7 @@ struct SessionHS {
         HIPCHK(launch_dsolve<double>(L.as<cpx<double>>(), h.as<cpx<double>>(), Ch.as<cpx<double>>(),
                                      Dh.as<cpx<double>>(), 1, F, K, p.rho_d, W, st));
       // d = real(ifft2(d_hat)) (L23:126); support of d - d_D{2} -> u_D{2} of the next d-iteration
-      HIPCHK(launch_c2r_dout<double>(Dh.as<cpx<double>>(), D.as<double>(), yD.as<double>(),
-                                     supp.as<double>(), dnorm.as<double>(), 0, KG, twc, G, r, st));
+      c2r_dout();
       HIPCHK(launch_project<double>(supp.as<double>(), Usup.as<double>(), KG, SS, 1.0, st));
       // objective (L23:132); its H z is v_D{1} of the next d-iteration (z is fixed here)
       HIPCHK(launch_hs_synth<double>(Dh.as<cpx<double>>(), Zh.as<cpx<double>>(),
@@ -1903,20 +2046,17 @@ struct SessionHS {
     HIPCHK(hipMemcpyAsync(zold.p, z.p, z.bytes, hipMemcpyDeviceToDevice, st));  // z_old (L23:159)
     // v = H z is current: the last D objective used z_hat = fft2(z) (L23:158)
     for (int iz = 0; iz < p.max_it_z; ++iz) {                                    // L23:165
-      HIPCHK(launch_hs_data_r2c<double>(v.as<double>(), eZ.as<double>(), bdev.as<double>(),
-                                        smp.as<double>(), Xi.as<cpx<double>>(), (int64_t)W * n,
-                                        twc, G, r, sbx, sby, th_Z1, st));        // L23:175,180,183-184
-      HIPCHK(launch_hs_z_r2c<double>(z.as<double>(), eZ2.as<double>(), Zh.as<cpx<double>>(),
-                                     (int64_t)K * n, twc, G, th_Z2, st));        // L23:176,180,183-184
+      data_r2c(eZ, th_Z1);                                                       // L23:175,180,183-184
+      z_r2c();                                                                   // L23:176,180,183-184
       HIPCHK(launch_hs_analysis<double>(Dh.as<cpx<double>>(), Xi.as<cpx<double>>(),
                                         Zh.as<cpx<double>>(), sden.as<double>(), p.rho_z,
                                         Zh.as<cpx<double>>(), F, W, K, n, st));  // L23:188, 302-324
-      HIPCHK(launch_hs_c2r_z<double>(Zh.as<cpx<double>>(), z.as<double>(), part.as<double>(),
-                                     (int64_t)K * n, twc, G, st));              // L23:189
-      HIPCHK(launch_sum_pairs<double>(part.as<double>(), K * n, pair.as<double>() + 2, st));
-      // objective (L23:195); H zhat is v_Z{1} of the next z-iteration (L23:171)
+      // objective (L23:195); H zhat is v_Z{1} of the next z-iteration (L23:171) -- formed
+      // before the C2R of zhat, which consumes Zh on global-pass slices
       HIPCHK(launch_hs_synth<double>(Dh.as<cpx<double>>(), Zh.as<cpx<double>>(),
                                      Xi.as<cpx<double>>(), F, W, K, n, st));
+      c2r_z();                                                                   // L23:189
+      HIPCHK(launch_sum_pairs<double>(part.as<double>(), K * n, pair.as<double>() + 2, st));
       obj = finish_objective();
       tr_oz[(size_t)it * p.max_it_z + iz] = obj;
     }
@@ -1926,8 +2066,7 @@ struct SessionHS {
       // roll back to the iterate before this outer iteration and stop
       HIPCHK(hipMemcpyAsync(z.p, zold.p, z.bytes, hipMemcpyDeviceToDevice, st));
       HIPCHK(hipMemcpyAsync(Dh.p, Dhold.p, Dh.bytes, hipMemcpyDeviceToDevice, st));
-      HIPCHK(launch_c2r_plain<double>(Dh.as<cpx<double>>(), F, D.as<double>(), P, KG, twc, G,
-                                      1.0 / (double)P, st));
+      c2r_plain_D();
       obj = objective_fresh();
       finished = true;
       flags |= 1;
@@ -1972,13 +2111,10 @@ struct SessionHS {
       // Dz = real(ifft2(sum_k d_hat .* fft2(z))) + smoothinit  (L23:234-235)
       DevBuf dz;
       dz.alloc(v.bytes);
-      HIPCHK(launch_r2c_embed<double>(z.as<double>(), P, G.X, G.Y, 0, 0, Zh.as<cpx<double>>(), F,
-                                      (int64_t)K * n, tw.as<cpx<double>>(), G, st));
+      r2c_full(z.as<double>(), Zh.as<cpx<double>>(), (int64_t)K * n);
       HIPCHK(launch_hs_synth<double>(Dh.as<cpx<double>>(), Zh.as<cpx<double>>(),
                                      Xi.as<cpx<double>>(), F, W, K, n, st));
-      HIPCHK(launch_hs_c2r_v<double>(Xi.as<cpx<double>>(), v.as<double>(), bdev.as<double>(),
-                                     smp.as<double>(), dz.as<double>(), part.as<double>(),
-                                     (int64_t)W * n, tw.as<cpx<double>>(), G, r, sbx, sby, st));
+      c2r_v(dz.as<double>());
       HIPCHK(hipStreamSynchronize(st));   // st is non-blocking: hipMemcpy does not order after it
       HIPCHK(hipMemcpy(out->DZ, dz.p, dz.bytes, hipMemcpyDeviceToHost));
     }

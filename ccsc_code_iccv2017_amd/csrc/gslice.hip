@@ -164,6 +164,105 @@ __global__ __launch_bounds__(256) void k_gp_crop(const T* __restrict__ R, const 
   if (threadIdx.x == 0) atomicAdd(&part[0], red[0] + red[1] + red[2] + red[3]);
 }
 
+// 2-3D learner (L23) on global-pass slices: the elementwise halves of hs23.hip's fused slice
+// kernels (k_hs_data_r2c, k_hs_z_r2c, k_hs_c2r_v, k_hs_c2r_z), slices [s][y][x] of X x Y.
+// Prologues (into R, the forward transform's input; elementwise):
+//   kHsData:   u = (Mtb + (v - e)/theta) / (M + 1/theta), Mtb = M (padarray(b) - smoothinit),
+//              e <- e - (v - u), R = u + e                  (L23:112,117,120-121 / 175,180,183-184)
+//   kHsSparse: u = max(0, 1 - theta/|z - e|) (z - e), e <- e - (z - u), R = u + e (L23:176,180,183-184)
+// Epilogues (R = the unnormalised C2R output; one workgroup per slice):
+//   kHsV:      v = R invP; DZ = v + smoothinit (nullable); part[2s] = ||crop(v + sm) - b||^2 (L23:334-337)
+//   kHsZ:      z = R invP; part[2s] = sum |z|               (L23:189, 338)
+template <typename T>
+__global__ void k_gp_hs_prolog(int mode, const T* __restrict__ a, T* __restrict__ e,
+                               const T* __restrict__ b, const T* __restrict__ sm,
+                               T* __restrict__ R, int X, int Y, int r, int sbx, int sby, T theta,
+                               int chunks) {
+  const int64_t slice = blockIdx.x / chunks;
+  const int ch = (int)(blockIdx.x - slice * chunks);
+  const int P = X * Y;
+  const int64_t off = slice * P;
+  const T* bs = b + slice * (int64_t)sbx * sby;
+  for (int i = ch * blockDim.x + threadIdx.x; i < P; i += chunks * blockDim.x) {
+    const T av = a[off + i], ev = e[off + i];
+    T u;
+    if (mode == kHsData) {
+      const int y = i / X, x = i - y * X;
+      const bool in = x >= r && x < r + sbx && y >= r && y < r + sby;
+      const T m = in ? (T)1 : (T)0;
+      const T mtb = in ? bs[(y - r) * sbx + (x - r)] - sm[off + i] : (T)0;
+      const T invth = (T)1 / theta;
+      u = (mtb + invth * (av - ev)) / (m + invth);
+    } else {
+      const T q = av - ev, qa = fabs(q);
+      u = ((qa > theta) ? (T)1 - theta / qa : (T)0) * q;
+    }
+    const T en = ev - (av - u);
+    e[off + i] = en;
+    R[off + i] = u + en;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_gp_hs_epilog(int mode, const T* __restrict__ R,
+                                                      T* __restrict__ dst, const T* __restrict__ b,
+                                                      const T* __restrict__ sm, T* __restrict__ DZ,
+                                                      T* __restrict__ part, int X, int Y, int r,
+                                                      int sbx, int sby, T invP) {
+  __shared__ T red[4];
+  const int64_t slice = blockIdx.x;
+  const int P = X * Y;
+  const int64_t off = slice * P;
+  const T* bs = b + slice * (int64_t)sbx * sby;
+  T acc = 0;
+  for (int i = threadIdx.x; i < P; i += 256) {
+    const T val = R[off + i] * invP;
+    dst[off + i] = val;
+    if (mode == kHsV) {
+      const int y = i / X, x = i - y * X;
+      const T smv = sm[off + i];
+      if (DZ) DZ[off + i] = val + smv;
+      if (x >= r && x < r + sbx && y >= r && y < r + sby) {
+        const T d = (val + smv) - bs[(y - r) * sbx + (x - r)];
+        acc += d * d;
+      }
+    } else {
+      acc += fabs(val);
+    }
+  }
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    part[2 * slice] = red[0] + red[1] + red[2] + red[3];
+    part[2 * slice + 1] = (T)0;
+  }
+}
+
+template <typename T>
+hipError_t launch_gp_hs_prolog(int mode, const T* a, T* e, const T* b, const T* sm, T* R, int X,
+                               int Y, int r, int sbx, int sby, T theta, int64_t count,
+                               hipStream_t st) {
+  if (count <= 0) return hipSuccess;
+  if (mode != kHsData && mode != kHsSparse) return hipErrorInvalidValue;
+  const int P = X * Y;
+  const int chunks = (int)std::min<int64_t>((P + 255) / 256, 64);
+  if (count * chunks >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_gp_hs_prolog<T>, dim3((unsigned)(count * chunks)), dim3(256), 0, st, mode,
+                     a, e, b, sm, R, X, Y, r, sbx, sby, theta, chunks);
+  return hipGetLastError();
+}
+template <typename T>
+hipError_t launch_gp_hs_epilog(int mode, const T* R, T* dst, const T* b, const T* sm, T* DZ,
+                               T* part, int X, int Y, int r, int sbx, int sby, T invP,
+                               int64_t count, hipStream_t st) {
+  if (count <= 0) return hipSuccess;
+  if (mode != kHsV && mode != kHsZ) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_gp_hs_epilog<T>, dim3((unsigned)count), dim3(256), 0, st, mode, R, dst, b,
+                     sm, DZ, part, X, Y, r, sbx, sby, invP);
+  return hipGetLastError();
+}
+
 template <typename T>
 hipError_t launch_gp_zdiag(cpx<T>* C, const cpx<T>* E, const T* sden, T rho, int F, int64_t count,
                            hipStream_t st) {
@@ -213,6 +312,12 @@ hipError_t launch_gp_epilog(int mode, const T* R, T* dst, const T* yv, T* supp, 
   return hipGetLastError();
 }
 
+template hipError_t launch_gp_hs_prolog<double>(int, const double*, double*, const double*,
+                                                const double*, double*, int, int, int, int, int,
+                                                double, int64_t, hipStream_t);
+template hipError_t launch_gp_hs_epilog<double>(int, const double*, double*, const double*,
+                                                const double*, double*, double*, int, int, int,
+                                                int, int, double, int64_t, hipStream_t);
 template hipError_t launch_gp_zdiag<double>(cpx<double>*, const cpx<double>*, const double*, double,
                                             int, int64_t, hipStream_t);
 template hipError_t launch_gp_views<double>(const cpx<double>*, const cpx<double>*, cpx<double>*, int,

@@ -148,10 +148,13 @@ inline bool woodbury_ok(int K, int ni) {
 inline bool woodbury_fits(int K, int ni) { return woodbury_ok(K, ni) && 4 * ni <= K; }
 template <typename T>
 hipError_t launch_gram_wb(const cpx<T>* Zh, const cpx<T>* Bh, cpx<T>* L, cpx<T>* h, int F, int K,
-                          int ni, T rho, int NV, hipStream_t st);
+                          int ni, T rho, int NV, bool staged, hipStream_t st);
+// staged: the session's choice of the staged many-view solve (CCSC_WB_STAGE, read once);
+// the same value must reach launch_gram_wb and launch_dsolve_wb (it sets h's layout)
 template <typename T>
 hipError_t launch_dsolve_wb(const cpx<T>* L, const cpx<T>* h, const cpx<T>* Ch, cpx<T>* Dh,
-                            int nblocks, int F, int K, int ni, T rho, int NV, hipStream_t st);
+                            int nblocks, int F, int K, int ni, T rho, int NV, bool staged,
+                            hipStream_t st);
 
 // ---- kernels3d.hip: the 3D learner's factored transforms -------------------
 // Spectra [slice][t][F2]; P2 = X*Y plane voxels.  Modes: see kernels3d.hip.
@@ -217,6 +220,17 @@ template <typename T>
 hipError_t launch_gp_epilog(int mode, const T* R, T* dst, const T* yv, T* supp, T* norms,
                             int64_t nfirst, T scale, int r, int X, int Y, int64_t count,
                             T* state, T theta, int wz, hipStream_t st, int Tn = 1);
+// the 2-3D learner's slices past one CU's LDS: prologues (masked data prox / sparsity prox +
+// dual into R) and epilogues (v or z from the C2R output + the objective's per-slice parts)
+enum GpHsMode : int { kHsData = 0, kHsSparse = 1, kHsV = 2, kHsZ = 3 };
+template <typename T>
+hipError_t launch_gp_hs_prolog(int mode, const T* a, T* e, const T* b, const T* sm, T* R, int X,
+                               int Y, int r, int sbx, int sby, T theta, int64_t count,
+                               hipStream_t st);
+template <typename T>
+hipError_t launch_gp_hs_epilog(int mode, const T* R, T* dst, const T* b, const T* sm, T* DZ,
+                               T* part, int X, int Y, int r, int sbx, int sby, T invP,
+                               int64_t count, hipStream_t st);
 
 // ---- hs23.hip: the 2-3D hyperspectral learner (L23) ----------------------------
 // Spectra slice-major [slice][F]: dhat [K][W], zhat [n][K], Xi1 / Yv [n][W]; h [F][W][K].

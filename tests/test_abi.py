@@ -197,3 +197,23 @@ def test_3d_and_4d_configs_supported_and_fit(L):
     p4.views[0] = p4.views[1] = 5
     assert L.lib().ccsc_supported(C.byref(p4), eb, len(eb)) == 0, eb.value
     assert plan_bytes(p4, 0, 1) < 288e9 * 0.9
+
+
+@pytest.mark.parametrize("sb", [(200, 200), (512, 512), (252, 150)])
+def test_hs23_grids_past_lds_supported(L, sb):
+    """The 2-3D learner on images whose 2D slice does not fit one CU's LDS (210^2, 522^2,
+    262 x 160) runs on the global line passes (VERDICT r05 missing item 2)."""
+    eb = L.errbuf()
+    p = _problem(L, 4, sb=sb, n=4, K=8)
+    p.views[0] = 31
+    assert L.lib().ccsc_supported(C.byref(p), eb, len(eb)) == 0, eb.value
+
+
+@pytest.mark.parametrize("K,UV,n", [(100, 5, 64), (100, 5, 10000), (49, 9, 64), (300, 5, 16)])
+def test_4d_many_filter_views_supported(L, K, UV, n):
+    """K * views past the Gram kernels' right-hand-side budget (2500 = 100 filters x 5 x 5
+    views, VERDICT r05 missing item 3): h is formed by the per-bin GEMM instead."""
+    eb = L.errbuf()
+    p = _problem(L, 3, sb=(64, 64), n=n, K=K)
+    p.views[0] = p.views[1] = UV
+    assert L.lib().ccsc_supported(C.byref(p), eb, len(eb)) == 0, eb.value
