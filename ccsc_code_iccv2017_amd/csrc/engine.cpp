@@ -283,7 +283,9 @@ static void resolve_problem(ccsc_problem& p) {
   // AUTO resolves to the form the consensus learners will run (observable through
   // ccsc_resolve): the ni x ni Woodbury factor for blocks of few patches, else K x K
   if (p.variant != CCSC_HS23 && p.dfactor == CCSC_DFACTOR_AUTO)
-    p.dfactor = woodbury_fits(p.K, p.ni) ? CCSC_DFACTOR_WOODBURY : CCSC_DFACTOR_CHOLESKY;
+    p.dfactor = (woodbury_fits(p.K, p.ni) || (p.K > 400 && wbig_ok(p.K, p.ni)))
+                    ? CCSC_DFACTOR_WOODBURY
+                    : CCSC_DFACTOR_CHOLESKY;
   const int r = p.psf / 2;
   for (int i = 0; i < p.ndim; ++i)
     if (p.sb[i] + 2 * r < p.psf) throw Err(CCSC_E_INVALID, "grid smaller than the filter");
@@ -310,12 +312,19 @@ static void check_supported(const ccsc_problem& p, Geom* Gout) {
   if ((int64_t)p.K * p.views[0] * p.views[1] > (int64_t)1 << 20)
     throw Err(CCSC_E_UNSUPPORTED, "K * views > 2^20 filter slices");
   // K <= 192: the register-resident MFMA factor (gramchol.hip); 192 < K <= 400: the
-  // HBM-resident Gram + left-looking Cholesky of gramchol_big.hip (consensus learners)
-  if (p.K > 400) throw Err(CCSC_E_UNSUPPORTED, "K > 400 exceeds the d-solve's rows per lane");
-  if (p.K > 192 && p.variant == CCSC_HS23)
-    throw Err(CCSC_E_UNSUPPORTED, "the 2-3D learner's factor holds K <= 192");
-  if (p.dfactor == CCSC_DFACTOR_WOODBURY && (p.variant == CCSC_HS23 || !woodbury_ok(p.K, p.ni)))
-    throw Err(CCSC_E_UNSUPPORTED, "the Woodbury D-factor needs ni <= 8 and ni K + ni^2 <= K (K + 1) / 2 "
+  // HBM-resident Gram + left-looking Cholesky of gramchol_big.hip (consensus learners);
+  // K > 400 (consensus) and K > 192 (2-3D): the reference's Woodbury form on the ni x ni
+  // (n x n) factor (wbig.hip), for ni <= 100 and ni K + ni^2 <= K (K + 1) / 2
+  if (p.K > 400 && p.variant != CCSC_HS23 &&
+      !(p.dfactor == CCSC_DFACTOR_WOODBURY && wbig_ok(p.K, p.ni)))
+    throw Err(CCSC_E_UNSUPPORTED, "K > 400 runs the Woodbury D-factor only, which needs ni <= 100 and "
+                                  "ni K + ni^2 <= K (K + 1) / 2");
+  if (p.K > 192 && p.variant == CCSC_HS23 && (p.n > INT32_MAX || !wbig_ok(p.K, (int)p.n)))
+    throw Err(CCSC_E_UNSUPPORTED, "the 2-3D learner past K = 192 runs the n x n Woodbury factor "
+                                  "(L23:290), which needs n <= 100 and n K + n^2 <= K (K + 1) / 2");
+  if (p.dfactor == CCSC_DFACTOR_WOODBURY &&
+      (p.variant == CCSC_HS23 || !(woodbury_ok(p.K, p.ni) || wbig_ok(p.K, p.ni))))
+    throw Err(CCSC_E_UNSUPPORTED, "the Woodbury D-factor needs ni <= 100 and ni K + ni^2 <= K (K + 1) / 2 "
                                   "(consensus learners only)");
   const int r = p.psf / 2;
   Geom g;
@@ -423,7 +432,11 @@ static Plan2D plan2d(const ccsc_problem& p, const Geom& g, int rank, int nranks)
   m.Dh = m.Ch;
   m.Zh = (size_t)p.ni * K * F * 16;
   // K > 192 (gramchol_big.hip): the block's code spectra transposed frequency-major
-  m.big = (K > 192 && p.dfactor != CCSC_DFACTOR_WOODBURY) ? m.Zh : 0;
+  // (and the Woodbury form past k_gram_wb's ni <= 8, wbig.hip: the same frequency-major slabs)
+  m.big = ((K > 192 && p.dfactor != CCSC_DFACTOR_WOODBURY) ||
+           (p.dfactor == CCSC_DFACTOR_WOODBURY && !woodbury_ok((int)K, p.ni)))
+              ? m.Zh
+              : 0;
   // 4D: view correlations E; 3D: spectra of the z-step's plane/t transforms, in the
   // t-minor tile order when k_tsolve3 runs (padded to whole tiles: sized for TC = 4),
   // with B^, the filter spectrum and sden in that order (misc)
@@ -511,6 +524,7 @@ struct Session2D {
   int NV, KG;   // views, filter slices per block (K * NV)
   bool is4, is3;
   bool woodbury;   // D-factor in Woodbury form (p.dfactor; AUTO: woodbury_fits, ni << K)
+  bool wbig = false;   // ... past k_gram_wb's ni <= 8 (wbig.hip; K > 400 resolves to it)
   bool gram_mf;    // Gram + Cholesky on the matrix cores (gramchol.hip; else the VALU form)
   bool dtile = false;   // tile d-solve on a factor with inverted diagonal tiles (dstep.hip)
   bool gram_big = false;   // K > 192: HBM-resident Gram + Cholesky (gramchol_big.hip), X its workspace
@@ -680,6 +694,7 @@ struct Session2D {
     Kp = K * (K + 1) / 2;
     woodbury = p.dfactor == CCSC_DFACTOR_WOODBURY ||
                (p.dfactor == CCSC_DFACTOR_AUTO && woodbury_fits(K, ni));
+    wbig = woodbury && !woodbury_ok(K, ni);
     NV = p.views[0] * p.views[1];
     KG = K * NV;
     {
@@ -794,7 +809,7 @@ struct Session2D {
     L.alloc(m.L);
     h.alloc(m.h);
     Zh.alloc(m.Zh);
-    if (gram_big) Xbig.alloc(m.big);
+    if (gram_big || wbig) Xbig.alloc(m.big);
     dhat.alloc((size_t)KG * F * 16);
     dtmp.alloc((size_t)KG * F * 16);
     sden.alloc((size_t)F * 8);
@@ -1361,7 +1376,9 @@ struct Session2D {
         const int NVg = h_sep ? 0 : NV;
         if (h_sep)
           HIPCHK(launch_hs_corr<double>(Zc, Bj, hj, F, NV, K, ni, st));
-        if (woodbury)
+        if (wbig)
+          HIPCHK(launch_wbig_gram(Zc, Bj, Xbig.as<cpx<double>>(), Lj, hj, F, K, ni, p.rho_d, NV, st));
+        else if (woodbury)
           HIPCHK(launch_gram_wb<double>(Zc, Bj, Lj, hj, F, K, ni, p.rho_d, NV, wb_stage, st));
         else if (gram_big)
           HIPCHK(launch_gram_big(Zc, Bj, Xbig.as<cpx<double>>(), Lj, hj, F, K, ni, p.rho_d, NVg, st));
@@ -1389,7 +1406,10 @@ struct Session2D {
     for (int id = 0; id < p.max_it_d; ++id) {
       timed(3, [&] { dual_fwd(); });
       timed(2, [&] {
-        if (woodbury)
+        if (wbig)
+          HIPCHK(launch_wbig_solve(L.as<cpx<double>>(), h.as<cpx<double>>(), Ch.as<cpx<double>>(),
+                                   Dh.as<cpx<double>>(), (int)nbl, F, K, ni, p.rho_d, NV, st));
+        else if (woodbury)
           HIPCHK(launch_dsolve_wb<double>(L.as<cpx<double>>(), h.as<cpx<double>>(),
                                           Ch.as<cpx<double>>(), Dh.as<cpx<double>>(), (int)nbl, F,
                                           K, ni, p.rho_d, NV, wb_stage, st));
@@ -1655,9 +1675,9 @@ struct Session2D {
 //            Ch [K][W][F] (xi_D{2}), Dh, Dhold [K][W][F] (d_hat), h [F][W][K],
 //            L [F][K(K+1)/2] (Cholesky of Z'Z + rho I per bin)
 struct PlanHS {
-  size_t b, vwn, dwk, zkn, Zh, Xi, dspec, L, h, misc, gr;
+  size_t b, vwn, dwk, zkn, Zh, Xi, dspec, L, h, misc, gr, wx;
   size_t total() const {
-    return b + 4 * vwn + 3 * dwk + 3 * zkn + Zh + Xi + 3 * dspec + L + h + misc + gr;
+    return b + 4 * vwn + 3 * dwk + 3 * zkn + Zh + Xi + 3 * dspec + L + h + misc + gr + wx;
   }
 };
 
@@ -1680,6 +1700,8 @@ static PlanHS plan_hs(const ccsc_problem& p, const Geom& g) {
            (size_t)g.G.ntw * 16 + (g.gp ? 64 * 1024 : 0);
   // global-pass slices: the real scratch of the largest transform batch
   m.gr = g.gp ? std::max({W * n, K * n, W * K}) * P * 8 : 0;
+  // K > 192: the n x n Woodbury factor (wbig.hip) and its frequency-major workspace
+  m.wx = K > 192 ? m.Zh : 0;
   return m;
 }
 
@@ -1708,6 +1730,9 @@ struct SessionHS {
   // 64 < K <= 112: the tile d-solve over the W wavelengths on a factor with inverted
   // diagonal tiles (dstep.hip; CCSC_DS_TILE=0 keeps the two-sweep k_dsolve)
   bool hs_dtile = false;
+  // K > 192: the reference's own n x n Woodbury form of opt_f (L23:290; wbig.hip)
+  bool hs_wbig = false;
+  DevBuf Xw;
   double obj = std::numeric_limits<double>::quiet_NaN();
   double obj_filter = obj, obj_z = obj;
   std::vector<double> v_obj_d, v_obj_z, v_tim, tr_od, tr_oz, tr_dd, tr_zd;
@@ -1725,6 +1750,8 @@ struct SessionHS {
     {
       const char* et = std::getenv("CCSC_DS_TILE");
       hs_dtile = dsolve_tile_ok(p.K, p.views[0]) && !(et && et[0] == '0');
+      hs_wbig = p.K > 192;
+      if (hs_wbig) hs_dtile = false;
     }
     if (!b || !smooth_init) throw Err(CCSC_E_INVALID, "b and smooth_init must not be NULL");
     G = g.G;
@@ -1774,6 +1801,7 @@ struct SessionHS {
     eZ2.alloc(zkn * 8);
     zold.alloc(zkn * 8);
     Zh.alloc(m.Zh);
+    if (m.wx) Xw.alloc(m.wx);
     Xi.alloc(m.Xi);
     Ch.alloc(m.dspec);
     Dh.alloc(m.dspec);
@@ -2009,8 +2037,12 @@ struct SessionHS {
     objective_fresh();
     // opt_f = (Z_f' Z_f + rho I)^-1 as a Cholesky factor per bin (L23:290)
     // on the matrix cores (gramchol.hip, K <= 192; no right-hand side here: NV = 0)
-    HIPCHK(launch_gram_chol_mf(Zh.as<cpx<double>>(), Zh.as<cpx<double>>(), L.as<cpx<double>>(),
-                               h.as<cpx<double>>(), F, K, n, p.rho_d, 0, st));
+    if (hs_wbig)
+      HIPCHK(launch_wbig_gram(Zh.as<cpx<double>>(), Zh.as<cpx<double>>(), Xw.as<cpx<double>>(),
+                              L.as<cpx<double>>(), h.as<cpx<double>>(), F, K, n, p.rho_d, 0, st));
+    else
+      HIPCHK(launch_gram_chol_mf(Zh.as<cpx<double>>(), Zh.as<cpx<double>>(), L.as<cpx<double>>(),
+                                 h.as<cpx<double>>(), F, K, n, p.rho_d, 0, st));
     // 64 < K <= 112: the tile d-solve over the W wavelengths (factor read once per solve)
     if (hs_dtile) HIPCHK(launch_invert_diag(L.as<cpx<double>>(), F, K, st));
     for (int id = 0; id < p.max_it_d; ++id) {                                    // L23:102
@@ -2021,7 +2053,10 @@ struct SessionHS {
       // d_hat = opt (Z' xi1 + rho xi2) per (bin, wavelength)  (L23:125, 289-295)
       HIPCHK(launch_hs_corr<double>(Zh.as<cpx<double>>(), Xi.as<cpx<double>>(),
                                     h.as<cpx<double>>(), F, W, K, n, st));
-      if (hs_dtile)
+      if (hs_wbig)
+        HIPCHK(launch_wbig_solve(L.as<cpx<double>>(), h.as<cpx<double>>(), Ch.as<cpx<double>>(),
+                                 Dh.as<cpx<double>>(), 1, F, K, n, p.rho_d, W, st));
+      else if (hs_dtile)
         HIPCHK(launch_dsolve_tile(L.as<cpx<double>>(), h.as<cpx<double>>(), Ch.as<cpx<double>>(),
                                   Dh.as<cpx<double>>(), 1, F, K, p.rho_d, W, st));
       else

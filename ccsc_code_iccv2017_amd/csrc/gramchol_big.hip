@@ -198,6 +198,11 @@ __global__ __launch_bounds__(kBgCholNT) void k_chol_big(cpx<double>* __restrict_
   }
 }
 
+hipError_t launch_zh_fmajor(const cpx<double>* Z, cpx<double>* X, int R, int F, hipStream_t st) {
+  hipLaunchKernelGGL(k_zh_fmajor, dim3((F + 63) / 64, (R + 63) / 64), dim3(256), 0, st, Z, X, R, F);
+  return hipGetLastError();
+}
+
 bool gram_big_ok(int K, int NV) { return K > 0 && K <= 16 * kBgMaxT && K * NV <= 8192; }
 
 hipError_t launch_gram_big(const cpx<double>* Zh, const cpx<double>* Bh, cpx<double>* X,

@@ -114,6 +114,20 @@ hipError_t launch_gram_chol_mf(const cpx<double>* Zh, const cpx<double>* Bh, cpx
 // transposed into X ([F][ni][K], ni K F complex of workspace), the Gram on the matrix
 // cores into the packed slots of L, then a left-looking Cholesky in place.
 bool gram_big_ok(int K, int NV);
+// X[f][r] = Z[r][f] for the R = ni K rows of a block's code spectra (frequency-major slabs)
+hipError_t launch_zh_fmajor(const cpx<double>* Z, cpx<double>* X, int R, int F, hipStream_t st);
+// The reference's Woodbury form past the packed K x K kernels (wbig.hip): per f the slot of
+// K(K+1)/2 complex holds A_f (ni x K) and the Cholesky factor of M_f = rho I + A_f A_f^H
+// (ni x ni), as k_gram_wb's layout; X is the ni K F complex frequency-major workspace.
+constexpr int kWgMaxNi = 100;
+bool wbig_ok(int K, int ni);
+size_t wbig_workspace(int K, int ni, int F);
+hipError_t launch_wbig_gram(const cpx<double>* Zh, const cpx<double>* Bh, cpx<double>* X,
+                            cpx<double>* L, cpx<double>* h, int F, int K, int ni, double rho, int NV,
+                            hipStream_t st);
+hipError_t launch_wbig_solve(const cpx<double>* L, const cpx<double>* h, const cpx<double>* Ch,
+                             cpx<double>* Dh, int nblocks, int F, int K, int ni, double rho, int NV,
+                             hipStream_t st);
 hipError_t launch_gram_big(const cpx<double>* Zh, const cpx<double>* Bh, cpx<double>* X,
                            cpx<double>* L, cpx<double>* h, int F, int K, int ni, double rho, int NV,
                            hipStream_t st);

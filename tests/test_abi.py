@@ -93,8 +93,8 @@ def test_supported_reports_reasons(L):
     eb = L.errbuf()
     p = _problem(L, 1)
     assert L.lib().ccsc_supported(C.byref(p), eb, len(eb)) == 0
-    # K > 400 -> UNSUPPORTED with the reason
-    p = _problem(L, 1, n=200, K=401)
+    # K > 400 with ni > 100 -> UNSUPPORTED with the reason
+    p = _problem(L, 1, n=400, K=401, ni=200)
     rc = L.lib().ccsc_supported(C.byref(p), eb, len(eb))
     assert rc == L.CCSC_E_UNSUPPORTED and b"K > 400" in eb.value
 
@@ -137,15 +137,24 @@ def test_generic_prime_grid_lengths_plan(L, sb):
 def test_filter_count_limits(L):
     """K <= 192: the register-resident MFMA factor; 192 < K <= 400: gramchol_big.hip, whose
     frequency-major code-spectra workspace (ni K F complex) joins the device plan; K > 400
-    and the 2-3D learner past K = 192 are CCSC_E_UNSUPPORTED with a reason."""
+    and the 2-3D learner past K = 192: the Woodbury form on the ni x ni (n x n) factor."""
     from ccsc_code_iccv2017_amd.learners import plan_bytes
     eb = L.errbuf()
-    for K, ok in [(192, True), (193, True), (400, True), (401, False)]:
+    for K, ok in [(192, True), (193, True), (400, True), (401, True), (4000, True)]:
         p = _problem(L, 1, n=200, K=K)
         rc = L.lib().ccsc_supported(C.byref(p), eb, len(eb))
         assert (rc == 0) == ok, (K, eb.value)
-        if not ok:
-            assert rc == L.CCSC_E_UNSUPPORTED and b"K > 400" in eb.value
+    # K > 400 resolves to the Woodbury factor (wbig.hip), which needs ni <= 100
+    from ccsc_code_iccv2017_amd.learners import resolve
+    assert resolve(_problem(L, 1, n=200, K=401)).dfactor == L.DFACTOR["woodbury"]
+    p = _problem(L, 1, n=400, K=401, ni=200)
+    rc = L.lib().ccsc_supported(C.byref(p), eb, len(eb))
+    assert rc == L.CCSC_E_UNSUPPORTED and b"K > 400" in eb.value
+    # the 2-3D learner past K = 192: the n x n Woodbury form for n <= 100 images
+    for n, ok in [(8, True), (100, True), (101, False)]:
+        p = _problem(L, 4, sb=(100, 100), n=n, K=300)
+        p.views[0] = 31
+        assert (L.lib().ccsc_supported(C.byref(p), eb, len(eb)) == 0) == ok, (n, eb.value)
     # the big-K workspace: plan(193) - plan(192) exceeds the ni K F complex of X alone
     F = 110 * 56
     grow = plan_bytes(_problem(L, 1, n=200, K=193), 0, 1) - plan_bytes(_problem(L, 1, n=200, K=192), 0, 1)

@@ -68,7 +68,11 @@ def _case(variant, sb, psf, K, n, ni, seed):
                                            # patches per block keep the oracle in seconds)
                                            ((12, 12), 5, 200, 24, 12),
                                            ((12, 12), 5, 260, 6, 3),
-                                           ((12, 12), 5, 400, 4, 2)])
+                                           ((12, 12), 5, 400, 4, 2),
+                                           # K > 400: the reference's Woodbury form on the
+                                           # ni x ni factor (wbig.hip), ni = 2 and 12
+                                           ((6, 6), 5, 420, 4, 2),
+                                           ((6, 6), 5, 450, 24, 12)])
 def test_learn_2d_matches_oracle(gpu_ctx, variant, sb, psf, K, n, ni):
     from ccsc_code_iccv2017_amd import learners as E
     b, d0, z0 = _case(variant, sb, psf, K, n, ni, seed=7)
@@ -285,6 +289,30 @@ def test_learn_4d_matches_oracle(gpu_ctx, sb, UV, psf, K, n):
     assert _rel(DZ_e, DZ_o) < 1e-7
     assert abs(obj_e - obj_o) <= 1e-9 * abs(obj_o)
     np.testing.assert_allclose(it_e["trace"]["obj_d"], np.array(tr_o["obj_d"]), rtol=1e-9)
+    np.testing.assert_allclose(it_e["trace"]["obj_z"], np.array(tr_o["obj_z"]), rtol=1e-9)
+
+
+@pytest.mark.parametrize("variant", ["dp", "dz"])
+@pytest.mark.parametrize("K,n,ni,max_it", [(100, 40, 20, 2), (280, 100, 100, 1)])
+def test_learn_2d_woodbury_many_patches_matches_oracle(gpu_ctx, variant, K, n, ni, max_it):
+    """The Woodbury D-factor past k_gram_wb's ni <= 8 (wbig.hip: A_f and the Cholesky factor
+    of rho I + A_f A_f^H, ni x ni up to the reference's ni = 100, dP:11,230-236), forced with
+    dfactor='woodbury' on shapes the K x K Cholesky also runs -- against the oracle."""
+    from ccsc_code_iccv2017_amd import learners as E
+    sb, psf = (12, 12) if K <= 100 else (6, 6), 5
+    b, d0, z0 = _case(variant, sb, psf, K, n, ni, seed=37)
+    ks = [psf, psf, K]
+    init = {"d": d0, "z": z0}
+    fo = O.learn_2d_dparallel if variant == "dp" else O.learn_2d_dzparallel
+    fe = (E.admm_learn_conv2D_large_dParallel if variant == "dp"
+          else E.admm_learn_conv2D_large_dzParallel)
+    d_o, z_o, DZ_o, it_o, tr_o = fo(b, ks, 1.0, 1.0, max_it, 0.0, "brief", init, ni=ni,
+                                    trace_objective=True)
+    d_e, z_e, DZ_e, it_e = fe(b, ks, 1.0, 1.0, max_it, 0.0, "brief", init, ni=ni,
+                              trace_objective=True, ctx=gpu_ctx, dfactor="woodbury")
+    assert _rel(d_e, d_o) < 1e-7
+    assert _rel(z_e, z_o) < 1e-7
+    assert _rel(DZ_e, DZ_o) < 1e-7
     np.testing.assert_allclose(it_e["trace"]["obj_z"], np.array(tr_o["obj_z"]), rtol=1e-9)
 
 

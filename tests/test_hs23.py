@@ -171,6 +171,8 @@ def test_hs_golden_fixture_regression():
     ((100, 100), 31, 11, 8, 2, 1.0, 1),  # C3's 110 x 110 grid
     ((20, 20), 31, 11, 120, 2, 1.0, 1),  # 112 < K <= 128: TM = 8 MFMA factor
     ((20, 20), 31, 11, 150, 2, 1.0, 1),  # 128 < K <= 192: TM = 10, three rows per lane
+    ((20, 20), 4, 11, 200, 2, 1.0, 1),   # K > 192: the n x n Woodbury factor (L23:290, wbig.hip)
+    ((12, 12), 4, 5, 300, 6, 1.0, 2),    # K = 300, n = 6 images
 ])
 def test_learn_hs23_matches_oracle(gpu_ctx, sb, W, psf, K, n, lam, max_it):
     from ccsc_code_iccv2017_amd import learners as E
