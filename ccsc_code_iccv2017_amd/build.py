@@ -7,6 +7,7 @@ snapshot to the GPU box (it is git-ignored, not gpurun-ignored).
 from __future__ import annotations
 
 import concurrent.futures as cf
+import hashlib
 import os
 import subprocess
 import sys
@@ -28,6 +29,16 @@ def _sources():
 
 def _deps():
     return sorted(list(CSRC.glob("*.hpp")) + [PKG.parent / "include" / "ccsc.h"])
+
+
+def source_hash() -> str:
+    """sha256 over the names and contents of every source and header the library is built
+    from (written next to the library as libccsc.srchash; tools/check_lib.py compares)."""
+    h = hashlib.sha256()
+    for p in sorted(_sources() + _deps(), key=lambda q: q.name):
+        h.update(p.name.encode())
+        h.update(p.read_bytes())
+    return h.hexdigest()
 
 
 def _needs(target: Path, inputs) -> bool:
@@ -65,8 +76,25 @@ def build(force: bool = False, jobs: int | None = None) -> Path:
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr[-6000:]}")
         stamp.write_text(sig + "\n" + f"{LIB.stat().st_mtime_ns}:{LIB.stat().st_size}")
+    # the library is now the link of these sources (a replaced library fails the stamp above)
+    LIB.with_suffix(".srchash").write_text(source_hash() + "\n")
     return LIB
+
+
+PROBE_SRC = PKG.parent / "tools" / "copy_probe.hip"
+PROBE = PKG.parent / "tools" / "libcopy_probe.so"
+
+
+def build_probe(force: bool = False) -> Path:
+    """bench.py's streaming-copy probe (tools/copy_probe.hip -> tools/libcopy_probe.so)."""
+    if force or _needs(PROBE, [PROBE_SRC]):
+        cmd = [HIPCC] + CFLAGS + ["-shared", str(PROBE_SRC), "-o", str(PROBE)]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed for {PROBE_SRC.name}:\n{r.stderr[-6000:]}")
+    return PROBE
 
 
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv))
+    print(build_probe(force="--force" in sys.argv))

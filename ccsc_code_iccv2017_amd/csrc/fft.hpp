@@ -212,11 +212,10 @@ struct Plan1D {
                         // generic-radix pass appends its R roots exp(-2 pi i m/R)
   int pfa;              // n = 2 M, rad = {2, M}: the M pass is fft_pass_pfa (M = kPfaM)
 };
-// Radices with an unrolled in-register butterfly; any other prime factor (up
-// to kMaxGenericRadix, e.g. 37 for the 74-point grids of the 3D/4D configs, or a
-// prime grid length such as 71 = 61 + 2*5) runs through fft_pass_generic, within
-// one task per thread (generic_tasks, engine.cpp).
-constexpr int kMaxGenericRadix = 127;
+// Radices with an unrolled in-register butterfly; any other odd factor (e.g. 37 for the
+// 74-point grids of the 3D/4D configs, 131 for 262 = 2 x 131, 13 and 17 for 221) runs through
+// fft_pass_generic.  The planner (plan1d, engine.cpp) takes the plan with the fewest generic
+// passes, then the fewest passes, within the slice kernels' per-thread task budget.
 constexpr int kGenericQP = 3;      // conjugate output pairs per generic-pass task
 
 // Per-slice description of the 2D grid (all in units of T unless noted).

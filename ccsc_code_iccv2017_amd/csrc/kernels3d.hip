@@ -16,12 +16,11 @@
 // the plane kernels' dense-lane 37-point pass (slice.hpp PK) with two output pairs per task:
 // 9 main waves + 3-4, 0-4 spilled VGPRs instead of 16-36 at three; C4 0.1845 -> 0.1823 s per
 // outer iteration, same box (profiles/r05/pfa_pack_q2_ab.txt)
-#ifndef CCSC_PFA74_QP
-#define CCSC_PFA74_QP 2
-#endif
 #include "slice.hpp"
 
 namespace ccsc {
+
+constexpr int kPlaneQP = 2;   // conjugate output pairs per 37-point task of the plane kernels
 
 // ---- plane forward: prologue -> 2D R2C -> dst[(slice*T + t)*F2 + f] --------
 // mode 0: embed src sub-volume [st][sy][sx] at offset (o, o, o) (zero padding)
@@ -97,7 +96,7 @@ void k_plane_fwd(int mode, const T* __restrict__ a,
     }
     zero_pad_row(S.slice, G);
   }
-  slice_r2c_rm<T, RM, true>(S.slice, G, S.tw);
+  slice_r2c_rm<T, RM, true, kPlaneQP>(S.slice, G, S.tw);
   if (tc > 0) {   // t-minor tiles (k_tsolve3's order)
     const int ntile = (GXh + tc - 1) / tc;
     cpx<T>* out = dst + slice * ((int64_t)GY * ntile * Tn * tc);
@@ -196,7 +195,7 @@ void k_plane_inv(int mode, const cpx<T>* src,
     const cpx<T>* in = src + (slice * Tn + t) * GF;
     for (int f = threadIdx.x; f < GF; f += kNT) lds_cpx_store(S.slice + Q::bin(f, G), 1, in[f]);
   }
-  slice_c2r_rm<T, RM, true>(S.slice, G, S.tw);
+  slice_c2r_rm<T, RM, true, kPlaneQP>(S.slice, G, S.tw);
   const int P = GX * GY;
   const int64_t off = (slice * Tn + t) * P;
   const bool nrm = (mode == 3 && norms) || (mode == 2 && slice < nfirst);
@@ -241,7 +240,7 @@ void k_plane_inv(int mode, const cpx<T>* src,
   }
   if (mode == 3 && nxt) {   // the next iteration's forward plane transform (k_plane_fwd mode 3)
     zero_pad_row(S.slice, G);
-    slice_r2c_rm<T, RM, true>(S.slice, G, S.tw);
+    slice_r2c_rm<T, RM, true, kPlaneQP>(S.slice, G, S.tw);
     if (tc > 0) {
       const int ntile = (GXh + tc - 1) / tc;
       cpx<T>* out = nxt + slice * ((int64_t)GY * ntile * Tn * tc);

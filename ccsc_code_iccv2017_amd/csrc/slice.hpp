@@ -101,22 +101,15 @@ struct SG {
 // the x passes read and write the line-minor layout (fpass LM): the forward one for the
 // split-to-half y pass, the inverse one, the last pass of the C2R, for the kernels' real
 // planes (SG<kRm74F>::px)
-// kPfaPre: the radix-2 passes store the prime pass's symmetric input pairs already formed
-// (fpass2_pairs, fft_pass_pfa<PRE>); 0 keeps the plain radix-2 pass (A/B builds)
-#ifndef CCSC_PFA_PRE
-#define CCSC_PFA_PRE 1
-#endif
-constexpr bool kPfaPre = CCSC_PFA_PRE != 0;
-#ifndef CCSC_PFA74_QP
-#define CCSC_PFA74_QP kPfaQP
-#endif
-// PK: the prime pass with dense lanes (fft_pass_pfa_packed; needs kPfaPre) -- the 3D plane
-// kernels (C4 0.1884 -> 0.1836 s per outer iteration); the 4D kernels keep the plain form
-// (C5 0.0157 -> 0.0159 with it, profiles/r05/pfa_pack_ab.txt).  CCSC_PFA_PACK=0 turns it off.
-#ifndef CCSC_PFA_PACK
-#define CCSC_PFA_PACK 1
-#endif
-constexpr bool kPfaPack = kPfaPre && CCSC_PFA_PACK != 0;
+// The radix-2 passes store the prime pass's symmetric input pairs already formed
+// (fpass2_pairs, fft_pass_pfa<PRE = true>; the plain radix-2 pass measured slower,
+// profiles/r05/pfa_pre_ab.txt).
+// PK (a template parameter of the slice transforms, chosen per kernel): the prime pass with
+// dense lanes (fft_pass_pfa_packed) -- the 3D plane kernels (C4 0.1884 -> 0.1836 s per outer
+// iteration); the 4D kernels keep the plain form (C5 0.0157 -> 0.0159 with it,
+// profiles/r05/pfa_pack_ab.txt).  QP: conjugate output pairs per prime-pass task (the 3D
+// plane kernels 2, the others kPfaQP).  Every choice is a template parameter, so one
+// mangled name never gets different bodies in different translation units.
 // the 37 roots of the packed pass's lane-varying tasks, one LDS copy per workgroup
 template <typename T>
 __device__ __forceinline__ cpx<T>* pfa74_roots() {
@@ -138,57 +131,52 @@ __device__ __forceinline__ void pfa74_fill_roots(int tid) {
     if (tid < kPfaM) pfa74_roots<T>()[tid] = {(T)tab[tid][0], (T)tab[tid][1]};
   }
 }
-template <typename T, int SIGN, bool PK>
+template <typename T, int SIGN, bool PK, int QP>
 __device__ __forceinline__ void pfa74(T* lds, bool xdir) {
   using FG = Grid74;
   constexpr LineGeom gy = {FG::Xh, 2, FG::RS, 1};
   constexpr LineGeom gxi = {FG::Yp / 2, 2, FG::Yp, 1};   // line-minor
   if constexpr (PK) {
     if (xdir)
-      fft_pass_pfa_packed<T, kPfaM, SIGN, CCSC_PFA74_QP, kNT, FG::Yp / 2>(lds, gxi, gxi,
-                                                                          pfa74_roots<T>());
+      fft_pass_pfa_packed<T, kPfaM, SIGN, QP, kNT, FG::Yp / 2>(lds, gxi, gxi, pfa74_roots<T>());
     else
-      fft_pass_pfa_packed<T, kPfaM, SIGN, CCSC_PFA74_QP, kNT, FG::Xh>(lds, gy, gy,
-                                                                      pfa74_roots<T>());
+      fft_pass_pfa_packed<T, kPfaM, SIGN, QP, kNT, FG::Xh>(lds, gy, gy, pfa74_roots<T>());
   } else {
-    if (xdir) fft_pass_pfa<T, kPfaM, SIGN, CCSC_PFA74_QP, kNT, kPfaPre>(lds, gxi, gxi);
-    else fft_pass_pfa<T, kPfaM, SIGN, CCSC_PFA74_QP, kNT, kPfaPre>(lds, gy, gy);
+    if (xdir) fft_pass_pfa<T, kPfaM, SIGN, QP, kNT, true>(lds, gxi, gxi);
+    else fft_pass_pfa<T, kPfaM, SIGN, QP, kNT, true>(lds, gy, gy);
   }
 }
 // the radix-2 pass of a 74-point direction ahead of pfa74
 template <typename T, bool XD, int SIGN, int MODE, int LM>
 __device__ __forceinline__ void rad2_74(T* lds, const cpx<T>* tw, int tid) {
-  if constexpr (kPfaPre) fpass2_pairs<T, Grid74, kNT, XD, MODE, LM>(lds, tid);
-  else fpass<T, Grid74, kNT, XD, 2, 1, SIGN, MODE, LM>(lds, tw, tid);
+  fpass2_pairs<T, Grid74, kNT, XD, MODE, LM>(lds, tid);
 }
 
 // slice_r2c / slice_c2r of instantiation RM (fft.hpp), the fixed passes on kRm74F
-template <typename T, int RM, bool PACK = false>
+template <typename T, int RM, bool PK = false, int QP = kPfaQP>
 __device__ __forceinline__ void slice_r2c_rm(T* lds, const Grid2D& G, const cpx<T>* tw) {
-  constexpr bool PK = PACK && kPfaPack;
   if constexpr (RM == kRm74F) {
     const int tid = threadIdx.x;
     pfa74_fill_roots<T, PK>(tid);
     lds_sync();
     rad2_74<T, true, -1, kModePlain, kLmIn | kLmOut>(lds, tw, tid);
-    pfa74<T, -1, PK>(lds, true);
+    pfa74<T, -1, PK, QP>(lds, true);
     rad2_74<T, false, -1, kModeSplitToHalf, kLmIn>(lds, tw, tid);
-    pfa74<T, -1, PK>(lds, false);
+    pfa74<T, -1, PK, QP>(lds, false);
   } else {
     slice_r2c<T, kMaxB, RM>(lds, G, tw);
   }
 }
-template <typename T, int RM, bool PACK = false>
+template <typename T, int RM, bool PK = false, int QP = kPfaQP>
 __device__ __forceinline__ void slice_c2r_rm(T* lds, const Grid2D& G, const cpx<T>* tw) {
-  constexpr bool PK = PACK && kPfaPack;
   if constexpr (RM == kRm74F) {
     const int tid = threadIdx.x;
     pfa74_fill_roots<T, PK>(tid);
     lds_sync();
     rad2_74<T, false, +1, kModePlain, 0>(lds, tw, tid);
-    pfa74<T, +1, PK>(lds, false);
+    pfa74<T, +1, PK, QP>(lds, false);
     rad2_74<T, true, +1, kModeHermPair, kLmOut>(lds, tw, tid);
-    pfa74<T, +1, PK>(lds, true);
+    pfa74<T, +1, PK, QP>(lds, true);
   } else {
     slice_c2r<T, kMaxB, RM>(lds, G, tw);
   }

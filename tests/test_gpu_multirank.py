@@ -21,17 +21,19 @@ def _free_port():
     return p
 
 
-def _case(variant):
+def _case(variant, big=False):
     rng = np.random.default_rng(99)
     ni, N, psf, K = 2, 3, 5, 3          # 3 blocks over 2 ranks: 2 + 1
-    b = rng.standard_normal((12, 11, ni * N))
+    # big: 150 x 149 patches (a 154 x 153 slice past one CU's LDS: the global-pass path)
+    sx, sy = (150, 149) if big else (12, 11)
+    b = rng.standard_normal((sx, sy, ni * N))
     d0 = rng.standard_normal((psf, psf, K))
-    X, Y = 16, 15
+    X, Y = sx + 4, sy + 4
     z0 = rng.standard_normal((X, Y, K, ni if variant == "dz" else ni * N))
     return b, d0, z0, ni, N, [psf, psf, K]
 
 
-def _worker(rank, world, port, out_dir, variant, tol):
+def _worker(rank, world, port, out_dir, variant, tol, big):
     import torch
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -46,7 +48,7 @@ def _worker(rank, world, port, out_dir, variant, tol):
         else:
             dist.broadcast(t, src=0)
 
-    b, d0, z0, ni, N, ks = _case(variant)
+    b, d0, z0, ni, N, ks = _case(variant, big)
     v = E.L.CCSC_DZPAR if variant == "dz" else E.L.CCSC_DPAR
     p = E.make_problem(v, b.shape, ks, 1.0, 1.0, 2, tol, "brief", ni=ni, trace_objective=True)
     ctx = E.Context(0, rank, world, host_comm=host_comm)
@@ -65,16 +67,21 @@ def _worker(rank, world, port, out_dir, variant, tol):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("variant,tol", [("dz", 0.0), ("dp", 1e-12)])
-def test_two_ranks_equal_one_rank(tmp_path, gpu_ctx, variant, tol):
+@pytest.mark.parametrize("variant,tol,big", [("dz", 0.0, False), ("dp", 1e-12, False),
+                                             # global-pass slices: the sharded
+                                             # support / d-norm / objective exchanges and the
+                                             # session's state handling on that path
+                                             ("dz", 0.0, True), ("dp", 1e-3, True)])
+def test_two_ranks_equal_one_rank(tmp_path, gpu_ctx, variant, tol, big):
+    """Session.step over two ranks (the bench's path) equals the oracle."""
     import torch.multiprocessing as mp
     from ccsc_code_iccv2017_amd import learners as E
     from oracle import ccsc_oracle as O
 
-    mp.start_processes(_worker, args=(2, _free_port(), str(tmp_path), variant, tol), nprocs=2,
-                       join=True, start_method="spawn")
+    mp.start_processes(_worker, args=(2, _free_port(), str(tmp_path), variant, tol, big),
+                       nprocs=2, join=True, start_method="spawn")
     parts = [np.load(tmp_path / f"{variant}_r{r}.npz") for r in range(2)]
-    b, d0, z0, ni, N, ks = _case(variant)
+    b, d0, z0, ni, N, ks = _case(variant, big)
     fn = O.learn_2d_dzparallel if variant == "dz" else O.learn_2d_dparallel
     d_o, z_o, DZ_o, it_o, tr_o = fn(b, ks, 1.0, 1.0, 2, tol, "brief", {"d": d0, "z": z0}, ni=ni,
                                     trace_objective=True)

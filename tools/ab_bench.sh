@@ -2,6 +2,7 @@
 # dir holds libccsc_<v>.so (push it un-ignored); n=1000 C2 slice (AB_N to change), per-kernel
 # times on stderr; every run's per-kernel line is appended to gpurun_out/ab/summary.txt
 set -o pipefail
+source tools/_libswap.sh
 d=$1; shift
 mkdir -p gpurun_out/ab
 for v in "$@"; do

@@ -4,6 +4,7 @@
 # (C1, C3, C4, C5, or $CONFIGS) and the n=1000 C2 slice of bench.py (per-kernel times on
 # stderr; skipped with SKIP_BENCH=1).
 set -o pipefail
+source tools/_libswap.sh
 d=$1; shift
 mkdir -p gpurun_out/ab
 for v in "$@"; do

@@ -2,6 +2,7 @@
 # run one pytest selection against several abv/ library variants: tools/gpu_var_test.sh <tag> <selection> v1 v2 ...
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+source tools/_libswap.sh
 tag=$1; sel=$2; shift 2
 mkdir -p gpurun_out/$tag
 for v in "$@"; do

@@ -4,6 +4,7 @@
 #   tools/gpu_zl_ab.sh <tag> <old> <new>
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+source tools/_libswap.sh
 tag=$1; old=$2; new=$3
 mkdir -p gpurun_out/$tag
 cp abx/libccsc_$new.so ccsc_code_iccv2017_amd/libccsc.so
@@ -15,4 +16,3 @@ for v in $old $new $old $new; do
   timeout -k 10 300 python bench.py --n ${AB_N:-1000} --steps 3 --warmup 1 --no-cpu-baseline --no-configs > gpurun_out/$tag/$v.json 2> gpurun_out/$tag/$v.err || exit 1
   echo "$v $(python -c "import json;d=json.load(open('gpurun_out/$tag/$v.json'));print(round(d['ms_per_step'],2), round(d['roofline']['avg_launch_ms'],3))") $(grep per-kernel gpurun_out/$tag/$v.err | cut -c1-300)" | tee -a gpurun_out/$tag/ab.txt
 done
-cp abx/libccsc_$new.so ccsc_code_iccv2017_amd/libccsc.so
