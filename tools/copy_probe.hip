@@ -1,9 +1,9 @@
 // Achievable HBM streaming rate on this GPU for bench.py's roofline line (VERDICT r05 weak 3:
 // torch's copy_ understated it): a hand-written copy with 16 B per lane, U independent 16-B
 // loads in flight per thread before their stores, a grid of whole rounds of workgroups on
-// every CU, in the plain and the nontemporal cache policy.  copy_probe() runs `reps` timed
-// copies of each form and returns the best (read + write bytes) / time in GB/s, the form in
-// *form (0 plain, 1 nontemporal).  Built by ccsc_code_iccv2017_amd/build.py into
+// every CU (or one pass over the buffer), in the plain and the nontemporal cache policy.
+// copy_probe() runs `reps` timed copies of each form and returns the best (read + write bytes)
+// / time in GB/s, the form in *form (bits: see below).  Built by ccsc_code_iccv2017_amd/build.py into
 // tools/libcopy_probe.so; the engine does not use it.
 #include <hip/hip_runtime.h>
 
@@ -42,17 +42,26 @@ extern "C" int copy_probe(const void* src, void* dst, int64_t bytes, int reps, d
   int dev = 0, ncu = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 2;
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 2;
-  const dim3 grid((unsigned)(ncu * 8)), block(256);   // 8 workgroups (32 waves) per CU
   hipEvent_t a, b;
   if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return 2;
   double best = 0;
   int best_form = 0;
-  for (int f = 0; f < 2; ++f) {
+  // form = policy (bit 0: nontemporal) | loads in flight (bit 1: 8, else 4) | workgroups per
+  // CU (bit 2: 16, else 8) | bit 3: one pass (a grid covering the buffer, no loop)
+  for (int f = 0; f < 16; ++f) {
+    const bool nt = f & 1, u8 = f & 2;
+    const int U = u8 ? 8 : 4;
+    const int64_t one_pass = (n + 256 * U - 1) / (256 * U);
+    if ((f & 8) && (f & 4)) continue;   // one pass: the grid size is the buffer's
+    if ((f & 8) && one_pass >= ((int64_t)1 << 31)) continue;
+    const dim3 grid((unsigned)((f & 8) ? one_pass : ncu * ((f & 4) ? 16 : 8))), block(256);
     auto go = [&] {
-      if (f == 0)
-        hipLaunchKernelGGL((k_copy<4, false>), grid, block, 0, 0, (const d2*)src, (d2*)dst, n);
-      else
-        hipLaunchKernelGGL((k_copy<4, true>), grid, block, 0, 0, (const d2*)src, (d2*)dst, n);
+      const d2* s_ = (const d2*)src;
+      d2* d_ = (d2*)dst;
+      if (nt && u8) hipLaunchKernelGGL((k_copy<8, true>), grid, block, 0, 0, s_, d_, n);
+      else if (nt) hipLaunchKernelGGL((k_copy<4, true>), grid, block, 0, 0, s_, d_, n);
+      else if (u8) hipLaunchKernelGGL((k_copy<8, false>), grid, block, 0, 0, s_, d_, n);
+      else hipLaunchKernelGGL((k_copy<4, false>), grid, block, 0, 0, s_, d_, n);
     };
     go();   // warm-up
     std::vector<float> ts;
