@@ -82,10 +82,13 @@ if __name__ == "__main__":
     ap.add_argument("--c4", action="store_true")
     ap.add_argument("--c3", action="store_true")
     ap.add_argument("--json", help="write the results (a test fixture) here")
+    ap.add_argument("--sb", help="C4 clip size, e.g. 44,44,22 (default 24,24,12)")
+    ap.add_argument("--n", type=int, default=16, help="C4 clips (a perfect square)")
     a = ap.parse_args()
     res = []
     if a.c4 or not a.c3:
-        res.append(c4())
+        sb = tuple(int(x) for x in a.sb.split(",")) if a.sb else (24, 24, 12)
+        res.append(c4(n=a.n, sb=sb))
     if a.c3 or not a.c4:
         res.append(c3())
     if a.json:
