@@ -366,9 +366,10 @@ static void check_supported(const ccsc_problem& p, Geom* Gout) {
   if (Gout) *Gout = g;
 }
 
+// (the 2-3D learner has one block of all n images, L23: its shards are runs of images)
 static void shard(const ccsc_problem& p, int rank, int nranks, int64_t& b0, int64_t& nb) {
   if (nranks <= 0 || rank < 0 || rank >= nranks) throw Err(CCSC_E_INVALID, "bad rank/nranks");
-  const int64_t N = p.n / p.ni;
+  const int64_t N = p.variant == CCSC_HS23 ? p.n : p.n / p.ni;
   if (N < nranks) throw Err(CCSC_E_INVALID, "fewer blocks than ranks");
   const int64_t base = N / nranks, rem = N % nranks;
   nb = base + (rank < rem ? 1 : 0);
@@ -509,6 +510,47 @@ static void init_group_comms(std::vector<ncclComm_t>& comms, const int32_t* devi
 // ---------------------------------------------------------------------------
 // Session: 2D consensus learners (dP / dZ)
 // ---------------------------------------------------------------------------
+// ---- collectives of a rank context ------------------------------------------
+// The transport is chosen by what the context was created with (a host callback or
+// an RCCL communicator), never by a communicator pointer an abort may have cleared;
+// in a multi-device group every collective first checks that no rank has failed.
+static void host_exchange(ccsc_ctx* ctx, hipStream_t st, int op, double* buf, size_t count) {
+  ctx->stage.resize(count);
+  HIPCHK(hipMemcpyAsync(ctx->stage.data(), buf, count * 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if (ctx->hostfn(ctx->hostuser, op, ctx->stage.data(), (int64_t)count) != 0)
+    throw Err(CCSC_E_RCCL, "host communicator callback failed");
+  HIPCHK(hipMemcpyAsync(buf, ctx->stage.data(), count * 8, hipMemcpyHostToDevice, st));
+  HIPCHK(hipStreamSynchronize(st));
+}
+static void ctx_collective(ccsc_ctx* ctx, hipStream_t st, int op, double* buf, size_t count) {
+  if (ctx->nranks <= 1 && !ctx->rccl_self) return;
+  if (ctx->hostfn) {   // the exchange itself returns an error once the group aborted
+    host_exchange(ctx, st, op, buf, count);
+    return;
+  }
+  CommGroup* g = ctx->grp.get();
+  if (g) g->inflight.fetch_add(1);
+  struct Leave {
+    CommGroup* g;
+    ~Leave() {
+      if (g) g->inflight.fetch_sub(1);
+    }
+  } leave{g};
+  if (g && g->aborted.load())
+    throw Err(CCSC_E_RCCL, "host communicator aborted: another rank of this context failed");
+  if (!ctx->comm) throw Err(CCSC_E_STATE, "multi-rank context without a communicator");
+  const ncclResult_t r = op == CCSC_COMM_ALLREDUCE_SUM
+                             ? ncclAllReduce(buf, buf, count, ncclDouble, ncclSum, ctx->comm, st)
+                             : ncclBroadcast(buf, buf, count, ncclDouble, 0, ctx->comm, st);
+  // a device-list group's communicators are non-blocking (init_group_comms): the enqueue
+  // may still be connecting; wait for it here, giving up once the group aborted, so no
+  // rank stays inside RCCL on a communicator abort_group is about to abort
+  if (r == ncclInProgress) wait_comm(ctx->comm, g ? &g->aborted : nullptr);
+  else if (r != ncclSuccess)
+    throw Err(CCSC_E_RCCL, std::string("RCCL collective failed: ") + ncclGetErrorString(r));
+}
+
 // Session of every consensus learner: dP, dZ, the 4D light-field learner (2D
 // spatial convolution, NV = U*V views share the codes, L4:18-21) and the 3D
 // learner (Tn > 1: plane transforms + t-direction FFT, L3).
@@ -876,55 +918,9 @@ struct Session2D {
     }
   }
 
-  // ---- collectives ----------------------------------------------------------
-  void host_exchange(int op, double* buf, size_t count) {
-    ctx->stage.resize(count);
-    HIPCHK(hipMemcpyAsync(ctx->stage.data(), buf, count * 8, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    if (ctx->hostfn(ctx->hostuser, op, ctx->stage.data(), (int64_t)count) != 0)
-      throw Err(CCSC_E_RCCL, "host communicator callback failed");
-    HIPCHK(hipMemcpyAsync(buf, ctx->stage.data(), count * 8, hipMemcpyHostToDevice, st));
-    HIPCHK(hipStreamSynchronize(st));
-  }
-  // The transport is chosen by what the context was created with (a host callback or
-  // an RCCL communicator), never by a communicator pointer an abort may have cleared;
-  // in a multi-device group every collective first checks that no rank has failed.
-  template <typename Fn>
-  void collective(int op, double* buf, size_t count, Fn&& rccl) {
-    if (ctx->nranks <= 1 && !ctx->rccl_self) return;
-    if (ctx->hostfn) {   // the exchange itself returns an error once the group aborted
-      host_exchange(op, buf, count);
-      return;
-    }
-    CommGroup* g = ctx->grp.get();
-    if (g) g->inflight.fetch_add(1);
-    struct Leave {
-      CommGroup* g;
-      ~Leave() {
-        if (g) g->inflight.fetch_sub(1);
-      }
-    } leave{g};
-    if (g && g->aborted.load())
-      throw Err(CCSC_E_RCCL, "host communicator aborted: another rank of this context failed");
-    if (!ctx->comm) throw Err(CCSC_E_STATE, "multi-rank context without a communicator");
-    const ncclResult_t r = rccl();
-    // a device-list group's communicators are non-blocking (init_group_comms): the enqueue
-    // may still be connecting; wait for it here, giving up once the group aborted, so no
-    // rank stays inside RCCL on a communicator abort_group is about to abort
-    if (r == ncclInProgress) wait_comm(ctx->comm, g ? &g->aborted : nullptr);
-    else if (r != ncclSuccess)
-      throw Err(CCSC_E_RCCL, std::string("RCCL collective failed: ") + ncclGetErrorString(r));
-  }
-  void allreduce(double* buf, size_t count) {
-    collective(CCSC_COMM_ALLREDUCE_SUM, buf, count, [&] {
-      return ncclAllReduce(buf, buf, count, ncclDouble, ncclSum, ctx->comm, st);
-    });
-  }
-  void bcast0(double* buf, size_t count) {
-    collective(CCSC_COMM_BCAST0, buf, count, [&] {
-      return ncclBroadcast(buf, buf, count, ncclDouble, 0, ctx->comm, st);
-    });
-  }
+  // ---- collectives (ctx_collective) -------------------------------------------
+  void allreduce(double* buf, size_t count) { ctx_collective(ctx, st, CCSC_COMM_ALLREDUCE_SUM, buf, count); }
+  void bcast0(double* buf, size_t count) { ctx_collective(ctx, st, CCSC_COMM_BCAST0, buf, count); }
   void pair_to_host(double* out2) {
     HIPCHK(hipMemcpyAsync(out2, pair.p, 2 * sizeof(double), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
@@ -1681,9 +1677,10 @@ struct PlanHS {
   }
 };
 
-static PlanHS plan_hs(const ccsc_problem& p, const Geom& g) {
+// n_local: the rank's images (shard(); the whole problem on one rank)
+static PlanHS plan_hs(const ccsc_problem& p, const Geom& g, int64_t n_local, bool dist) {
   PlanHS m{};
-  const size_t P = g.P(), F = g.F(), K = p.K, W = p.views[0], n = p.n;
+  const size_t P = g.P(), F = g.F(), K = p.K, W = p.views[0], n = (size_t)n_local;
   const size_t SS = (size_t)p.psf * p.psf;
   m.b = (size_t)p.sb[0] * p.sb[1] * W * n * 8;
   m.vwn = P * W * n * 8;
@@ -1700,8 +1697,9 @@ static PlanHS plan_hs(const ccsc_problem& p, const Geom& g) {
            (size_t)g.G.ntw * 16 + (g.gp ? 64 * 1024 : 0);
   // global-pass slices: the real scratch of the largest transform batch
   m.gr = g.gp ? std::max({W * n, K * n, W * K}) * P * 8 : 0;
-  // K > 192: the n x n Woodbury factor (wbig.hip) and its frequency-major workspace
-  m.wx = K > 192 ? m.Zh : 0;
+  // K > 192: the n x n Woodbury factor (wbig.hip) and its frequency-major workspace; several
+  // ranks: the same workspace for the per-rank Gram (gramchol_big.hip, summed over the ranks)
+  m.wx = (K > 192 || dist) ? m.Zh : 0;
   return m;
 }
 
@@ -1733,6 +1731,13 @@ struct SessionHS {
   // K > 192: the reference's own n x n Woodbury form of opt_f (L23:290; wbig.hip)
   bool hs_wbig = false;
   DevBuf Xw;
+  // several ranks (one process per GPU, images sharded in contiguous runs, shard()): the
+  // d-solve couples every image per frequency (L23:289-295), so each rank forms the Gram of
+  // its images (gramchol_big.hip, rho on rank 0 only) and the right-hand sides Z^H xi1 of its
+  // images, both are summed over the ranks (allreduce), and every rank factors and solves the
+  // same system; the objective's sums, the z change norms and max(b) (L23:36) are reduced too
+  bool dist = false;
+  int64_t i0 = 0;   // first image of this rank
   double obj = std::numeric_limits<double>::quiet_NaN();
   double obj_filter = obj, obj_z = obj;
   std::vector<double> v_obj_d, v_obj_z, v_tim, tr_od, tr_oz, tr_dd, tr_zd;
@@ -1744,9 +1749,12 @@ struct SessionHS {
     resolve_problem(p);
     if (p.variant != CCSC_HS23) throw Err(CCSC_E_INVALID, "SessionHS runs the 2-3D learner only");
     check_supported(p, &g);
-    if (ctx->nranks != 1)
-      throw Err(CCSC_E_UNSUPPORTED, "the 2-3D learner runs on one rank (its d-solve sums over "
-                                    "every image per frequency; SURVEY.md 8e: replicas only)");
+    dist = ctx->nranks > 1 || ctx->rccl_self;
+    if (dist && p.K > 192)
+      throw Err(CCSC_E_UNSUPPORTED, "the 2-3D learner past K = 192 (the n x n Woodbury factor "
+                                    "couples every image) runs on one rank");
+    int64_t nloc = p.n;
+    shard(p, ctx->rank, ctx->nranks, i0, nloc);
     {
       const char* et = std::getenv("CCSC_DS_TILE");
       hs_dtile = dsolve_tile_ok(p.K, p.views[0]) && !(et && et[0] == '0');
@@ -1756,7 +1764,7 @@ struct SessionHS {
     if (!b || !smooth_init) throw Err(CCSC_E_INVALID, "b and smooth_init must not be NULL");
     G = g.G;
     gp = g.gp;
-    m = plan_hs(p, g);
+    m = plan_hs(p, g, nloc, dist);
     r = p.psf / 2;
     s = p.psf;
     SS = s * s;
@@ -1767,7 +1775,7 @@ struct SessionHS {
     F = G.F;
     sbx = (int)p.sb[0];
     sby = (int)p.sb[1];
-    n = (int)p.n;
+    n = (int)nloc;   // this rank's images
     if (r > sbx || r > sby)
       throw Err(CCSC_E_UNSUPPORTED, "symmetric padding wider than the image (L23:19)");
 
@@ -1832,6 +1840,17 @@ struct SessionHS {
     double bmax = 0;
     HIPCHK(hipMemcpyAsync(&bmax, pair.p, sizeof(double), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
+    if (dist) {   // max over the ranks through the sum collective: one slot per rank
+      std::vector<double> mx((size_t)ctx->nranks, 0.0);
+      mx[(size_t)ctx->rank] = bmax;
+      DevBuf rm;
+      rm.alloc(mx.size() * 8);
+      HIPCHK(hipMemcpy(rm.p, mx.data(), rm.bytes, hipMemcpyHostToDevice));
+      ctx_collective(ctx, st, CCSC_COMM_ALLREDUCE_SUM, rm.as<double>(), mx.size());
+      HIPCHK(hipMemcpyAsync(mx.data(), rm.p, rm.bytes, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      bmax = *std::max_element(mx.begin(), mx.end());
+    }
     if (!(bmax > 0)) throw Err(CCSC_E_INVALID, "max(b(:)) must be positive (L23:36)");
     gamma_h = 60.0 * p.lambda_prior / bmax;
     const double gD1 = gamma_h / p.rho_d;                // gammas_D = [gh/5000, gh]  (L23:37)
@@ -1994,6 +2013,8 @@ struct SessionHS {
   double finish_objective() {
     c2r_v(nullptr);
     HIPCHK(launch_sum_pairs<double>(part.as<double>(), W * n, pair.as<double>(), st));
+    // the data term and sum |z| over every rank's images
+    if (dist) ctx_collective(ctx, st, CCSC_COMM_ALLREDUCE_SUM, pair.as<double>(), 4);
     double h4[4];
     HIPCHK(hipMemcpyAsync(h4, pair.p, sizeof h4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
@@ -2008,9 +2029,11 @@ struct SessionHS {
                                    Xi.as<cpx<double>>(), F, W, K, n, st));
     return finish_objective();
   }
-  double rel_change(const DevBuf& a, const DevBuf& b) {
+  // global: a and b are rank-local (z; D is the same on every rank)
+  double rel_change(const DevBuf& a, const DevBuf& b, bool global = false) {
     HIPCHK(launch_norms<double>(a.as<double>(), b.as<double>(), (int64_t)a.bytes / 8,
                                 part.as<double>(), pair.as<double>() + 4, st));
+    if (global && dist) ctx_collective(ctx, st, CCSC_COMM_ALLREDUCE_SUM, pair.as<double>() + 4, 2);
     double h2[2];
     HIPCHK(hipMemcpyAsync(h2, pair.as<double>() + 4, sizeof h2, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
@@ -2037,10 +2060,19 @@ struct SessionHS {
     objective_fresh();
     // opt_f = (Z_f' Z_f + rho I)^-1 as a Cholesky factor per bin (L23:290)
     // on the matrix cores (gramchol.hip, K <= 192; no right-hand side here: NV = 0)
-    if (hs_wbig)
+    if (hs_wbig) {
       HIPCHK(launch_wbig_gram(Zh.as<cpx<double>>(), Zh.as<cpx<double>>(), Xw.as<cpx<double>>(),
                               L.as<cpx<double>>(), h.as<cpx<double>>(), F, K, n, p.rho_d, 0, st));
-    else
+    } else if (dist) {
+      // the Gram of this rank's images (rho I on rank 0 only), summed over the ranks, then
+      // the same Cholesky on every rank
+      HIPCHK(launch_gram_big(Zh.as<cpx<double>>(), Zh.as<cpx<double>>(), Xw.as<cpx<double>>(),
+                             L.as<cpx<double>>(), h.as<cpx<double>>(), F, K, n,
+                             ctx->rank == 0 ? p.rho_d : 0.0, 0, st, false));
+      ctx_collective(ctx, st, CCSC_COMM_ALLREDUCE_SUM, L.as<double>(),
+                     (size_t)2 * F * (K * (K + 1) / 2));
+      HIPCHK(launch_chol_big(L.as<cpx<double>>(), F, K, st));
+    } else
       HIPCHK(launch_gram_chol_mf(Zh.as<cpx<double>>(), Zh.as<cpx<double>>(), L.as<cpx<double>>(),
                                  h.as<cpx<double>>(), F, K, n, p.rho_d, 0, st));
     // 64 < K <= 112: the tile d-solve over the W wavelengths (factor read once per solve)
@@ -2053,6 +2085,7 @@ struct SessionHS {
       // d_hat = opt (Z' xi1 + rho xi2) per (bin, wavelength)  (L23:125, 289-295)
       HIPCHK(launch_hs_corr<double>(Zh.as<cpx<double>>(), Xi.as<cpx<double>>(),
                                     h.as<cpx<double>>(), F, W, K, n, st));
+      if (dist) ctx_collective(ctx, st, CCSC_COMM_ALLREDUCE_SUM, h.as<double>(), (size_t)2 * F * W * K);
       if (hs_wbig)
         HIPCHK(launch_wbig_solve(L.as<cpx<double>>(), h.as<cpx<double>>(), Ch.as<cpx<double>>(),
                                  Dh.as<cpx<double>>(), 1, F, K, n, p.rho_d, W, st));
@@ -2106,7 +2139,7 @@ struct SessionHS {
       finished = true;
       flags |= 1;
     } else {
-      const double z_diff = rel_change(z, zold);                                 // L23:216-220
+      const double z_diff = rel_change(z, zold, true);                           // L23:216-220
       tr_zd[(size_t)it * p.max_it_z] = z_diff;
       if (z_diff < p.tol && d_diff < p.tol) finished = true;                     // L23:223
     }
@@ -2374,8 +2407,9 @@ int32_t ccsc_plan_bytes(const ccsc_problem* p, int32_t rank, int32_t nranks, uin
     Geom g;
     check_supported(q, &g);
     if (q.variant == CCSC_HS23) {
-      if (nranks != 1) throw Err(CCSC_E_UNSUPPORTED, "the 2-3D learner runs on one rank");
-      *bytes = plan_hs(q, g).total();
+      int64_t i0 = 0, nl = 0;
+      shard(q, rank, nranks, i0, nl);
+      *bytes = plan_hs(q, g, nl, nranks > 1).total();
     } else {
       *bytes = plan2d(q, g, rank, nranks).total();
     }
@@ -2564,7 +2598,8 @@ ccsc_session* ccsc_session_create_hs23(ccsc_ctx* ctx, const ccsc_problem* p, con
   guarded(err, errlen, [&] {
     if (!ctx || !p) throw Err(CCSC_E_INVALID, "NULL ctx/problem");
     if (!ctx->subs.empty())
-      throw Err(CCSC_E_UNSUPPORTED, "the 2-3D learner runs on one device");
+      throw Err(CCSC_E_UNSUPPORTED, "the 2-3D learner runs one process per GPU (a rank context of "
+                                    "ccsc_create / ccsc_create_hostcomm), not on a device list");
     HIPCHK(hipSetDevice(ctx->device));
     std::unique_ptr<ccsc_session> s(new ccsc_session());
     s->hs.reset(new SessionHS(ctx, *p, b, smooth_init, d0, z0));
@@ -2647,8 +2682,8 @@ int32_t ccsc_learn_hs23(ccsc_ctx* ctx, const ccsc_problem* p, const double* b,
   return guarded(err, errlen, [&] {
     if (!ctx || !p) throw Err(CCSC_E_INVALID, "NULL ctx/problem");
     if (!ctx->subs.empty())
-      throw Err(CCSC_E_UNSUPPORTED, "the 2-3D learner runs on one device (its d-solve couples "
-                                    "every image per frequency)");
+      throw Err(CCSC_E_UNSUPPORTED, "the 2-3D learner runs one process per GPU (a rank context of "
+                                    "ccsc_create / ccsc_create_hostcomm), not on a device list");
     HIPCHK(hipSetDevice(ctx->device));
     SessionHS S(ctx, *p, b, smooth_init, d0, z0);
     S.ensure_trace_capacity(S.p.max_it);

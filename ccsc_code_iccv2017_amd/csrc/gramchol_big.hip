@@ -207,7 +207,7 @@ bool gram_big_ok(int K, int NV) { return K > 0 && K <= 16 * kBgMaxT && K * NV <=
 
 hipError_t launch_gram_big(const cpx<double>* Zh, const cpx<double>* Bh, cpx<double>* X,
                            cpx<double>* L, cpx<double>* h, int F, int K, int ni, double rho, int NV,
-                           hipStream_t st) {
+                           hipStream_t st, bool factor) {
   if (!gram_big_ok(K, NV)) return hipErrorInvalidValue;
   const int R = ni * K;
   hipLaunchKernelGGL(k_zh_fmajor, dim3((F + 63) / 64, (R + 63) / 64), dim3(256), 0, st, Zh, X, R, F);
@@ -215,6 +215,12 @@ hipError_t launch_gram_big(const cpx<double>* Zh, const cpx<double>* Bh, cpx<dou
   // (J, f): the T workgroups of one frequency are dispatched together, so its slab of
   // code spectra is read from HBM once and re-read from L2
   hipLaunchKernelGGL(k_gram_big, dim3(T * F), dim3(256), 0, st, X, Bh, L, h, F, K, ni, rho, NV);
+  if (factor) hipLaunchKernelGGL(k_chol_big, dim3(F), dim3(kBgCholNT), 0, st, L, F, K);
+  return hipGetLastError();
+}
+
+hipError_t launch_chol_big(cpx<double>* L, int F, int K, hipStream_t st) {
+  if (!gram_big_ok(K, 0)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_chol_big, dim3(F), dim3(kBgCholNT), 0, st, L, F, K);
   return hipGetLastError();
 }

@@ -130,7 +130,10 @@ hipError_t launch_wbig_solve(const cpx<double>* L, const cpx<double>* h, const c
                              hipStream_t st);
 hipError_t launch_gram_big(const cpx<double>* Zh, const cpx<double>* Bh, cpx<double>* X,
                            cpx<double>* L, cpx<double>* h, int F, int K, int ni, double rho, int NV,
-                           hipStream_t st);
+                           hipStream_t st, bool factor = true);
+// the Cholesky of launch_gram_big alone, in place on packed lower Grams (factor = false above,
+// e.g. after a sum of per-rank Grams)
+hipError_t launch_chol_big(cpx<double>* L, int F, int K, hipStream_t st);
 // x_{f,uv} = (L L^H)^{-1} (h_{f,uv} + rho * C_{f,uv}) for every (block, f, view);
 // C and Dh are [blk][K][NV][F].
 template <typename T>

@@ -228,7 +228,8 @@ class Session:
             raise L.CCSCError(L.CCSC_E_INVALID, eb.value.decode(errors="replace"))
         b0, nb = shard(self.p, ctx.rank, ctx.nranks)
         self.block_begin, self.nblocks = b0, nb
-        self.n_local = nb * self.p.ni
+        # (the 2-3D learner's shards are runs of images: ccsc_shard counts images for it)
+        self.n_local = nb if self.p.variant == L.CCSC_HS23 else nb * self.p.ni
         self.outer = 0
 
     def step(self, n_outer: int = 1) -> bool:

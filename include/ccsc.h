@@ -151,7 +151,10 @@ int32_t ccsc_resolve(ccsc_problem* p, char* err, size_t errlen);
 /* CCSC_OK if this build runs the (valid) problem on the GPU engine, else
  * CCSC_E_UNSUPPORTED with the reason (grid radices, LDS budget, K, variant). */
 int32_t ccsc_supported(const ccsc_problem* p, char* err, size_t errlen);
-/* Blocks [*block_begin, *block_begin + *block_count) of ni patches go to `rank`. */
+/* Blocks [*block_begin, *block_begin + *block_count) of ni patches go to `rank`.  The 2-3D
+ * learner (one block of all n images, L23) shards single images: its "blocks" are images; on
+ * several ranks each passes its images' b / smooth_init / z0 with the global n in the problem,
+ * and every rank holds the same filters (the Gram Z'Z and Z'xi1 are summed over the ranks). */
 int32_t ccsc_shard(const ccsc_problem* p, int32_t rank, int32_t nranks,
                    int64_t* block_begin, int64_t* block_count, char* err, size_t errlen);
 /* Device bytes one rank needs for this problem. */

@@ -263,3 +263,81 @@ def test_distinct_devices_over_rccl_equal_one_device(gpu_ctx):
         np.testing.assert_allclose(d3, d1, rtol=0, atol=1e-10 * np.abs(d1).max())
     finally:
         mctx.close()
+
+
+def _hs_case():
+    rng = np.random.default_rng(77)
+    sb, W, psf, K, n = (12, 11), 3, 5, 4, 5      # 5 images over 2 ranks: 3 + 2
+    r = psf // 2
+    b = rng.random(sb + (W, n))
+    sm = 0.5 * rng.random(sb + (W, n))
+    init = {"d": rng.standard_normal((psf, psf, K)),
+            "z": rng.standard_normal((sb[0] + 2 * r, sb[1] + 2 * r, K, n))}
+    return b, sm, init, [psf, psf, W, K]
+
+
+def _hs_worker(rank, world, port, out_dir, K):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from ccsc_code_iccv2017_amd import learners as E
+
+    def host_comm(op, arr):
+        t = torch.from_numpy(arr)
+        if op == 0:
+            dist.all_reduce(t)
+        else:
+            dist.broadcast(t, src=0)
+
+    b, sm, init, ks = _hs_case()
+    ks = ks[:3] + [K]
+    d0 = init["d"] if K == 4 else np.random.default_rng(5).standard_normal((ks[0], ks[1], K))
+    z0 = init["z"] if K == 4 else np.random.default_rng(6).standard_normal(init["z"].shape[:2] + (K, b.shape[-1]))
+    p = E.make_problem(E.L.CCSC_HS23, b.shape, ks, 1.0, 0.2, 3, 0.0, "brief")
+    ctx = E.Context(0, rank, world, host_comm=host_comm)
+    i0, ni = E.shard(E.resolve(p), rank, world)
+    s = E.Session(ctx, p, b[..., i0:i0 + ni], d0, z0[..., i0:i0 + ni], smooth_init=sm[..., i0:i0 + ni])
+    done = False
+    while s.outer < 3 and not done:
+        done = s.step(1)
+    d_res, z_res, DZ, obj = s.results(want_obj=True)
+    it = s.iterlog()
+    np.savez(os.path.join(out_dir, f"hs_r{rank}.npz"), d=d_res, z=z_res, DZ=DZ, obj=obj,
+             oz=it["trace"]["obj_z"], od=it["trace"]["obj_d"], i0=i0, ni=ni)
+    s.close()
+    ctx.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("K", [4, 100])
+def test_hs23_two_ranks_equal_oracle(tmp_path, gpu_ctx, K):
+    """The 2-3D learner over two ranks (VERDICT r05 missing item 5; L23's d-solve couples every
+    image per frequency, admm_learn.m:289-295): images sharded 3 + 2, each rank's Gram (on the
+    matrix cores, gramchol_big.hip) and right-hand sides Z^H xi1 summed over the ranks, the
+    objective's sums and max(b) reduced -- equals the oracle on the whole problem."""
+    import torch.multiprocessing as mp
+    from oracle import ccsc_oracle as O
+
+    mp.start_processes(_hs_worker, args=(2, _free_port(), str(tmp_path), K), nprocs=2, join=True,
+                       start_method="spawn")
+    parts = [np.load(tmp_path / f"hs_r{r}.npz") for r in range(2)]
+    b, sm, init, ks = _hs_case()
+    ks = ks[:3] + [K]
+    if K != 4:
+        init = {"d": np.random.default_rng(5).standard_normal((ks[0], ks[1], K)),
+                "z": np.random.default_rng(6).standard_normal(init["z"].shape[:2] + (K, b.shape[-1]))}
+    d_o, z_o, Dz_o, obj_o, tr_o = O.learn_hs23(b, ks, 1.0, 0.2, 3, 0.0, "brief", init, sm)
+    assert [int(q["ni"]) for q in parts] == [3, 2]
+    z = np.concatenate([q["z"] for q in parts], axis=3)
+    Dz = np.concatenate([q["DZ"] for q in parts], axis=3)
+    for q in parts:
+        np.testing.assert_allclose(q["d"], d_o, rtol=0, atol=1e-8 * np.abs(d_o).max())
+        assert abs(float(q["obj"]) - obj_o) <= 1e-9 * abs(obj_o)
+        for i in range(tr_o["outer"]):
+            np.testing.assert_allclose(q["oz"][i], tr_o["obj_z"][i], rtol=1e-9)
+            np.testing.assert_allclose(q["od"][i], tr_o["obj_d"][i], rtol=1e-9)
+    np.testing.assert_allclose(z, z_o, rtol=0, atol=1e-8 * np.abs(z_o).max())
+    np.testing.assert_allclose(Dz, Dz_o, rtol=0, atol=1e-8 * np.abs(Dz_o).max())
