@@ -1822,7 +1822,7 @@ struct SessionHS {
     dnorm.alloc((size_t)2 * KG * 8);
     part.alloc((size_t)2 * std::max<int64_t>(std::max<int64_t>((int64_t)W * n, (int64_t)K * n),
                                              kNormParts) * 8);
-    pair.alloc(8 * 8);
+    pair.alloc(12 * 8);
 
     // data: b and smoothinit = padarray(smooth_init, [r r 0 0], 'symmetric') (L23:19)
     HIPCHK(hipMemcpy(bdev.p, b, m.b, hipMemcpyHostToDevice));
@@ -2013,10 +2013,16 @@ struct SessionHS {
   double finish_objective() {
     c2r_v(nullptr);
     HIPCHK(launch_sum_pairs<double>(part.as<double>(), W * n, pair.as<double>(), st));
-    // the data term and sum |z| over every rank's images
-    if (dist) ctx_collective(ctx, st, CCSC_COMM_ALLREDUCE_SUM, pair.as<double>(), 4);
+    // the data term and sum |z| over every rank's images, reduced in a copy: pair[2] (this
+    // rank's sum |z|) serves every objective of a d-phase
+    const double* ps = pair.as<double>();
+    if (dist) {
+      HIPCHK(hipMemcpyAsync(pair.as<double>() + 8, ps, 4 * sizeof(double), hipMemcpyDeviceToDevice, st));
+      ctx_collective(ctx, st, CCSC_COMM_ALLREDUCE_SUM, pair.as<double>() + 8, 4);
+      ps = pair.as<double>() + 8;
+    }
     double h4[4];
-    HIPCHK(hipMemcpyAsync(h4, pair.p, sizeof h4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(h4, ps, sizeof h4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     return p.lambda_residual * 0.5 * h4[0] + p.lambda_prior * W * h4[2];   // g_z: z repeated W times (L23:332,338)
   }
