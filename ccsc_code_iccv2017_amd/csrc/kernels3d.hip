@@ -45,6 +45,33 @@ __device__ __forceinline__ int64_t plane_of_block(int64_t nplanes) {
 }
 __host__ inline unsigned plane_grid(int64_t nplanes) { return (unsigned)(((nplanes + 7) / 8) * 8); }
 
+// A kNT-strided loop over n elements whose global loads are issued B at a time before any is
+// used: one memory round trip per batch instead of per element.  (As plain loops, every
+// iteration waited vmcnt(0) for its own load: the plane kernels' spectrum and state loops made
+// 3 and 6 dependent HBM round trips per plane and thread -- the plane kernels' waves were
+// parked 67% of their lifetime, profiles/r06/c4_pmc.)  ld(e) loads, use(e, v) consumes.
+template <int B, typename Ld, typename Use>
+__device__ __forceinline__ void batched_loop(int n, Ld&& ld, Use&& use) {
+  using V = decltype(ld(0));
+  for (int base = threadIdx.x; base < n; base += B * kNT) {
+    V v[B];
+#pragma unroll
+    for (int i = 0; i < B; ++i) {
+      const int e = base + i * kNT;
+      if (e < n) v[i] = ld(e);
+    }
+#pragma unroll
+    for (int i = 0; i < B; ++i) {
+      const int e = base + i * kNT;
+      if (e < n) use(e, v[i]);
+    }
+  }
+}
+template <typename T>
+struct Pair2 {
+  T a, b;
+};
+
 template <typename T, int RM>
 __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(slice_waves<RM>())))
 void k_plane_fwd(int mode, const T* __restrict__ a,
@@ -79,20 +106,24 @@ void k_plane_fwd(int mode, const T* __restrict__ a,
     const int64_t off = (slice * Tn + t) * P;
     const int st3 = (t + r) % Tn;
     const T* u = usup + (int64_t)(slice % KG) * s * s * s;
-    for (int e = threadIdx.x; e < P; e += kNT) {
-      const int y = e / GX, x = e - y * GX;
-      T c;
-      if (mode == 3) {   // the z-step (L3:168-172) on the state a = z + y
-        const T q = b[off + e];
-        c = fma((T)-2, fmax(-theta, fmin(q, theta)), q);
-      } else {
-        const int sxx = (x + r) % GX, syy = (y + r) % GY;
-        const T uv = (sxx < s && syy < s && st3 < s) ? u[(st3 * s + syy) * s + sxx] : (T)0;
-        const T yn = b[off + e] + a[off + e] - uv;
-        b[off + e] = yn;
-        c = uv - yn;
-      }
-      S.slice[Q::px(x, y, G)] = c;
+    if (mode == 3) {   // the z-step (L3:168-172) on the state a = z + y
+      batched_loop<3>(
+          P, [&](int e) { return b[off + e]; },
+          [&](int e, T q) {
+            const int y = e / GX, x = e - y * GX;
+            S.slice[Q::px(x, y, G)] = fma((T)-2, fmax(-theta, fmin(q, theta)), q);
+          });
+    } else {
+      batched_loop<3>(
+          P, [&](int e) { return Pair2<T>{b[off + e], a[off + e]}; },
+          [&](int e, Pair2<T> ba) {
+            const int y = e / GX, x = e - y * GX;
+            const int sxx = (x + r) % GX, syy = (y + r) % GY;
+            const T uv = (sxx < s && syy < s && st3 < s) ? u[(st3 * s + syy) * s + sxx] : (T)0;
+            const T yn = ba.a + ba.b - uv;
+            b[off + e] = yn;
+            S.slice[Q::px(x, y, G)] = uv - yn;
+          });
     }
     zero_pad_row(S.slice, G);
   }
@@ -189,35 +220,42 @@ void k_plane_inv(int mode, const cpx<T>* src,
   if (tc > 0) {   // t-minor tiles (k_tsolve3's order)
     const int ntile = (GXh + tc - 1) / tc;
     const cpx<T>* in = src + slice * ((int64_t)GY * ntile * Tn * tc);
-    for (int f = threadIdx.x; f < GF; f += kNT)
-      lds_cpx_store(S.slice + Q::bin(f, G), 1, in[ttile_idx(t, f, Tn, GXh, tc, ntile)]);
+    batched_loop<3>(
+        GF, [&](int f) { return in[ttile_idx(t, f, Tn, GXh, tc, ntile)]; },
+        [&](int f, cpx<T> v) { lds_cpx_store(S.slice + Q::bin(f, G), 1, v); });
   } else {
     const cpx<T>* in = src + (slice * Tn + t) * GF;
-    for (int f = threadIdx.x; f < GF; f += kNT) lds_cpx_store(S.slice + Q::bin(f, G), 1, in[f]);
+    batched_loop<3>(
+        GF, [&](int f) { return in[f]; },
+        [&](int f, cpx<T> v) { lds_cpx_store(S.slice + Q::bin(f, G), 1, v); });
   }
   slice_c2r_rm<T, RM, true, kPlaneQP>(S.slice, G, S.tw);
   const int P = GX * GY;
   const int64_t off = (slice * Tn + t) * P;
   const bool nrm = (mode == 3 && norms) || (mode == 2 && slice < nfirst);
   T acc_d = 0, acc_n = 0;
-  for (int e = threadIdx.x; e < P; e += kNT) {
-    const int y = e / GX, x = e - y * GX;
-    const T v = S.slice[Q::px(x, y, G)] * scale;
-    if (nrm) {
-      const T o = dst[off + e];
-      acc_d += (v - o) * (v - o);
-      acc_n += v * v;
-    }
-    if (mode == 3) {
-      const T q = state[off + e];
-      const T an = v + fmax(-theta, fmin(q, theta));
-      state[off + e] = an;
-      if (wz) dst[off + e] = v;
-      if (nxt) S.slice[Q::px(x, y, G)] = fma((T)-2, fmax(-theta, fmin(an, theta)), an);
-    } else {
-      dst[off + e] = v;
-    }
-  }
+  // the old z / D (norms) and the state of a batch are loaded before any is used
+  batched_loop<3>(
+      P,
+      [&](int e) {
+        return Pair2<T>{nrm ? dst[off + e] : (T)0, mode == 3 ? state[off + e] : (T)0};
+      },
+      [&](int e, Pair2<T> oq) {
+        const int y = e / GX, x = e - y * GX;
+        const T v = S.slice[Q::px(x, y, G)] * scale;
+        if (nrm) {
+          acc_d += (v - oq.a) * (v - oq.a);
+          acc_n += v * v;
+        }
+        if (mode == 3) {
+          const T an = v + fmax(-theta, fmin(oq.b, theta));
+          state[off + e] = an;
+          if (wz) dst[off + e] = v;
+          if (nxt) S.slice[Q::px(x, y, G)] = fma((T)-2, fmax(-theta, fmin(an, theta)), an);
+        } else {
+          dst[off + e] = v;
+        }
+      });
   if (mode == 2) {
     const int s = 2 * r + 1;
     const int st3 = (t + r) % Tn;          // support plane index (L3:239-240 circshift)
