@@ -109,4 +109,31 @@ __device__ __forceinline__ T block_sum(T v, T* scratch) {
   return s;
 }
 
+// A block-strided loop (NT threads) over n elements whose global loads are issued B at a
+// time before any is used: one memory round trip per batch instead of per element.  As plain
+// `for (e = tid; e < n; e += NT)` loops the compiler waits vmcnt(0) for every iteration's own
+// load (the 3D plane kernels made 3 and 6 dependent HBM round trips per plane and thread, the
+// line passes of recon.hip ~10 per workgroup).  ld(e) loads, use(e, v) consumes.
+template <int B, int NT = kNT, typename Ld, typename Use>
+__device__ __forceinline__ void batched_loop(int n, Ld&& ld, Use&& use) {
+  using V = decltype(ld(0));
+  for (int base = threadIdx.x; base < n; base += B * NT) {
+    V v[B];
+#pragma unroll
+    for (int i = 0; i < B; ++i) {
+      const int e = base + i * NT;
+      if (e < n) v[i] = ld(e);
+    }
+#pragma unroll
+    for (int i = 0; i < B; ++i) {
+      const int e = base + i * NT;
+      if (e < n) use(e, v[i]);
+    }
+  }
+}
+template <typename T>
+struct Pair2 {
+  T a, b;
+};
+
 }  // namespace ccsc

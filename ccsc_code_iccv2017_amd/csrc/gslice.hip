@@ -73,21 +73,28 @@ __global__ __launch_bounds__(256) void k_gp_epilog(int mode, const T* __restrict
   const int64_t off = slice * P;
   const bool nrm = (mode == 3 && norms) || (mode == 2 && slice < nfirst);
   T acc_d = 0, acc_n = 0;
-  for (int e = threadIdx.x; e < P; e += 256) {
-    const T v = R[off + e] * scale;
-    if (nrm) {
-      const T o = dst[off + e];
-      acc_d += (v - o) * (v - o);
-      acc_n += v * v;
-    }
-    if (mode == 3) {
-      const T q = state[off + e];
-      state[off + e] = v + fmax(-theta, fmin(q, theta));
-      if (wz) dst[off + e] = v;
-    } else {
-      dst[off + e] = v;
-    }
-  }
+  struct In {
+    T r, o, q;
+  };
+  // four elements' loads in flight per thread (common.hpp batched_loop)
+  batched_loop<4, 256>(
+      P,
+      [&](int e) {
+        return In{R[off + e], nrm ? dst[off + e] : (T)0, mode == 3 ? state[off + e] : (T)0};
+      },
+      [&](int e, In in) {
+        const T v = in.r * scale;
+        if (nrm) {
+          acc_d += (v - in.o) * (v - in.o);
+          acc_n += v * v;
+        }
+        if (mode == 3) {
+          state[off + e] = v + fmax(-theta, fmin(in.q, theta));
+          if (wz) dst[off + e] = v;
+        } else {
+          dst[off + e] = v;
+        }
+      });
   if (mode == 2) {
     // support gather, [t][y][x] per slice (3D: the planes (t + r) mod Tn < s, L3:239-240)
     const int s = 2 * r + 1, sT = Tn > 1 ? s : 1;
@@ -215,21 +222,23 @@ __global__ __launch_bounds__(256) void k_gp_hs_epilog(int mode, const T* __restr
   const int64_t off = slice * P;
   const T* bs = b + slice * (int64_t)sbx * sby;
   T acc = 0;
-  for (int i = threadIdx.x; i < P; i += 256) {
-    const T val = R[off + i] * invP;
-    dst[off + i] = val;
-    if (mode == kHsV) {
-      const int y = i / X, x = i - y * X;
-      const T smv = sm[off + i];
-      if (DZ) DZ[off + i] = val + smv;
-      if (x >= r && x < r + sbx && y >= r && y < r + sby) {
-        const T d = (val + smv) - bs[(y - r) * sbx + (x - r)];
-        acc += d * d;
-      }
-    } else {
-      acc += fabs(val);
-    }
-  }
+  batched_loop<4, 256>(
+      P, [&](int i) { return Pair2<T>{R[off + i], mode == kHsV ? sm[off + i] : (T)0}; },
+      [&](int i, Pair2<T> rs) {
+        const T val = rs.a * invP;
+        dst[off + i] = val;
+        if (mode == kHsV) {
+          const int y = i / X, x = i - y * X;
+          const T smv = rs.b;
+          if (DZ) DZ[off + i] = val + smv;
+          if (x >= r && x < r + sbx && y >= r && y < r + sby) {
+            const T d = (val + smv) - bs[(y - r) * sbx + (x - r)];
+            acc += d * d;
+          }
+        } else {
+          acc += fabs(val);
+        }
+      });
   acc = wave_sum(acc);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
   __syncthreads();

@@ -117,12 +117,11 @@ __device__ __forceinline__ bool hs_inside(int x, int y, int r, int sbx, int sby)
 template <typename T>
 __device__ __forceinline__ void lds_from_spectrum(T* lds, const cpx<T>* __restrict__ in,
                                                   const Grid2D& G) {
-  for (int f = threadIdx.x; f < G.F; f += kNT) {
-    const cpx<T> c = in[f];
+  batched_loop<3>(G.F, [&](int f) { return in[f]; }, [&](int f, cpx<T> c) {
     const int o = bin_off(f, G);
     lds[o] = c.x;
     lds[o + 1] = c.y;
-  }
+  });
 }
 
 template <typename T>
@@ -154,17 +153,16 @@ __global__ __launch_bounds__(kNT) void k_hs_c2r_v(const cpx<T>* __restrict__ Ys,
   const int64_t off = s * P;
   const T* bs = b + s * (int64_t)sbx * sby;
   T acc = 0;
-  for (int e = threadIdx.x; e < P; e += kNT) {
+  batched_loop<3>(P, [&](int e) { return sm[off + e]; }, [&](int e, T smv) {
     const int y = e / G.X, x = e - y * G.X;
     const T val = S.slice[y * G.RS + x] * invP;
-    const T smv = sm[off + e];
     v[off + e] = val;
     if (DZ) DZ[off + e] = val + smv;
     if (hs_inside(x, y, r, sbx, sby)) {
       const T d = (val + smv) - bs[(y - r) * sbx + (x - r)];
       acc += d * d;
     }
-  }
+  });
   acc = block_sum(acc, S.red);
   if (threadIdx.x == 0) {
     part[2 * s] = acc;
@@ -189,19 +187,22 @@ __global__ __launch_bounds__(kNT) void k_hs_data_r2c(const T* __restrict__ v, T*
   const int P = G.X * G.Y;
   const int64_t off = s * P;
   const T* bs = b + s * (int64_t)sbx * sby;
-  for (int i = threadIdx.x; i < P; i += kNT) {
+  struct In {
+    T v, e, sm;
+  };
+  batched_loop<3>(P, [&](int i) { return In{v[off + i], e[off + i], sm[off + i]}; }, [&](int i, In ve) {
     const int y = i / G.X, x = i - y * G.X;
-    const T vv = v[off + i], ev = e[off + i];
+    const T vv = ve.v, ev = ve.e;
     T m = 0, mtb = 0;
     if (hs_inside(x, y, r, sbx, sby)) {
       m = (T)1;
-      mtb = bs[(y - r) * sbx + (x - r)] - sm[off + i];
+      mtb = bs[(y - r) * sbx + (x - r)] - ve.sm;
     }
     const T u = (mtb + invtheta * (vv - ev)) / (m + invtheta);
     const T en = ev - (vv - u);
     e[off + i] = en;
     S.slice[y * G.RS + x] = u + en;
-  }
+  });
   zero_pad_row(S.slice, G);
   slice_r2c<T, kMaxB>(S.slice, G, S.tw);
   lds_to_spectrum(S.slice, Xi + s * G.F, G);
@@ -221,16 +222,16 @@ __global__ __launch_bounds__(kNT) void k_hs_z_r2c(const T* __restrict__ z, T* __
   const int64_t s = blockIdx.x;
   const int P = G.X * G.Y;
   const int64_t off = s * P;
-  for (int i = threadIdx.x; i < P; i += kNT) {
+  batched_loop<3>(P, [&](int i) { return Pair2<T>{z[off + i], e[off + i]}; }, [&](int i, Pair2<T> ze) {
     const int y = i / G.X, x = i - y * G.X;
-    const T zv = z[off + i], ev = e[off + i];
+    const T zv = ze.a, ev = ze.b;
     const T a = zv - ev;
     const T aa = fabs(a);
     const T u = ((aa > theta) ? (T)1 - theta / aa : (T)0) * a;
     const T en = ev - (zv - u);
     e[off + i] = en;
     S.slice[y * G.RS + x] = u + en;
-  }
+  });
   zero_pad_row(S.slice, G);
   slice_r2c<T, kMaxB>(S.slice, G, S.tw);
   lds_to_spectrum(S.slice, Xi + s * G.F, G);

@@ -33,10 +33,10 @@ __global__ __launch_bounds__(kNT) void k_r2c_embed(const T* __restrict__ src, in
   if (!full)
     for (int e = threadIdx.x; e < G.Yp * G.RS; e += kNT) S.slice[e] = (T)0;
   __syncthreads();
-  for (int e = threadIdx.x; e < sx * sy; e += kNT) {
+  batched_loop<3>(sx * sy, [&](int e) { return in[e]; }, [&](int e, T v) {
     const int y = e / sx, x = e - y * sx;
-    S.slice[(y + oy) * G.RS + x + ox] = in[e];
-  }
+    S.slice[(y + oy) * G.RS + x + ox] = v;
+  });
   if (full) zero_pad_row(S.slice, G);
   slice_r2c<T, kMaxB>(S.slice, G, S.tw);
   cpx<T>* out = dst + (int64_t)blockIdx.x * dst_slice;
@@ -54,12 +54,11 @@ __global__ __launch_bounds__(kNT) void k_c2r_plain(const cpx<T>* __restrict__ sr
   Smem<T> S = carve<T>(smem, G);
   load_twiddles(S.tw, twg, G.ntw);
   const cpx<T>* in = src + (int64_t)blockIdx.x * src_slice;
-  for (int f = threadIdx.x; f < G.F; f += kNT) {
-    const cpx<T> v = in[f];
+  batched_loop<3>(G.F, [&](int f) { return in[f]; }, [&](int f, cpx<T> v) {
     const int o = bin_off(f, G);
     S.slice[o] = v.x;
     S.slice[o + 1] = v.y;
-  }
+  });
   slice_c2r<T, kMaxB>(S.slice, G, S.tw);
   T* out = dst + (int64_t)blockIdx.x * dst_slice;
   const int P = G.X * G.Y;
@@ -94,15 +93,17 @@ void k_dual_r2c(const T* __restrict__ D, T* __restrict__ yD,
   const int P = GX * GY;
   const int64_t off = (int64_t)slice * P;
   const T* u = Usup + (int64_t)g * s * s;
-  for (int e = threadIdx.x; e < P; e += kNT) {
-    const int y = e / GX, x = e - y * GX;
-    const int xr = x + r, yr = y + r;
-    const int sxx = xr >= GX ? xr - GX : xr, syy = yr >= GY ? yr - GY : yr;   // (x + r) mod X
-    const T uv = (sxx < s && syy < s) ? u[syy * s + sxx] : (T)0;
-    const T yv = yD[off + e] + D[off + e] - uv;
-    yD[off + e] = yv;
-    S.slice[Q::px(x, y, G)] = uv - yv;
-  }
+  batched_loop<3>(
+      P, [&](int e) { return Pair2<T>{yD[off + e], D[off + e]}; },
+      [&](int e, Pair2<T> yd) {
+        const int y = e / GX, x = e - y * GX;
+        const int xr = x + r, yr = y + r;
+        const int sxx = xr >= GX ? xr - GX : xr, syy = yr >= GY ? yr - GY : yr;   // (x + r) mod X
+        const T uv = (sxx < s && syy < s) ? u[syy * s + sxx] : (T)0;
+        const T yv = yd.a + yd.b - uv;
+        yD[off + e] = yv;
+        S.slice[Q::px(x, y, G)] = uv - yv;
+      });
   zero_pad_row(S.slice, G);
   slice_r2c_rm<T, RM>(S.slice, G, S.tw);
   cpx<T>* out = Ch + (int64_t)slice * GF;
@@ -130,27 +131,25 @@ void k_c2r_dout(const cpx<T>* __restrict__ Dh,
   if constexpr (!Q::fixed) load_twiddles(S.tw, twg, G.ntw);
   const int slice = blockIdx.x;
   const cpx<T>* in = Dh + (int64_t)slice * GF;
-  for (int f = threadIdx.x; f < GF; f += kNT) {
-    const cpx<T> v = in[f];
+  batched_loop<3>(GF, [&](int f) { return in[f]; }, [&](int f, cpx<T> v) {
     const int o = Q::bin(f, G);
     S.slice[o] = v.x;
     S.slice[o + 1] = v.y;
-  }
+  });
   slice_c2r_rm<T, RM>(S.slice, G, S.tw);
   const int P = GX * GY;
   const int64_t off = (int64_t)slice * P;
   const bool first = slice < nfirst;
   T acc_d = 0, acc_n = 0;
-  for (int e = threadIdx.x; e < P; e += kNT) {
+  batched_loop<3>(P, [&](int e) { return first ? D[off + e] : (T)0; }, [&](int e, T o) {
     const int y = e / GX, x = e - y * GX;
     const T v = S.slice[Q::px(x, y, G)] * invP;
     if (first) {
-      const T o = D[off + e];
       acc_d += (v - o) * (v - o);
       acc_n += v * v;
     }
     D[off + e] = v;
-  }
+  });
   const int s = 2 * r + 1;
   T* sp = supp + (int64_t)slice * s * s;
   for (int q = threadIdx.x; q < s * s; q += kNT) {

@@ -45,32 +45,6 @@ __device__ __forceinline__ int64_t plane_of_block(int64_t nplanes) {
 }
 __host__ inline unsigned plane_grid(int64_t nplanes) { return (unsigned)(((nplanes + 7) / 8) * 8); }
 
-// A kNT-strided loop over n elements whose global loads are issued B at a time before any is
-// used: one memory round trip per batch instead of per element.  (As plain loops, every
-// iteration waited vmcnt(0) for its own load: the plane kernels' spectrum and state loops made
-// 3 and 6 dependent HBM round trips per plane and thread -- the plane kernels' waves were
-// parked 67% of their lifetime, profiles/r06/c4_pmc.)  ld(e) loads, use(e, v) consumes.
-template <int B, typename Ld, typename Use>
-__device__ __forceinline__ void batched_loop(int n, Ld&& ld, Use&& use) {
-  using V = decltype(ld(0));
-  for (int base = threadIdx.x; base < n; base += B * kNT) {
-    V v[B];
-#pragma unroll
-    for (int i = 0; i < B; ++i) {
-      const int e = base + i * kNT;
-      if (e < n) v[i] = ld(e);
-    }
-#pragma unroll
-    for (int i = 0; i < B; ++i) {
-      const int e = base + i * kNT;
-      if (e < n) use(e, v[i]);
-    }
-  }
-}
-template <typename T>
-struct Pair2 {
-  T a, b;
-};
 
 template <typename T, int RM>
 __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(slice_waves<RM>())))

@@ -59,26 +59,33 @@ __device__ __forceinline__ void rows_body(const RowArgs<T>& a, const RowGeom& rg
   const int64_t sbase = (slice * rg.rows + row0) * (int64_t)Xh;    // spectra
   // twiddle tables in LDS (every pass reads them per butterfly)
   cpx<T>* s_tw = reinterpret_cast<cpx<T>*>(lds + rows_tw_off(rg));
-  for (int i = threadIdx.x; i < rg.ntw; i += kLineNT) s_tw[i] = tw[i];
+  batched_loop<4, kLineNT>(rg.ntw, [&](int i) { return tw[i]; }, [&](int i, cpx<T> v) { s_tw[i] = v; });
 
-  // ---- load ---------------------------------------------------------------
+  // ---- load (batched: every load of a batch in flight before the first LDS store) ----
   if (MODE == kRowFwd) {
-    for (int i = threadIdx.x; i < G.Yp * X; i += kLineNT) {
-      const int ry = i / X, x = i - ry * X;
-      lds[ry * RS + x] = ry < nrows ? a.src[rbase + (int64_t)ry * X + x] : (T)0;
-    }
+    batched_loop<4, kLineNT>(
+        G.Yp * X,
+        [&](int i) {
+          const int ry = i / X, x = i - ry * X;
+          return ry < nrows ? a.src[rbase + (int64_t)ry * X + x] : (T)0;
+        },
+        [&](int i, T v) {
+          const int ry = i / X, x = i - ry * X;
+          lds[ry * RS + x] = v;
+        });
   } else if (a.first) {
     for (int i = threadIdx.x; i < G.Yp * X; i += kLineNT) {
       const int ry = i / X, x = i - ry * X;
       lds[ry * RS + x] = (T)0;
     }
   } else {
-    for (int i = threadIdx.x; i < nrows * Xh; i += kLineNT) {
-      const int ry = i / Xh, xp = i - ry * Xh;
-      const cpx<T> c = a.S[sbase + (int64_t)ry * Xh + xp];
-      lds[ry * RS + 2 * xp] = c.x;
-      lds[ry * RS + 2 * xp + 1] = c.y;
-    }
+    batched_loop<4, kLineNT>(
+        nrows * Xh, [&](int i) { return a.S[sbase + i]; },
+        [&](int i, cpx<T> c) {
+          const int ry = i / Xh, xp = i - ry * Xh;
+          lds[ry * RS + 2 * xp] = c.x;
+          lds[ry * RS + 2 * xp + 1] = c.y;
+        });
     lds_sync();
     fft_dir<T, kMaxB, +1, kPlanSlots, kLineNT, kLineGT, kLineBS>(lds, kModeHermPair, gx, gx, G, G.px, s_tw);
   }
@@ -90,61 +97,75 @@ __device__ __forceinline__ void rows_body(const RowArgs<T>& a, const RowGeom& rg
     const bool act = !a.active || a.active[img] != 0;
     const T th = a.theta ? a.theta[img] : (T)0;
     const bool ident = a.prox == 1 && sl == 0;
-    for (int i = threadIdx.x; i < nrows * X; i += kLineNT) {
-      const int ry = i / X, x = i - ry * X;
-      const int64_t gi = rbase + (int64_t)ry * X + x;
-      const T z = lds[ry * RS + x];
-      const T zo = a.Z[gi];
-      const T dz = z - zo;
-      p0 += dz * dz;
-      p1 += z * z;
-      p2 += fabs(z);
-      if (act) a.Z[gi] = z;
-      if (MODE == kRowIterZ) {
-        const T d = a.D[gi];
-        const T av = z - d;                               // v2 - d2
-        const T u = ident ? av : soft_thr(av, th);        // SI:89, SP:84
-        const T dn = d - (z - u);                         // SI:93
-        a.D[gi] = dn;
-        lds[ry * RS + x] = u + dn;                        // xi2 (SI:96)
-      }
-    }
+    batched_loop<4, kLineNT>(
+        nrows * X,
+        [&](int i) {
+          const int64_t gi = rbase + i;   // (rows of X reals: gi = rbase + ry X + x)
+          return Pair2<T>{a.Z[gi], MODE == kRowIterZ ? a.D[gi] : (T)0};
+        },
+        [&](int i, Pair2<T> zd) {
+          const int ry = i / X, x = i - ry * X;
+          const int64_t gi = rbase + i;
+          const T z = lds[ry * RS + x];
+          const T dz = z - zd.a;
+          p0 += dz * dz;
+          p1 += z * z;
+          p2 += fabs(z);
+          if (act) a.Z[gi] = z;
+          if (MODE == kRowIterZ) {
+            const T d = zd.b;
+            const T av = z - d;                               // v2 - d2
+            const T u = ident ? av : soft_thr(av, th);        // SI:89, SP:84
+            const T dn = d - (z - u);                         // SI:93
+            a.D[gi] = dn;
+            lds[ry * RS + x] = u + dn;                        // xi2 (SI:96)
+          }
+        });
   } else if (MODE == kRowIterX) {
     const T th = a.theta[img];
     const T ith = (T)1 / th;
-    for (int i = threadIdx.x; i < nrows * X; i += kLineNT) {
-      const int ry = i / X, x = i - ry * X;
-      const int64_t gi = rbase + (int64_t)ry * X + x;
-      const T v = lds[ry * RS + x];
-      const T m = a.M[gi], mb = a.Mb[gi];
-      const T sm = a.SM ? a.SM[gi] : (T)0;
-      // objective residual mask .* crop(Dz) - mask .* b (SI:196; SD:144 and SV:171 with
-      // smoothinit); M is zero outside the image, so the whole grid is the crop
-      const T e = m * (v + (a.obj_sm ? sm : (T)0)) - mb;
-      p0 += e * e;
-      if (a.XO) {
-        const int row = row0 + ry;
-        const int y = row % a.Y;
-        if (x >= a.px0 && x < a.px1 && y >= a.py0 && y < a.py1) {
-          const T q = a.XO[gi] - (v + (a.psnr_sm ? sm : (T)0));   // SI:60
-          p1 += q * q;
-        }
-      }
-      const T d = a.D[gi];
-      const T w = v - d;
-      T u;
-      if (a.prox == 1) {   // Poisson where data is present, identity elsewhere (SP:193-205)
-        const T wt = w - th;
-        u = m != (T)0 ? (T)0.5 * (wt + sqrt(wt * wt + (T)4 * th * mb)) : w;
-      } else {             // (Mtb + w/th) / (MtM + 1/th), Mtb = M b - M smoothinit (SI:29,152)
-        const T mtb = mb - m * sm;
-        const T mtm = a.mtm_sq ? m * m : m;
-        u = (mtb + ith * w) / (mtm + ith);
-      }
-      const T dn = d - (v - u);
-      a.D[gi] = dn;
-      lds[ry * RS + x] = u + dn;                          // xi1
-    }
+    struct XIn {
+      T m, mb, sm, d;
+    };
+    batched_loop<2, kLineNT>(
+        nrows * X,
+        [&](int i) {
+          const int64_t gi = rbase + i;
+          return XIn{a.M[gi], a.Mb[gi], a.SM ? a.SM[gi] : (T)0, a.D[gi]};
+        },
+        [&](int i, XIn in) {
+          const int ry = i / X, x = i - ry * X;
+          const int64_t gi = rbase + (int64_t)ry * X + x;
+          const T v = lds[ry * RS + x];
+          const T m = in.m, mb = in.mb;
+          const T sm = in.sm;
+          // objective residual mask .* crop(Dz) - mask .* b (SI:196; SD:144 and SV:171 with
+          // smoothinit); M is zero outside the image, so the whole grid is the crop
+          const T e = m * (v + (a.obj_sm ? sm : (T)0)) - mb;
+          p0 += e * e;
+          if (a.XO) {
+            const int row = row0 + ry;
+            const int y = row % a.Y;
+            if (x >= a.px0 && x < a.px1 && y >= a.py0 && y < a.py1) {
+              const T q = a.XO[gi] - (v + (a.psnr_sm ? sm : (T)0));   // SI:60
+              p1 += q * q;
+            }
+          }
+          const T d = in.d;
+          const T w = v - d;
+          T u;
+          if (a.prox == 1) {   // Poisson where data is present, identity elsewhere (SP:193-205)
+            const T wt = w - th;
+            u = m != (T)0 ? (T)0.5 * (wt + sqrt(wt * wt + (T)4 * th * mb)) : w;
+          } else {             // (Mtb + w/th) / (MtM + 1/th), Mtb = M b - M smoothinit (SI:29,152)
+            const T mtb = mb - m * sm;
+            const T mtm = a.mtm_sq ? m * m : m;
+            u = (mtb + ith * w) / (mtm + ith);
+          }
+          const T dn = d - (v - u);
+          a.D[gi] = dn;
+          lds[ry * RS + x] = u + dn;                          // xi1
+        });
   } else if (MODE == kRowRes) {
     for (int i = threadIdx.x; i < nrows * X; i += kLineNT) {
       const int ry = i / X, x = i - ry * X;
@@ -242,14 +263,18 @@ __global__ __launch_bounds__(kLineNT) void k_cols(cpx<T>* __restrict__ S, cpx<T>
   const int nc = min(TC, cg.Xh - c0);
   cpx<T>* base = S + (o % cg.ninner) * cg.sin + (o / cg.ninner) * cg.sout + c0;
   cpx<T>* s_tw = reinterpret_cast<cpx<T>*>(lds + (size_t)2 * n * TC);
-  for (int i = threadIdx.x; i < cg.ntw; i += kLineNT) s_tw[i] = tw[i];
-  for (int i = threadIdx.x; i < n * TC; i += kLineNT) {
-    const int e = i / TC, c = i - e * TC;
-    cpx<T> v = {(T)0, (T)0};
-    if (c < nc) v = base[(int64_t)e * cg.es + c];
-    lds[2 * i] = v.x;
-    lds[2 * i + 1] = v.y;
-  }
+  batched_loop<4, kLineNT>(cg.ntw, [&](int i) { return tw[i]; }, [&](int i, cpx<T> v) { s_tw[i] = v; });
+  // the line set's columns, four loads in flight per thread before their LDS stores
+  batched_loop<4, kLineNT>(
+      n * TC,
+      [&](int i) {
+        const int e = i / TC, c = i - e * TC;
+        return c < nc ? base[(int64_t)e * cg.es + c] : cpx<T>{(T)0, (T)0};
+      },
+      [&](int i, cpx<T> v) {
+        lds[2 * i] = v.x;
+        lds[2 * i + 1] = v.y;
+      });
   const LineGeom g = {TC, 2, 2 * TC, 1};
   Grid2D Gd{};
   lds_sync();

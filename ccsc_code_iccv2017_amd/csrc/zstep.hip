@@ -38,35 +38,37 @@ void k_zstep_diag(T* __restrict__ z, T* __restrict__ as,
   const int64_t off = slice * P;
   theta = __builtin_canonicalize(theta);
   lds_sync();
-  for (int e = threadIdx.x; e < P; e += kNT) {
+  // (loads batched: common.hpp batched_loop)
+  batched_loop<3>(P, [&](int e) { return as[off + e]; }, [&](int e, T a) {
     const int y = e / GX, x = e - y * GX;
-    const T a = as[off + e];
     S.slice[Q::px(x, y, G)] = fma((T)-2, fmax(-theta, fmin(a, theta)), a);
-  }
+  });
   zero_pad_row(S.slice, G);
   slice_r2c_rm<T, RM>(S.slice, G, S.tw);
   const cpx<T>* Es = E + slice * F;
-  for (int f = threadIdx.x; f < F; f += kNT) {
+  struct ES {
+    cpx<T> e;
+    T sc;
+  };
+  batched_loop<3>(F, [&](int f) { return ES{Es[f], sden[f]}; }, [&](int f, ES es) {
     T* q = S.slice + Q::bin(f, G);
     const cpx<T> c = lds_cpx(q, 1);
-    const cpx<T> e = Es[f];
-    const T sc = sden[f];
-    lds_cpx_store(q, 1, cpx<T>{(e.x + rho * c.x) * sc, (e.y + rho * c.y) * sc});
-  }
+    lds_cpx_store(q, 1, cpx<T>{(es.e.x + rho * c.x) * es.sc, (es.e.y + rho * c.y) * es.sc});
+  });
   slice_c2r_rm<T, RM>(S.slice, G, S.tw);
   T nd = 0, nz = 0;
-  for (int e = threadIdx.x; e < P; e += kNT) {
-    const int y = e / GX, x = e - y * GX;
-    const T zn = S.slice[Q::px(x, y, G)];
-    if (TOL) {
-      const T zo = z[off + e];
-      nd += (zn - zo) * (zn - zo);
-      nz += zn * zn;
-    }
-    const T a = as[off + e];
-    as[off + e] = zn + fmax(-theta, fmin(a, theta));
-    if (WZ) z[off + e] = zn;
-  }
+  batched_loop<3>(
+      P, [&](int e) { return Pair2<T>{TOL ? z[off + e] : (T)0, as[off + e]}; },
+      [&](int e, Pair2<T> za) {
+        const int y = e / GX, x = e - y * GX;
+        const T zn = S.slice[Q::px(x, y, G)];
+        if (TOL) {
+          nd += (zn - za.a) * (zn - za.a);
+          nz += zn * zn;
+        }
+        as[off + e] = zn + fmax(-theta, fmin(za.b, theta));
+        if (WZ) z[off + e] = zn;
+      });
   if (TOL) {
     nd = block_sum(nd, S.red);
     nz = block_sum(nz, S.red);
