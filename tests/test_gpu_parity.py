@@ -582,14 +582,23 @@ def test_dfactor_woodbury_rejected_when_blocks_too_large(gpu_ctx):
     assert ei.value.code == L.CCSC_E_UNSUPPORTED
 
 
-def test_k_above_the_factor_budget_rejected(gpu_ctx):
-    """K <= 400 runs (K > 192: gramchol_big.hip); larger K is a clean CCSC_E_UNSUPPORTED."""
+def test_k_above_400_runs_woodbury_and_ni_above_100_is_rejected(gpu_ctx):
+    """K > 400 runs on the Woodbury factor (wbig.hip; ni = 1 here) and matches the oracle; a
+    block of more than 100 patches past K = 400 is a clean CCSC_E_UNSUPPORTED."""
     from ccsc_code_iccv2017_amd import _lib as L
     from ccsc_code_iccv2017_amd import learners as E
     b, d0, z0 = _case("dz", (6, 6), 3, 401, 2, 1, seed=4)
+    init = {"d": d0, "z": z0}
+    d_e, z_e, DZ_e, _ = E.admm_learn_conv2D_large_dzParallel(b, [3, 3, 401], 1.0, 1.0, 1, 0.0,
+                                                             "none", init, ni=1, ctx=gpu_ctx)
+    d_o, z_o, DZ_o, _, _ = O.learn_2d_dzparallel(b, [3, 3, 401], 1.0, 1.0, 1, 0.0, "none", init,
+                                                 ni=1)
+    assert _rel(d_e, d_o) < 1e-7
+    assert _rel(z_e, z_o) < 1e-7
+    b2, d2, z2 = _case("dz", (6, 6), 3, 401, 202, 101, seed=4)
     with pytest.raises(L.CCSCError) as ei:
-        E.admm_learn_conv2D_large_dzParallel(b, [3, 3, 401], 1.0, 1.0, 1, 0.0, "none",
-                                             {"d": d0, "z": z0}, ni=1, ctx=gpu_ctx)
+        E.admm_learn_conv2D_large_dzParallel(b2, [3, 3, 401], 1.0, 1.0, 1, 0.0, "none",
+                                             {"d": d2, "z": z2}, ni=101, ctx=gpu_ctx)
     assert ei.value.code == L.CCSC_E_UNSUPPORTED
 
 
