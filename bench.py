@@ -162,6 +162,12 @@ def sq_limits(k):
         "wave_parked": k["SQ_WAIT_ANY"] / wc,
         "wave_issue_stalled": k["SQ_WAIT_INST_ANY"] / wc,
         "valu_insts_per_wave": k.get("SQ_INSTS_VALU", float("nan")) / max(k.get("SQ_WAVES", 1), 1),
+        # LDS bank-conflict cycles per LDS issue cycle, and the LDS share with them counted
+        # (lds_busy counts issue only)
+        "lds_conflict_per_issue": (k["SQ_LDS_BANK_CONFLICT"] / k["SQ_ACTIVE_INST_LDS"]
+                                   if "SQ_LDS_BANK_CONFLICT" in k and k["SQ_ACTIVE_INST_LDS"] else None),
+        "lds_busy_incl_conflicts": (4.0 * (k["SQ_ACTIVE_INST_LDS"] + k["SQ_LDS_BANK_CONFLICT"]) / simd_cycles
+                                    if "SQ_LDS_BANK_CONFLICT" in k else None),
     }
 
 
