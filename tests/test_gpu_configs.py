@@ -198,15 +198,17 @@ def test_c3_fullsize_20_iterations(gpu_ctx):
     assert np.all(np.abs(norms - 1) < 1e-4), (norms.min(), norms.max())
 
 
-def test_c4_reduced_norm_offset_matches_oracle(gpu_ctx):
-    """The norm offset of C4's d_res is the algorithm's own: on a C4-shaped problem at
-    1/9 the size (K = 49 11^3 filters, 24x24x12 synthetic clips, n = 16 -> ni = 4,
-    Woodbury), 20 outer iterations, the engine reproduces the float64 oracle's per-filter
-    norms of d_res = crop(D{1}) (tests/golden/c4_reduced_norms.json, tools/norm_offset.py:
-    1.000000 .. 1.000162, with the projected consensus u at exactly 1)."""
+@pytest.mark.parametrize("fixture", ["c4_reduced_norms.json", "c4_third_norms.json"])
+def test_c4_reduced_norm_offset_matches_oracle(gpu_ctx, fixture):
+    """The norm offset of C4's d_res is the algorithm's own: on C4-shaped problems (K = 49
+    11^3 filters, n = 16 synthetic clips -> ni = 4, Woodbury) of 24x24x12 (1/19 of a C4 clip's
+    volume) and 44x44x22 (1/3), 20 outer iterations, the engine reproduces the float64
+    oracle's per-filter norms of d_res = crop(D{1}) (tests/golden/c4_*_norms.json,
+    tools/norm_offset.py: 1.000000 .. 1.000162 and 1.000001 .. 1.000036, the projected
+    consensus u at exactly 1; profiles/r04/norm_offset_c4.txt, profiles/r06/norm_offset_c4_third.txt)."""
     from ccsc_code_iccv2017_amd import learners as E
     from ccsc_code_iccv2017_amd import synth
-    g = json.load(open(os.path.join(GOLD, "c4_reduced_norms.json")))
+    g = json.load(open(os.path.join(GOLD, fixture)))
     sb, K, n, psf, iters = tuple(g["sb"]), g["K"], g["n"], g["psf"], g["iters"]
     b = synth.clips_3d(n, sb, K=K, psf=psf, device="cpu")
     r = psf // 2
@@ -218,7 +220,7 @@ def test_c4_reduced_norm_offset_matches_oracle(gpu_ctx):
     norms = np.sqrt((d_e ** 2).sum(axis=(0, 1, 2)))
     print(f"C4-shaped engine norms {norms.min():.6f} .. {norms.max():.6f}")
     np.testing.assert_allclose(norms, np.array(g["d_res_norms"]), rtol=1e-8)
-    assert norms.max() > 1.0 + 1e-4   # the outward drift, not round-off
+    assert norms.max() > 1.0 + 1e-5   # the outward drift, not round-off
 
 
 def test_c3_reduced_norms_match_oracle(gpu_ctx):
