@@ -12,11 +12,11 @@ tag=${1:-r03}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 out=gpurun_out/$tag
 mkdir -p $out
-B="python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-configs"
+B="python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-configs --no-shard-diag"
 if [ "$2" != "nobench" ]; then
   timeout -k 10 600 python3 bench.py > $out/bench.json 2> $out/bench.err || exit $?
 fi
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d $out/trace -o trace -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-configs > $out/trace.log 2>&1 || exit $?
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d $out/trace -o trace -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-configs --no-shard-diag > $out/trace.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -f csv -d $out/fetch -o fetch -- $B > $out/fetch.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -f csv -d $out/write -o write -- $B > $out/write.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE -f csv -d $out/sq -o sq -- $B > $out/sq.log 2>&1 || exit $?
