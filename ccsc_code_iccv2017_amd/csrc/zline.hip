@@ -154,7 +154,8 @@ __device__ __forceinline__ void wave_lds_fence() {
 // the slot's constant part folds into the instruction's offset field).
 // Idle lanes (lane 10 of a line in layout A, lanes 55..63, the clamped lines of the
 // last wave) run on clamped indices and so duplicate a real lane exactly: their
-// LDS and global stores write the same value to the same address, no guards.
+// LDS and global stores write the same value to the same address, no guards
+// (k_zline masks lanes 55..63 and the clamped lines out of its phases).
 // The outputs stream to sink(k1, value) as the last stage forms them.
 // ODDROT: the inputs of the lanes n1 odd arrive divided by -i (the y-R2C's two-for-one
 // separation of the odd rows, see P7): in layout B they are register n1 (compile time),
@@ -399,6 +400,12 @@ __global__ __launch_bounds__(zl::NT) __attribute__((amdgpu_waves_per_eu(3, 3))) 
     const int sb = min(s, 10), sa = min(s, 9);
     const int c = min(5 * wave + l, 55);   // y-line (column)
     const int j = min(5 * wave + l, 54);   // x-line (row pair)
+    // lanes that duplicate another lane's work (55..63: line 4, k2 = 10; lines 1..4 of the last
+    // wave: column 55 again) sit the phases out -- their stores only repeated a real lane's, and
+    // the kernel is power-limited: 5.886 -> 5.817 ms at n = 1000
+    // (profiles/r06/zline_lane_mask_ab.txt)
+    const bool xlive = lane < 55;
+    const bool ylive = lane < 55 && (__builtin_amdgcn_readfirstlane(wave) < zl::NW - 1 || lane < 11);
     const int64_t sl = (p * K + k) * zl::P;
     cpx<T> zc[11];   // c = u - y of the row pair (x-lines, layout A) for the R2C
     const uint32_t po = (uint32_t)(j * 10 + fresh(sa)) * 16u;   // pair n2 at po + n2*550*16
@@ -411,40 +418,42 @@ __global__ __launch_bounds__(zl::NT) __attribute__((amdgpu_waves_per_eu(3, 3))) 
     auto yw = [&](int n1) { return (n1 < 5 ? ywE : ywO) + (uint32_t)zr::A(n1 % 5) * 16u; };
     auto yr = [&](int k2) { return yX + (uint32_t)k2 * kPSB; };
     if constexpr (MODE >= 2) {
-      // ---- P1: y-C2R of conj(dcorr_k) w from bins to column c of every region ----
-      const cpx<T>* dk = dcorr + (int64_t)k * zl::F;
-      const uint32_t bo = (uint32_t)(c * 11 + sb) * 16u;
-      const bool wl = __builtin_amdgcn_readfirstlane(wave) < kZlWL;
-      // every operand load first, then the products (sched_barrier): interleaved, the
-      // scheduler waits for each load pair in turn -- ten L2 round trips per wave
-      cpx<T> b[10], wv[10];
-      if (wl) {
+      if (ylive) {
+        // ---- P1: y-C2R of conj(dcorr_k) w from bins to column c of every region ----
+        const cpx<T>* dk = dcorr + (int64_t)k * zl::F;
+        const uint32_t bo = (uint32_t)(c * 11 + sb) * 16u;
+        const bool wl = __builtin_amdgcn_readfirstlane(wave) < kZlWL;
+        // every operand load first, then the products (sched_barrier): interleaved, the
+        // scheduler waits for each load pair in turn -- ten L2 round trips per wave
+        cpx<T> b[10], wv[10];
+        if (wl) {
 #pragma unroll
-        for (int i = 0; i < 10; ++i) {
-          const int k1 = kOrd10in[i];
-          b[k1] = fld<cpx<T>>(dk, bo, k1 * 616 * 16);
-          wv[k1] = sW[k1 * 385 + c * 11 + sb];
-        }
-      } else {
+          for (int i = 0; i < 10; ++i) {
+            const int k1 = kOrd10in[i];
+            b[k1] = fld<cpx<T>>(dk, bo, k1 * 616 * 16);
+            wv[k1] = sW[k1 * 385 + c * 11 + sb];
+          }
+        } else {
 #pragma unroll
-        for (int i = 0; i < 10; ++i) {
-          const int k1 = kOrd10in[i];
-          b[k1] = fld<cpx<T>>(dk, bo, k1 * 616 * 16);
-          wv[k1] = wld<cpx<T>>(Wp, bo, k1 * 616 * 16);
+          for (int i = 0; i < 10; ++i) {
+            const int k1 = kOrd10in[i];
+            b[k1] = fld<cpx<T>>(dk, bo, k1 * 616 * 16);
+            wv[k1] = wld<cpx<T>>(Wp, bo, k1 * 616 * 16);
+          }
         }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < 10; ++i) b[kOrd10in[i]] = cmulc(b[kOrd10in[i]], wv[kOrd10in[i]]);
+        // row (11 n1 + 10 n2) mod 110 of lane n1 = sa: region (sa >> 1, n2 + (sa & 1)), its
+        // column slot ze (even rows) / zo (odd rows); the odd lanes wrap at n2 = 10
+        const uint32_t ys = (uint32_t)(zr::A(sa >> 1) + ((sa & 1) ? zr::PS + yzO : yzE)) * 16u;
+        const uint32_t ys10 = ys - ((sa & 1) ? 11u * kPSB : 0u);
+        inv_line_r<T>(b, yw, yr, [&](int n2, cpx<T> val) {
+          lds_cpx_at<T>((n2 == 10 ? ys10 : ys) + (uint32_t)n2 * kPSB) = val;
+        });
       }
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int i = 0; i < 10; ++i) b[kOrd10in[i]] = cmulc(b[kOrd10in[i]], wv[kOrd10in[i]]);
-      // row (11 n1 + 10 n2) mod 110 of lane n1 = sa: region (sa >> 1, n2 + (sa & 1)), its
-      // column slot ze (even rows) / zo (odd rows); the odd lanes wrap at n2 = 10
-      const uint32_t ys = (uint32_t)(zr::A(sa >> 1) + ((sa & 1) ? zr::PS + yzO : yzE)) * 16u;
-      const uint32_t ys10 = ys - ((sa & 1) ? 11u * kPSB : 0u);
-      inv_line_r<T>(b, yw, yr, [&](int n2, cpx<T> val) {
-        lds_cpx_at<T>((n2 == 10 ? ys10 : ys) + (uint32_t)n2 * kPSB) = val;
-      });
       zl_sync();   // P2
-      if (xwave) {
+      if (xwave && xlive) {
         // ---- P3: x-C2R of row pair j from its region: Z(x) = H_2j(x) + i H_2j+1(x) ----
         const int s3 = fresh(sb);
         const int R = zr::region(j);
@@ -518,7 +527,7 @@ __global__ __launch_bounds__(zl::NT) __attribute__((amdgpu_waves_per_eu(3, 3))) 
     } else {
       // ---- P4 (mode 0): a = z + y from the materialised natural layout ----
       V2 av0[11];
-      if (xwave) {
+      if (xwave && xlive) {
         const T* z0 = Zn + sl + 2 * j * zl::X;
         const T* y0 = Yn + sl + 2 * j * zl::X;
 #pragma unroll
@@ -535,7 +544,7 @@ __global__ __launch_bounds__(zl::NT) __attribute__((amdgpu_waves_per_eu(3, 3))) 
       }
       V2 zv[kStore ? 11 : 1];
       if constexpr (kStore) {
-        if (xwave) {
+        if (xwave && xlive) {
           const T* z0 = Zn + sl + 2 * j * zl::X;
 #pragma unroll
           for (int n2 = 0; n2 < 11; ++n2) {
@@ -546,7 +555,7 @@ __global__ __launch_bounds__(zl::NT) __attribute__((amdgpu_waves_per_eu(3, 3))) 
         }
       }
       __syncthreads();   // the slice is read in natural order before it is rewritten in state order
-      if (xwave) {
+      if (xwave && xlive) {
 #pragma unroll
         for (int n2 = 0; n2 < 11; ++n2) {
           zst<V2>(Ao + sl, po + n2 * 550 * 16, av0[n2]);
@@ -559,7 +568,7 @@ __global__ __launch_bounds__(zl::NT) __attribute__((amdgpu_waves_per_eu(3, 3))) 
       continue;
     }
     // ---- P5: x-R2C of the row pair -> Z_j(x) at slot zslot(x) of its region ----
-    if (xwave) {
+    if (xwave && xlive) {
       const int R = zr::region(j);
       const uint32_t xa = (uint32_t)(R + fresh(sb)) * 16u;
       const uint32_t xn = (uint32_t)(R + zr::TAU(fresh(sa))) * 16u;
@@ -571,40 +580,42 @@ __global__ __launch_bounds__(zl::NT) __attribute__((amdgpu_waves_per_eu(3, 3))) 
     zl_sync();   // P6
     // ---- P7: column c, rows y = (11 n1 + 10 n2) mod 110: two-for-one separation of
     // Z_j(c), Z_j(110 - c) of pair y >> 1 (region (n1 >> 1, n2 + (n1 & 1))) ----
-    cpx<T> col[11];
-    {
-      const int n1 = fresh(sa);
-      const T sg = (n1 & 1) ? (T)-1 : (T)1;
-      const uint32_t rb = (uint32_t)(zr::A(n1 >> 1) + (n1 & 1) * zr::PS) * 16u;
-      const uint32_t rb10 = rb - ((n1 & 1) ? 11u * kPSB : 0u);
-      const uint32_t a1 = (uint32_t)zr::ze(c) * 16u, a2 = (uint32_t)zr::zm(c) * 16u;
-      // even rows z1 + conj z2, odd rows z1 - conj z2 -- twice the row spectra (the 1/2 is
-      // applied once to the patch's accumulated bins), the odd rows' times i (the -i is
-      // applied in P9's DFT-10, where the odd rows are compile-time registers -- ODDROT)
-      cpx<T> z1[11], z2[11];
+    if (ylive) {
+      cpx<T> col[11];
+      {
+        const int n1 = fresh(sa);
+        const T sg = (n1 & 1) ? (T)-1 : (T)1;
+        const uint32_t rb = (uint32_t)(zr::A(n1 >> 1) + (n1 & 1) * zr::PS) * 16u;
+        const uint32_t rb10 = rb - ((n1 & 1) ? 11u * kPSB : 0u);
+        const uint32_t a1 = (uint32_t)zr::ze(c) * 16u, a2 = (uint32_t)zr::zm(c) * 16u;
+        // even rows z1 + conj z2, odd rows z1 - conj z2 -- twice the row spectra (the 1/2 is
+        // applied once to the patch's accumulated bins), the odd rows' times i (the -i is
+        // applied in P9's DFT-10, where the odd rows are compile-time registers -- ODDROT)
+        cpx<T> z1[11], z2[11];
 #pragma unroll
-      for (int i = 0; i < 11; ++i) {
-        const int n2 = kOrd11[i];
-        const uint32_t r = (n2 == 10 ? rb10 : rb) + (uint32_t)n2 * kPSB;
-        z1[n2] = lds_cpx_at<T>(r + a1);
-        z2[n2] = lds_cpx_at<T>(r + a2);
-      }
-      __builtin_amdgcn_sched_barrier(0);
+        for (int i = 0; i < 11; ++i) {
+          const int n2 = kOrd11[i];
+          const uint32_t r = (n2 == 10 ? rb10 : rb) + (uint32_t)n2 * kPSB;
+          z1[n2] = lds_cpx_at<T>(r + a1);
+          z2[n2] = lds_cpx_at<T>(r + a2);
+        }
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int i = 0; i < 11; ++i) {
-        const int n2 = kOrd11[i];
-        col[n2] = {fma(sg, z2[n2].x, z1[n2].x), fma(-sg, z2[n2].y, z1[n2].y)};
+        for (int i = 0; i < 11; ++i) {
+          const int n2 = kOrd11[i];
+          col[n2] = {fma(sg, z2[n2].x, z1[n2].x), fma(-sg, z2[n2].y, z1[n2].y)};
+        }
       }
-    }
-    // no barrier: P9's exchange reuses the slots this line alone just read
-    // ---- P9: y-R2C of column c -> bins, accumulate sum_k dhat_k C_k ----
-    {
-      const int s9 = fresh(sb);
-      const cpx<T>* dk = dhat + (int64_t)k * zl::F;
-      const uint32_t bo = (uint32_t)(c * 11 + s9) * 16u;
-      fwd_line_r<T, true>(col, yr, yw, [&](int k1, cpx<T> cb) {
-        acc[k1] = cmac(acc[k1], fld<cpx<T>>(dk, bo, k1 * 616 * 16), cb);
-      });
+      // no barrier: P9's exchange reuses the slots this line alone just read
+      // ---- P9: y-R2C of column c -> bins, accumulate sum_k dhat_k C_k ----
+      {
+        const int s9 = fresh(sb);
+        const cpx<T>* dk = dhat + (int64_t)k * zl::F;
+        const uint32_t bo = (uint32_t)(c * 11 + s9) * 16u;
+        fwd_line_r<T, true>(col, yr, yw, [&](int k1, cpx<T> cb) {
+          acc[k1] = cmac(acc[k1], fld<cpx<T>>(dk, bo, k1 * 616 * 16), cb);
+        });
+      }
     }
   }
   // w = (B - acc) * sden  (sden = 1/((rho + s) X Y)); each lane owns its slots
@@ -703,7 +714,9 @@ __global__ __launch_bounds__(zl::NT) void k_zhat_line(const T* __restrict__ A,
     const uint32_t Ey = (uint32_t)tcol(c) * 16u;
     const uint32_t Ex = (uint32_t)(10 * min(wave, 10) * zl::RS + l * 110) * 16u;
     const int64_t sl = (p * K + k) * zl::P;
-    if (xwave) {
+    // the duplicate lanes sit out, as in k_zline
+    const bool ylive = lane < 55 && (__builtin_amdgcn_readfirstlane(wave) < zl::NW - 1 || lane < 11);
+    if (xwave && lane < 55) {
       // ---- P4/P5: c = u - y of row pair j (layout A) -> x-R2C -> rows 2j, 2j+1 of T ----
       const uint32_t po = (uint32_t)(j * 10 + fresh(sa)) * 16u;
       cpx<T> zc[11];
@@ -719,7 +732,7 @@ __global__ __launch_bounds__(zl::NT) void k_zhat_line(const T* __restrict__ A,
     lds_sync();
     // ---- P7: column c, rows y = n1 + 10 n2: two-for-one separation ----
     cpx<T> col[11];
-    {
+    if (ylive) {
       const int n1 = fresh(sa);
       const int zc1 = zslot(c), zc2 = zslot((c == 0) ? 0 : zl::X - c);
       // twice the row spectra (halved at the store); odd rows times i (undone in P9, ODDROT)
@@ -735,7 +748,7 @@ __global__ __launch_bounds__(zl::NT) void k_zhat_line(const T* __restrict__ A,
     }
     lds_sync();
     // ---- P9: y-R2C of column c -> bins (x' = c, y = elem_b(k2, k1)) + XY conj(dcorr) w ----
-    {
+    if (ylive) {
       const int s9 = fresh(sb);
       const cpx<T>* dk = dcorr + (int64_t)k * zl::F;
       const uint32_t bo = (uint32_t)(c * 11 + s9) * 16u;

@@ -53,6 +53,8 @@ def c4(n=16, sb=(24, 24, 12), K=49, psf=11, iters=20):
             "b": "synth.clips_3d(n, sb, K=K, psf=psf, device='cpu')",
             "init": "numpy default_rng(44): d ~ randn(psf^3, K), then z ~ randn(sp + [K, n])",
             "d_res_norms": np.sqrt((d_res ** 2).sum(axis=(0, 1, 2))).tolist(),
+            "d1_norms_per_outer": [np.sqrt((O.crop_filters(D1, 3, r) ** 2).sum(axis=(0, 1, 2))).tolist()
+                                   for D1 in tr["D1"]],
             "u_norms_last": np.sqrt((O.crop_filters(tr["U"][-1], 3, r) ** 2).sum(axis=(0, 1, 2))).tolist()}
 
 
@@ -84,11 +86,12 @@ if __name__ == "__main__":
     ap.add_argument("--json", help="write the results (a test fixture) here")
     ap.add_argument("--sb", help="C4 clip size, e.g. 44,44,22 (default 24,24,12)")
     ap.add_argument("--n", type=int, default=16, help="C4 clips (a perfect square)")
+    ap.add_argument("--iters", type=int, default=20, help="C4 outer iterations")
     a = ap.parse_args()
     res = []
     if a.c4 or not a.c3:
         sb = tuple(int(x) for x in a.sb.split(",")) if a.sb else (24, 24, 12)
-        res.append(c4(n=a.n, sb=sb))
+        res.append(c4(n=a.n, sb=sb, iters=a.iters))
     if a.c3 or not a.c4:
         res.append(c3())
     if a.json:
