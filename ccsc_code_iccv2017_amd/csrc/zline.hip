@@ -714,9 +714,9 @@ __global__ __launch_bounds__(zl::NT) void k_zhat_line(const T* __restrict__ A,
     const uint32_t Ey = (uint32_t)tcol(c) * 16u;
     const uint32_t Ex = (uint32_t)(10 * min(wave, 10) * zl::RS + l * 110) * 16u;
     const int64_t sl = (p * K + k) * zl::P;
-    // the duplicate lanes sit out, as in k_zline
-    const bool ylive = lane < 55 && (__builtin_amdgcn_readfirstlane(wave) < zl::NW - 1 || lane < 11);
-    if (xwave && lane < 55) {
+    // (masking the duplicate lanes out, as k_zline does, slowed this kernel beside the Gram:
+    // 808.0 vs 790.8 ms per C2 step, profiles/r06/zline_lane_mask_ab.txt)
+    if (xwave) {
       // ---- P4/P5: c = u - y of row pair j (layout A) -> x-R2C -> rows 2j, 2j+1 of T ----
       const uint32_t po = (uint32_t)(j * 10 + fresh(sa)) * 16u;
       cpx<T> zc[11];
@@ -732,7 +732,7 @@ __global__ __launch_bounds__(zl::NT) void k_zhat_line(const T* __restrict__ A,
     lds_sync();
     // ---- P7: column c, rows y = n1 + 10 n2: two-for-one separation ----
     cpx<T> col[11];
-    if (ylive) {
+    {
       const int n1 = fresh(sa);
       const int zc1 = zslot(c), zc2 = zslot((c == 0) ? 0 : zl::X - c);
       // twice the row spectra (halved at the store); odd rows times i (undone in P9, ODDROT)
@@ -748,7 +748,7 @@ __global__ __launch_bounds__(zl::NT) void k_zhat_line(const T* __restrict__ A,
     }
     lds_sync();
     // ---- P9: y-R2C of column c -> bins (x' = c, y = elem_b(k2, k1)) + XY conj(dcorr) w ----
-    if (ylive) {
+    {
       const int s9 = fresh(sb);
       const cpx<T>* dk = dcorr + (int64_t)k * zl::F;
       const uint32_t bo = (uint32_t)(c * 11 + s9) * 16u;
