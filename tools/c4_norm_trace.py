@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Engine per-filter norms of d_res = crop(D{1}) on a C4-shaped problem after 1, 2, 3, ...
 outer iterations (each a fresh run from the same init, or from one perturbed at relative size
-$C4_TRACE_EPS), beside the oracle's trace from
+$C4_TRACE_EPS; the engine's norms to $C4_TRACE_JSON), beside the oracle's trace from
 tools/norm_offset.py --json (its d1_norms_per_outer): where the two part, and how fast.
   python tools/c4_norm_trace.py <oracle.json> [iters ...] > gpurun_out/c4trace.txt   (GPU)
 """
@@ -24,6 +24,7 @@ def main():
     b = synth.clips_3d(n, sb, K=K, psf=psf, device="cpu")
     r = psf // 2
     sp = [s + 2 * r for s in sb]
+    dump = {}
     for it in its:
         rng = np.random.default_rng(44)
         init = {"d": rng.standard_normal((psf,) * 3 + (K,)), "z": rng.standard_normal(sp + [K, n])}
@@ -38,6 +39,9 @@ def main():
             rel = np.abs(e - o) / o
             line += f"   oracle {o.min():.9f} .. {o.max():.9f}   max rel diff {rel.max():.3e}"
         print(line, flush=True)
+        dump[it] = e.tolist()
+    if os.environ.get("C4_TRACE_JSON"):
+        json.dump(dump, open(os.environ["C4_TRACE_JSON"], "w"))
 
 
 if __name__ == "__main__":
