@@ -203,7 +203,8 @@ def test_c4_reduced_norm_offset_matches_oracle(gpu_ctx, fixture):
     """The norm offset of C4's d_res is the algorithm's own: on C4-shaped problems (K = 49
     11^3 filters, n = 16 synthetic clips -> ni = 4, Woodbury) of 24x24x12 (1/19 of a C4 clip's
     volume) and 44x44x22 (1/3), 20 outer iterations, the engine reproduces the float64
-    oracle's per-filter norms of d_res = crop(D{1}) (tests/golden/c4_*_norms.json,
+    oracle's per-filter norms of d_res = crop(D{1}) (the 1/3 case exactly at 8 iterations and as a
+    band at 20, see pin_note; tests/golden/c4_*_norms.json,
     tools/norm_offset.py: 1.000000 .. 1.000162 and 1.000001 .. 1.000036, the projected
     consensus u at exactly 1; profiles/r04/norm_offset_c4.txt, profiles/r06/norm_offset_c4_third.txt)."""
     from ccsc_code_iccv2017_amd import learners as E
@@ -213,13 +214,24 @@ def test_c4_reduced_norm_offset_matches_oracle(gpu_ctx, fixture):
     b = synth.clips_3d(n, sb, K=K, psf=psf, device="cpu")
     r = psf // 2
     sp = [s + 2 * r for s in sb]
-    rng = np.random.default_rng(44)
-    init = {"d": rng.standard_normal((psf,) * 3 + (K,)), "z": rng.standard_normal(sp + [K, n])}
-    d_e, *_ = E.admm_learn_conv3D_large(b, [psf] * 3 + [K], 1.0, 1.0, iters, 0.0, "none", init,
-                                       ctx=gpu_ctx)
-    norms = np.sqrt((d_e ** 2).sum(axis=(0, 1, 2)))
+
+    def run(it):
+        rng = np.random.default_rng(44)
+        init = {"d": rng.standard_normal((psf,) * 3 + (K,)), "z": rng.standard_normal(sp + [K, n])}
+        d_e, *_ = E.admm_learn_conv3D_large(b, [psf] * 3 + [K], 1.0, 1.0, it, 0.0, "none", init,
+                                           ctx=gpu_ctx)
+        return np.sqrt((d_e ** 2).sum(axis=(0, 1, 2)))
+
+    norms = run(iters)
     print(f"C4-shaped engine norms {norms.min():.6f} .. {norms.max():.6f}")
-    np.testing.assert_allclose(norms, np.array(g["d_res_norms"]), rtol=1e-8)
+    if "pin_iters" in g:
+        # the 1/3-volume problem amplifies rounding-level differences ~10^2-10^3x per outer
+        # iteration past iteration 8 (g["pin_note"], profiles/r06/c4_third_divergence.txt):
+        # pinned where both are still exact, the 20-iteration norms compared as a band
+        np.testing.assert_allclose(run(g["pin_iters"]), np.array(g["pin_norms"]), rtol=1e-10)
+        np.testing.assert_allclose(norms, np.array(g["d_res_norms"]), rtol=0, atol=1e-4)
+    else:
+        np.testing.assert_allclose(norms, np.array(g["d_res_norms"]), rtol=1e-8)
     assert norms.max() > 1.0 + 1e-5   # the outward drift, not round-off
 
 
